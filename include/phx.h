@@ -1,0 +1,160 @@
+/*
+ * phx.h — C ABI of libphx.so, the MI355X-native (gfx950) adversarial-patch optimisation step.
+ *
+ * This is the drop-in boundary for the inner step of tiiuae/MLAdversarialObjectDetection's
+ * attacker_train.py.  Each entry point replaces one reference interface; the reference
+ * file:line it stands in for is given next to it (paths relative to the reference root).
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Device pointers are HIP device memory (e.g. PyTorch-ROCm
+ *    tensors' data_ptr()); every launch is enqueued on the caller's stream (`stream`, a
+ *    hipStream_t passed as void*; NULL = the null stream).  No entry point synchronises the
+ *    device unless its comment says so.
+ *  - Layouts: images NHWC float32 [B,H,W,3] in the victim's normalised space; boxes
+ *    [ymin,xmin,ymax,xmax] float32 pixels; the trainable parameter buffer is the contiguous
+ *    float32 vector [patch 640*640*3 | scale 1] (`PHX_NPARAM` floats), gradients use the same
+ *    layout (the reference's `_trainable_variables = [scale, patch]`, attacker.py:63, in a
+ *    flat order that lets one RCCL all-reduce cover both).
+ *  - Errors: every int-returning call returns 0 on success and a negative PHX_E* code on
+ *    failure; phx_last_error() returns the message.  No C++ exception crosses the ABI.
+ */
+#ifndef PHX_H_
+#define PHX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PHX_ABI_VERSION 1
+
+#define PHX_PATCH_SIZE 640                               /* attacker.py:43 */
+#define PHX_NPATCH (PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3)
+#define PHX_NPARAM (PHX_NPATCH + 1)                      /* [patch | scale] */
+#define PHX_MAX_OUT 100                                  /* nms max_output_size, hparams_config.py:264 */
+
+enum {
+  PHX_OK = 0,
+  PHX_EINVAL = -1,   /* bad argument / shape */
+  PHX_EHIP = -2,     /* HIP runtime error */
+  PHX_ESTATE = -3,   /* call order (e.g. weights not loaded) */
+  PHX_ECAP = -4,     /* capacity exceeded (batch > max_batch, ...) */
+};
+
+/* BN modes.  LOCAL = training-mode batch statistics over the rank's batch, as
+ * the reference's attack step (victim inherits training=True, attacker.py:172); FROZEN =
+ * inference BN with moving statistics (attacker.py:325 test_step). */
+enum { PHX_BN_LOCAL = 0, PHX_BN_FROZEN = 1 };
+
+typedef struct phx_config {
+  const char* model_name;   /* "efficientdet-d0" ... "-d7", "efficientdet-lite0".."-lite4"
+                               (hparams_config.py:301-467)                                  */
+  int image_size;           /* 0 = model default; square images only                         */
+  int max_batch;            /* per-rank batch capacity (workspace is sized for it)            */
+  int bn_mode;              /* PHX_BN_LOCAL / PHX_BN_FROZEN                                   */
+  float score_thresh;       /* nms_configs.score_thresh (attacker_train.py:31 override = 0.5) */
+  uint64_t seed;            /* Philox key for all EOT randomness                              */
+} phx_config;
+
+typedef struct phx_ctx phx_ctx;
+
+/* Per-step metrics written by phx_step_grad (host-readable device or host memory, PHX_NMETRIC
+ * floats), the reference's add_metric set, attacker.py:196-207. */
+enum {
+  PHX_M_LOSS = 0,        /* sum_b m_b^2 + scale_loss (+ 1e-5*TV on the rank that owns TV)  */
+  PHX_M_SCALE_LOSS = 1,  /* sum_b (m_b - s)^2                                              */
+  PHX_M_TV = 2,          /* total_variation(patch)                                         */
+  PHX_M_SUM_M = 3,       /* sum_b m_b      (mean_max_score = SUM_M / B)                    */
+  PHX_M_SUM_M2 = 4,      /* sum_b m_b^2    (std_max_score)                                 */
+  PHX_M_ASR_NUM = 5,     /* #second-pass boxes >= 0.5 after soft-NMS                       */
+  PHX_M_ASR_DEN = 6,     /* #first-pass boxes >= 0.5                                       */
+  PHX_M_NBOX = 7,        /* #patches pasted                                                */
+  PHX_NMETRIC = 8
+};
+
+/* ---- lifetime --------------------------------------------------------------------------- */
+/* Replaces util.get_victim_model (util.py:177) + infer_lib.KerasDriver.__init__
+ * (infer_lib.py:385-403): builds the EfficientDet program for `cfg` on `device`. */
+int phx_create(const phx_config* cfg, int device, phx_ctx** out);
+void phx_destroy(phx_ctx* ctx);
+const char* phx_last_error(const phx_ctx* ctx);
+int phx_abi_version(void);
+
+/* JSON list of the victim's tensors in blob order: [{"name","shape","offset","kind"}...].
+ * kind: "kernel","bias","gamma","beta","moving_mean","moving_variance","wsm".
+ * Writes at most `cap` bytes (NUL-terminated); *needed = full length + 1. */
+int phx_weight_manifest(const phx_ctx* ctx, char* buf, size_t cap, size_t* needed);
+size_t phx_weight_count(const phx_ctx* ctx);   /* floats in the blob */
+/* Copies a host float32 blob laid out per the manifest (restore_ckpt, util_keras.py:108). */
+int phx_load_weights(phx_ctx* ctx, const float* host_blob, size_t nfloats);
+/* Copies the (possibly updated) BN moving statistics back into a host blob. */
+int phx_read_weights(phx_ctx* ctx, float* host_blob, size_t nfloats);
+
+/* ---- victim ----------------------------------------------------------------------------- */
+/* EfficientDetModel.call(images, pre_mode=None, post_mode=None) (efficientdet_keras.py:966)
+ * followed by postprocess.pre_nms (postprocess.py:119): per anchor max logit score (sigmoid),
+ * argmax class and decoded box.  scores [B,A], classes [B,A] int32, boxes [B,A,4].
+ * A = phx_num_anchors(). BN statistics per cfg.bn_mode (moving stats are updated in LOCAL). */
+int phx_detect(phx_ctx* ctx, const float* images, int B, float* scores, int32_t* classes,
+               float* boxes, void* stream);
+int phx_num_anchors(const phx_ctx* ctx);
+int phx_image_size(const phx_ctx* ctx);
+
+/* PatchAttacker.first_pass (attacker.py:91-116): detect + person/valid/threshold filter +
+ * gaussian soft-NMS (postprocess.nms, postprocess.py:159-205 → NonMaxSuppressionV5) +
+ * clip_boxes.  out_boxes [B,100,4], out_scores [B,100], out_count [B] (device). */
+int phx_first_pass(phx_ctx* ctx, const float* images, int B, float* out_boxes,
+                   float* out_scores, int32_t* out_count, void* stream);
+
+/* Soft-NMS alone over caller-provided candidates (postprocess.nms with padded=True):
+ * boxes [B,N,4], scores [B,N], count [B] valid candidates per row. */
+int phx_soft_nms(phx_ctx* ctx, const float* boxes, const float* scores, const int32_t* count,
+                 int B, int N, float* out_boxes, float* out_scores, int32_t* out_count,
+                 void* stream);
+
+/* ---- EOT patch pipeline ----------------------------------------------------------------- */
+/* BrightnessMatcher.call((src, tgt)) (brightness_matcher.py:43-73) for one src per image:
+ * src [B,P,P,3], tgt [B,H,W,3] -> out [B,P,P,3]. */
+int phx_brightness_match(phx_ctx* ctx, const float* src, int P, const float* tgt, int H, int W,
+                         int B, float* out, void* stream);
+
+/* Patcher.call([boxes, images]) (attacker.py:490-498): print variation, brightness match,
+ * placement, antialiased resize, noise, brightness jitter, ±20° rotate, composite, paste.
+ * boxes [B,maxb,4] with count [B]; params = [patch | scale]; `step` keys the RNG.
+ * Also returns per-box placements [B,maxb,8] (ymin,xmin,ps,diag,angle,delta,valid,-) if
+ * `placements` is non-NULL. */
+int phx_patch_images(phx_ctx* ctx, const float* images, int B, const float* boxes,
+                     const int32_t* count, int maxb, const float* params, int64_t step,
+                     int global_image_offset, float* out_images, float* placements,
+                     void* stream);
+
+/* ---- the step --------------------------------------------------------------------------- */
+/* PatchAttacker.call(images, training=True) (attacker.py:172-219): first pass (or the
+ * caller's boxes when `boxes` != NULL: "injected" placement), EOT paste, second pass, loss,
+ * and the gradient of the loss w.r.t. [patch | scale] written to `grad` (PHX_NPARAM floats,
+ * overwritten).  `add_tv` = 1 adds the 1e-5*TV term (rank 0 only under data parallelism).
+ * metrics: PHX_NMETRIC floats (device pointer).  `global_image_offset` = rank * B keys the
+ * RNG so draws are independent of the GPU count. */
+int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
+                  const int32_t* count, int maxb, const float* params, int64_t step,
+                  int global_image_offset, int add_tv, float* grad, float* metrics,
+                  void* stream);
+
+/* Keras Adam (ResourceApplyAdam, beta1 .9, beta2 .999, eps 1e-7; attacker_train.py:38) on
+ * [patch | scale] followed by the variable constraints clip(patch,-1,1), clip(scale,0,1)
+ * (attacker.py:51-54).  m, v: PHX_NPARAM floats each.  t = 1-based iteration. */
+int phx_adam_clip(phx_ctx* ctx, float* params, const float* grad, float* m, float* v,
+                  float lr, int64_t t, void* stream);
+
+/* Debug / test hooks (parity tests call these; not on the timed path).
+ * phx_debug_last_patched: copies the last step's patched images [B,H,W,3] (device->device). */
+int phx_debug_last_patched(phx_ctx* ctx, float* out, void* stream);
+/* Last step's per-image max scores m_b [B] and loss-anchor index [B] (device->device). */
+int phx_debug_last_maxscores(phx_ctx* ctx, float* m, int32_t* anchor, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PHX_H_ */

@@ -1,0 +1,145 @@
+"""ctypes binding of libphx.so (the C ABI declared in include/phx.h).
+
+The shared library is built in-tree (``python -m mladversarialobjectdetection_amd.build`` or
+``__graft_entry__.build()``) and loaded from this package directory.  There is deliberately no
+fallback: if the library is missing every entry point raises, so a GPU run can never silently
+execute anything but the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_size_t, c_uint64, c_void_p
+
+ABI_VERSION = 1
+PATCH_SIZE = 640
+NPATCH = PATCH_SIZE * PATCH_SIZE * 3
+NPARAM = NPATCH + 1
+MAX_OUT = 100
+
+# metric slots (phx.h PHX_M_*)
+M_LOSS, M_SCALE_LOSS, M_TV, M_SUM_M, M_SUM_M2, M_ASR_NUM, M_ASR_DEN, M_NBOX = range(8)
+NMETRIC = 8
+
+BN_LOCAL, BN_FROZEN = 0, 1
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libphx.so")
+
+
+class PhxError(RuntimeError):
+    pass
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [
+        ("model_name", c_char_p),
+        ("image_size", c_int),
+        ("max_batch", c_int),
+        ("bn_mode", c_int),
+        ("score_thresh", c_float),
+        ("seed", c_uint64),
+    ]
+
+
+# (name, restype, argtypes) — one row per declaration in include/phx.h
+_SIGS = [
+    ("phx_abi_version", c_int, []),
+    ("phx_create", c_int, [POINTER(_Config), c_int, POINTER(c_void_p)]),
+    ("phx_destroy", None, [c_void_p]),
+    ("phx_last_error", c_char_p, [c_void_p]),
+    ("phx_weight_manifest", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
+    ("phx_weight_count", c_size_t, [c_void_p]),
+    ("phx_load_weights", c_int, [c_void_p, c_void_p, c_size_t]),
+    ("phx_read_weights", c_int, [c_void_p, c_void_p, c_size_t]),
+    ("phx_detect", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("phx_num_anchors", c_int, [c_void_p]),
+    ("phx_image_size", c_int, [c_void_p]),
+    ("phx_first_pass", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("phx_soft_nms", c_int,
+     [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("phx_brightness_match", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("phx_patch_images", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_void_p,
+      c_void_p, c_void_p]),
+    ("phx_step_grad", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
+      c_void_p, c_void_p, c_void_p]),
+    ("phx_adam_clip", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int64, c_void_p]),
+    ("phx_debug_last_patched", c_int, [c_void_p, c_void_p, c_void_p]),
+    ("phx_debug_last_maxscores", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+]
+
+EXPORTED = [s[0] for s in _SIGS]
+
+_lib = None
+
+
+def load(path: str | None = None):
+    """Load libphx.so once; raise PhxError when it is missing (no CPU fallback exists)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise PhxError(
+            f"{p} not found: build the HIP extension first (python -m "
+            "mladversarialobjectdetection_amd.build)")
+    lib = ctypes.CDLL(p)
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.phx_abi_version() != ABI_VERSION:
+        raise PhxError("libphx ABI version mismatch")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(ctx, rc: int, what: str):
+    if rc != 0:
+        msg = load().phx_last_error(ctx)
+        raise PhxError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+class Context:
+    """Owns one phx_ctx (one victim model on one device)."""
+
+    def __init__(self, model_name="efficientdet-d0", image_size=0, max_batch=16,
+                 bn_mode=BN_LOCAL, score_thresh=0.5, seed=0, device=0):
+        lib = load()
+        self.lib = lib
+        cfg = _Config(model_name.encode(), int(image_size), int(max_batch), int(bn_mode),
+                      float(score_thresh), int(seed) & ((1 << 64) - 1))
+        h = c_void_p()
+        rc = lib.phx_create(ctypes.byref(cfg), int(device), ctypes.byref(h))
+        if rc != 0:
+            raise PhxError(f"phx_create({model_name}) failed ({rc})")
+        self.h = h
+        self.model_name = model_name
+        self.max_batch = int(max_batch)
+        self.image_size = lib.phx_image_size(h)
+        self.num_anchors = lib.phx_num_anchors(h)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.phx_destroy(h)
+            self.h = None
+
+    def manifest(self):
+        need = c_size_t()
+        self.lib.phx_weight_manifest(self.h, None, 0, ctypes.byref(need))
+        buf = ctypes.create_string_buffer(need.value)
+        self.lib.phx_weight_manifest(self.h, buf, need.value, ctypes.byref(need))
+        return json.loads(buf.value.decode())
+
+    def weight_count(self) -> int:
+        return int(self.lib.phx_weight_count(self.h))
+
+    def call(self, name: str, *args):
+        rc = getattr(self.lib, name)(self.h, *args)
+        check(self.h, rc, name)

@@ -1,0 +1,818 @@
+// api.cpp — libphx C ABI: context, weight management, the program executor (victim forward
+// and data-gradient), and the attack step that strings the kernels together on one stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "model.hpp"
+#include "phx.h"
+#include "post.hpp"
+
+using namespace phx;
+
+namespace {
+
+constexpr float kBnEps = 1e-3f;  // efficientnet_builder.py:179, util_keras.py:35
+
+template <typename T>
+T* dalloc(size_t n) {
+  if (n == 0) n = 1;
+  void* p = nullptr;
+  PHX_HIP(hipMalloc(&p, n * sizeof(T)));
+  return reinterpret_cast<T*>(p);
+}
+
+struct DevFree {
+  void operator()(void* p) const {
+    if (p) (void)hipFree(p);
+  }
+};
+using DPtr = std::unique_ptr<void, DevFree>;
+
+// Per-batch-size executable state: program + arenas + step buffers.
+struct Exec {
+  Program prog;
+  int B = 0;
+  std::vector<DPtr> owned;
+  float* act = nullptr;
+  float* grad = nullptr;
+  std::vector<float*> slot_a, slot_b, slot_c;  // BN: mean,rstd ; SE: pool(+part),hidden,scale
+  double* red = nullptr;                       // BN partial sums
+  float* coef = nullptr;                       // BN backward coefficients
+  float* se_g = nullptr;                       // SE backward scratch
+  std::vector<int> se_of_tensor;               // tensor id -> SE op index producing it (-1)
+  LevelDesc* lev_dev = nullptr;
+  std::vector<LevelDesc> lev;
+  long* dxoff_dev = nullptr;
+  std::vector<long> dxoff;
+  bool cls_contig = true;
+  // pre_nms / nms / loss
+  float *scores = nullptr, *boxes = nullptr;
+  int* classes = nullptr;
+  uint8_t* keep = nullptr;
+  float* nms_ws = nullptr;
+  int* nms_wi = nullptr;
+  float *nms1_boxes = nullptr, *nms1_scores = nullptr;
+  int* nms1_count = nullptr;
+  float *nms2_boxes = nullptr, *nms2_scores = nullptr;
+  int* nms2_count = nullptr;
+  float *mraw = nullptr, *dm = nullptr;
+  int *argm = nullptr, *nties = nullptr;
+  // EOT
+  EotDims ed{};
+  ImgParams* img = nullptr;
+  BoxPlace* place = nullptr;  // followed by the int lists
+  SpanEntry* spans = nullptr;
+  double* ysum = nullptr;
+  float* ymean = nullptr;
+  float *rstore = nullptr, *dstore = nullptr;
+  float *matched = nullptr, *dmatched = nullptr;
+  double* dsum = nullptr;
+  double* tvs = nullptr;
+  int* err = nullptr;
+  float* patched = nullptr;
+  int16_t* owner = nullptr;
+
+  template <typename T>
+  T* alloc(size_t n) {
+    T* p = dalloc<T>(n);
+    owned.emplace_back(p);
+    return p;
+  }
+  float* tptr(int t, const float* input) const {
+    if (t == prog.input) return const_cast<float*>(input);
+    return act + prog.tensors[t].off;
+  }
+  float* gptr(int t) const {
+    long g = prog.tensors[t].goff;
+    return g < 0 ? nullptr : grad + g;
+  }
+};
+
+}  // namespace
+
+struct phx_ctx {
+  ModelConfig mc;
+  int device = 0;
+  int max_batch = 0;
+  int bn_mode = PHX_BN_LOCAL;
+  float score_thresh = 0.5f;
+  uint64_t seed = 0;
+  std::vector<WeightEntry> weights;
+  size_t wfloats = 0;
+  std::string manifest_json;
+  DPtr d_w, d_wt;
+  std::vector<long> wt_map;  // weight offset -> offset in d_wt (dense map over kernel entries)
+  std::vector<std::pair<long, long>> wt_pairs;
+  bool weights_loaded = false;
+  DPtr d_anchors;
+  int A = 0;
+  std::vector<std::unique_ptr<Exec>> execs;
+  Exec* last = nullptr;
+  std::string err;
+  // scratch for phx_soft_nms standalone
+  DPtr sn_ws, sn_wi;
+  size_t sn_cap = 0;
+
+  float* w() const { return reinterpret_cast<float*>(d_w.get()); }
+  const float* wt_of(long off) const {
+    for (auto& p : wt_pairs)
+      if (p.first == off) return reinterpret_cast<const float*>(d_wt.get()) + p.second;
+    throw std::runtime_error("no transposed kernel for weight offset");
+  }
+  Exec& exec_for(int B);
+};
+
+namespace {
+
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '"' || c == '\\') o.push_back('\\');
+    o.push_back(c);
+  }
+  return o;
+}
+
+// anchors.py:83-165 in float64, cast to float32
+std::vector<float> make_anchors(const ModelConfig& mc) {
+  std::vector<int> fs{mc.image_size};
+  int f = mc.image_size;
+  for (int l = 1; l <= mc.max_level; ++l) {
+    f = (f - 1) / 2 + 1;
+    fs.push_back(f);
+  }
+  std::vector<float> out;
+  for (int level = mc.min_level; level <= mc.max_level; ++level) {
+    const double stride = (double)fs[0] / (double)fs[level];
+    struct C { double base_x, base_y, ax, ay; };
+    std::vector<C> cs;
+    for (int o = 0; o < mc.num_scales; ++o) {
+      for (float ar : mc.aspect_ratios) {
+        double octave = (double)o / (double)mc.num_scales;
+        double base = (double)mc.anchor_scale * stride * std::pow(2.0, octave);
+        double ax = std::sqrt((double)ar);
+        double ay = 1.0 / ax;
+        cs.push_back({base, base, ax, ay});
+      }
+    }
+    std::vector<double> xs, ys;
+    // numpy arange: start + i*step
+    for (int i = 0;; ++i) {
+      double v = stride / 2 + i * stride;
+      if (v >= mc.image_size) break;
+      xs.push_back(v);
+    }
+    ys = xs;
+    for (double yv : ys) {
+      for (double xv : xs) {
+        for (const C& c : cs) {
+          double sx2 = c.base_x * c.ax / 2.0, sy2 = c.base_y * c.ay / 2.0;
+          out.push_back((float)(yv - sy2));
+          out.push_back((float)(xv - sx2));
+          out.push_back((float)(yv + sy2));
+          out.push_back((float)(xv + sx2));
+        }
+      }
+    }
+  }
+  return out;
+}
+
+int fail(phx_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// executor
+// ------------------------------------------------------------------------------------------
+Exec& phx_ctx::exec_for(int B) {
+  for (auto& e : execs)
+    if (e->B == B) return *e;
+  auto ex = std::make_unique<Exec>();
+  Exec& E = *ex;
+  E.B = B;
+  NetBuilder nb(mc, B, bn_mode == PHX_BN_LOCAL);
+  nb.build();
+  E.prog = nb.program();
+  Program& P = E.prog;
+  E.act = E.alloc<float>(P.act_floats);
+  E.grad = E.alloc<float>(P.grad_floats);
+  // statistics slots and scratch
+  E.slot_a.assign(P.n_slots, nullptr);
+  E.slot_b.assign(P.n_slots, nullptr);
+  E.slot_c.assign(P.n_slots, nullptr);
+  size_t red_need = 1, coef_need = 1, seg_need = 1;
+  E.se_of_tensor.assign(P.tensors.size(), -1);
+  for (size_t i = 0; i < P.ops.size(); ++i) {
+    const Op& op = P.ops[i];
+    const Tensor& ti = P.tensors[op.in[0]];
+    if (op.t == OP_BN) {
+      E.slot_a[op.slot] = E.alloc<float>(ti.c);
+      E.slot_b[op.slot] = E.alloc<float>(ti.c);
+      red_need = std::max(red_need, bn_stats_scratch_doubles((long)ti.rows(), ti.c));
+      coef_need = std::max(coef_need, (size_t)ti.c * 3);
+    } else if (op.t == OP_SE) {
+      E.slot_a[op.slot] = E.alloc<float>((size_t)B * ti.c * 65);
+      E.slot_b[op.slot] = E.alloc<float>((size_t)B * op.cse);
+      E.slot_c[op.slot] = E.alloc<float>((size_t)B * ti.c);
+      seg_need = std::max(seg_need, (size_t)B * ti.c * 65);
+      E.se_of_tensor[op.out] = (int)i;
+    }
+  }
+  E.red = E.alloc<double>(red_need);
+  E.coef = E.alloc<float>(coef_need);
+  E.se_g = E.alloc<float>(seg_need);
+  // level tables (class / box outputs)
+  const int nlev = (int)P.cls_out.size();
+  const int na = mc.num_anchors();
+  int a0 = 0;
+  const float* base = E.act + P.tensors[P.cls_out[0]].off;
+  const float* bbase = E.act + P.tensors[P.box_out[0]].off;
+  for (int l = 0; l < nlev; ++l) {
+    const Tensor& tc = P.tensors[P.cls_out[l]];
+    const Tensor& tb = P.tensors[P.box_out[l]];
+    LevelDesc d;
+    d.cls_off = (long)tc.off - (long)P.tensors[P.cls_out[0]].off;
+    d.box_off = (long)tb.off - (long)P.tensors[P.box_out[0]].off;
+    d.h = tc.h;
+    d.w = tc.w;
+    d.anchor0 = a0;
+    a0 += tc.h * tc.w * na;
+    E.lev.push_back(d);
+    // input of the class-predict pointwise conv
+    for (const Op& op : P.ops)
+      if (op.out == P.cls_out[l]) E.dxoff.push_back(P.tensors[op.in[0]].goff);
+  }
+  (void)base; (void)bbase;
+  if (a0 != A) throw std::runtime_error("anchor count mismatch");
+  E.lev_dev = E.alloc<LevelDesc>(nlev);
+  PHX_HIP(hipMemcpy(E.lev_dev, E.lev.data(), nlev * sizeof(LevelDesc), hipMemcpyHostToDevice));
+  E.dxoff_dev = E.alloc<long>(nlev);
+  PHX_HIP(hipMemcpy(E.dxoff_dev, E.dxoff.data(), nlev * sizeof(long), hipMemcpyHostToDevice));
+  // post-processing buffers
+  const long BA = (long)B * A;
+  E.scores = E.alloc<float>(BA);
+  E.classes = E.alloc<int>(BA);
+  E.boxes = E.alloc<float>(BA * 4);
+  E.keep = E.alloc<uint8_t>(BA);
+  E.nms_ws = E.alloc<float>(BA);
+  E.nms_wi = E.alloc<int>(BA * 2);
+  E.nms1_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
+  E.nms1_scores = E.alloc<float>((size_t)B * PHX_MAX_OUT);
+  E.nms1_count = E.alloc<int>(B);
+  E.nms2_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
+  E.nms2_scores = E.alloc<float>((size_t)B * PHX_MAX_OUT);
+  E.nms2_count = E.alloc<int>(B);
+  E.mraw = E.alloc<float>(B);
+  E.dm = E.alloc<float>(B);
+  E.argm = E.alloc<int>(B);
+  E.nties = E.alloc<int>(B);
+  // EOT
+  const int S = mc.image_size;
+  E.ed.B = B;
+  E.ed.H = S;
+  E.ed.W = S;
+  E.ed.maxb = PHX_MAX_OUT;
+  E.ed.P = PHX_PATCH_SIZE;
+  E.ed.span_stride = S;
+  // worst case: every slot holds a full-image patch
+  E.ed.rcap = (long)B * PHX_MAX_OUT * S * S * 3;
+  const long nslot = (long)B * PHX_MAX_OUT;
+  E.img = E.alloc<ImgParams>(B);
+  {
+    size_t bytes = nslot * sizeof(BoxPlace) + (4 + 2 * B + 2 * nslot + 1) * sizeof(int);
+    E.place = reinterpret_cast<BoxPlace*>(E.alloc<char>(bytes));
+  }
+  E.spans = E.alloc<SpanEntry>(nslot * S);
+  E.ysum = E.alloc<double>((size_t)B * 2 * 64);
+  E.ymean = E.alloc<float>((size_t)B * 2);
+  E.rstore = E.alloc<float>(E.ed.rcap);
+  E.dstore = E.alloc<float>(E.ed.rcap);
+  const size_t np = (size_t)PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3;
+  E.matched = E.alloc<float>(np * B);
+  E.dmatched = E.alloc<float>(np * B);
+  E.dsum = E.alloc<double>((size_t)B * 64);
+  E.tvs = E.alloc<double>(256);
+  E.err = E.alloc<int>(1);
+  E.patched = E.alloc<float>((size_t)B * S * S * 3);
+  E.owner = E.alloc<int16_t>((size_t)B * S * S * 3);
+  execs.push_back(std::move(ex));
+  return *execs.back();
+}
+
+namespace {
+
+// victim forward over the program (EfficientDetNet.call, efficientdet_keras.py:884-906)
+void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
+  const Program& P = E.prog;
+  float* W = ctx->w();
+  const bool frozen = ctx->bn_mode == PHX_BN_FROZEN;
+  for (size_t i = 0; i < P.ops.size(); ++i) {
+    const Op& op = P.ops[i];
+    const Tensor& ti = P.tensors[op.in[0]];
+    const Tensor& to = P.tensors[op.out];
+    float* x = E.tptr(op.in[0], input);
+    float* y = E.tptr(op.out, input);
+    switch (op.t) {
+      case OP_STEM:
+        launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s);
+        break;
+      case OP_PW: {
+        const float* A = x;
+        const float* rs = nullptr;
+        int rpi = 1;
+        int se = E.se_of_tensor[op.in[0]];
+        if (se >= 0) {  // SE excitation folded into the GEMM's A load
+          const Op& sop = P.ops[se];
+          A = E.tptr(sop.in[0], input);
+          rs = E.slot_c[sop.slot];
+          rpi = ti.h * ti.w;
+        }
+        launch_gemm(A, ctx->wt_of(op.w), op.b >= 0 ? W + op.b : nullptr, y, (int)ti.rows(), to.c,
+                    ti.c, false, rs, rpi, s);
+        break;
+      }
+      case OP_DW:
+        launch_dw_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
+                      op.pad_l, s);
+        break;
+      case OP_BN: {
+        float* mean = E.slot_a[op.slot];
+        float* rstd = E.slot_b[op.slot];
+        if (frozen)
+          launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, ti.c, kBnEps, s);
+        else
+          launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.mmean, W + op.mvar,
+                          kBnEps, s);
+        launch_bn_apply(x, mean, rstd, W + op.gamma, W + op.beta, y, (long)ti.rows(), ti.c, op.act,
+                        s);
+        break;
+      }
+      case OP_SE:
+        launch_se_fwd(x, nullptr, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1, W + op.b1, W + op.w2,
+                      W + op.b2, op.act, E.slot_a[op.slot], E.slot_b[op.slot], E.slot_c[op.slot], s);
+        break;
+      case OP_ADD:
+        launch_add(x, E.tptr(op.in[1], input), y, (long)to.numel(), s);
+        break;
+      case OP_MAXPOOL:
+        launch_maxpool_fwd(x, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
+                           op.pad_l, s);
+        break;
+      case OP_UPSAMPLE:
+        launch_upsample_fwd(x, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, s);
+        break;
+      case OP_FUSE: {
+        const float* xs[3] = {nullptr, nullptr, nullptr};
+        for (int k = 0; k < op.nin; ++k) xs[k] = E.tptr(op.in[k], input);
+        launch_fuse_fwd(xs, op.nin, op.wsm[0] >= 0 ? W + op.wsm[0] : nullptr,
+                        op.wsm[1] >= 0 ? W + op.wsm[1] : nullptr,
+                        op.wsm[2] >= 0 ? W + op.wsm[2] : nullptr, op.fuse_method, op.act, y,
+                        (long)to.numel(), s);
+        break;
+      }
+    }
+  }
+}
+
+bool is_cls_out(const Program& P, int t) {
+  return std::find(P.cls_out.begin(), P.cls_out.end(), t) != P.cls_out.end();
+}
+
+// data-gradient of the victim from the sparse class-logit gradient (attacker.py:217)
+void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
+  const Program& P = E.prog;
+  float* W = ctx->w();
+  const bool frozen = ctx->bn_mode == PHX_BN_FROZEN;
+  const int na = ctx->mc.num_anchors();
+  // 1. sparse class-head gradient into the inputs of the class-predict pointwise convs
+  int K = 0;
+  long wpred = -1;
+  for (int l = 0; l < (int)P.cls_out.size(); ++l) {
+    for (const Op& op : P.ops) {
+      if (op.out != P.cls_out[l]) continue;
+      const Tensor& ti = P.tensors[op.in[0]];
+      PHX_HIP(hipMemsetAsync(E.gptr(op.in[0]), 0, ti.numel() * sizeof(float), s));
+      K = ti.c;
+      wpred = op.w;
+    }
+  }
+  launch_cls_scatter(E.scores, E.keep, E.mraw, E.nties, E.dm, E.act + P.tensors[P.cls_out[0]].off,
+                     E.lev_dev, (int)E.lev.size(), ctx->A, E.B, ctx->mc.num_classes, na,
+                     W + wpred, K, E.grad, E.dxoff_dev, s);
+  // 2. reverse sweep
+  for (int i = (int)P.ops.size() - 1; i >= 0; --i) {
+    const Op& op = P.ops[i];
+    if (!op.bwd) continue;
+    if (op.t == OP_PW && is_cls_out(P, op.out)) continue;  // handled by the scatter
+    const Tensor& ti = P.tensors[op.in[0]];
+    const Tensor& to = P.tensors[op.out];
+    const float* dy = E.gptr(op.out);
+    float* dx = E.gptr(op.in[0]);
+    switch (op.t) {
+      case OP_STEM:
+        launch_stem_bwd(dy, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
+                        op.acc[0], s);
+        break;
+      case OP_PW:
+        // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
+        launch_gemm(dy, W + op.w, nullptr, dx, (int)ti.rows(), ti.c, to.c, op.acc[0], nullptr, 1, s);
+        break;
+      case OP_DW:
+        launch_dw_bwd(dy, W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride,
+                      op.pad_t, op.pad_l, op.acc[0], s);
+        break;
+      case OP_BN:
+        launch_bn_bwd(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
+                      W + op.gamma, W + op.beta, dx, (long)ti.rows(), ti.c, op.act, frozen,
+                      op.acc[0], E.red, E.coef, s);
+        break;
+      case OP_SE:
+        launch_se_bwd(dy, E.tptr(op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
+                      W + op.b1, W + op.w2, W + op.b2, op.act, E.slot_a[op.slot],
+                      E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s);
+        break;
+      case OP_ADD:
+        launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s);
+        launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s);
+        break;
+      case OP_MAXPOOL:
+        launch_maxpool_bwd(E.tptr(op.in[0], input), dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w,
+                           op.k, op.stride, op.pad_t, op.pad_l, op.acc[0], s);
+        break;
+      case OP_UPSAMPLE:
+        launch_upsample_bwd(dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.acc[0], s);
+        break;
+      case OP_FUSE: {
+        const float* xs[3] = {nullptr, nullptr, nullptr};
+        float* dxs[3] = {nullptr, nullptr, nullptr};
+        bool acc[3] = {false, false, false};
+        for (int k = 0; k < op.nin; ++k) {
+          xs[k] = E.tptr(op.in[k], input);
+          dxs[k] = E.gptr(op.in[k]);
+          acc[k] = op.acc[k];
+        }
+        launch_fuse_bwd(xs, op.nin, op.wsm[0] >= 0 ? W + op.wsm[0] : nullptr,
+                        op.wsm[1] >= 0 ? W + op.wsm[1] : nullptr,
+                        op.wsm[2] >= 0 ? W + op.wsm[2] : nullptr, op.fuse_method, op.act, dy, dxs,
+                        acc, (long)to.numel(), s);
+        break;
+      }
+    }
+  }
+}
+
+void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
+  const Program& P = E.prog;
+  const float S = (float)ctx->mc.image_size;
+  launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
+                 E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
+                 ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->score_thresh,
+                 E.scores, E.classes, E.boxes, E.keep, s);
+}
+
+// postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25
+void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s) {
+  launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->score_thresh,
+                  0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s);
+}
+
+void check_ready(phx_ctx* ctx, int B) {
+  if (!ctx->weights_loaded) throw std::logic_error("weights not loaded");
+  if (B <= 0 || B > ctx->max_batch) throw std::out_of_range("batch exceeds max_batch");
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+#define PHX_TRY(ctx)                                                           \
+  try {
+#define PHX_CATCH(ctx)                                                         \
+  }                                                                            \
+  catch (const std::out_of_range& e) { return fail(ctx, PHX_ECAP, e.what()); } \
+  catch (const std::invalid_argument& e) { return fail(ctx, PHX_EINVAL, e.what()); } \
+  catch (const std::logic_error& e) { return fail(ctx, PHX_ESTATE, e.what()); } \
+  catch (const HipError& e) { return fail(ctx, PHX_EHIP, e.what()); }          \
+  catch (const std::exception& e) { return fail(ctx, PHX_EINVAL, e.what()); }
+
+extern "C" {
+
+int phx_abi_version(void) { return PHX_ABI_VERSION; }
+
+int phx_create(const phx_config* cfg, int device, phx_ctx** out) {
+  if (!cfg || !out || !cfg->model_name) return PHX_EINVAL;
+  *out = nullptr;
+  auto ctx = std::make_unique<phx_ctx>();
+  try {
+    if (!get_model_config(cfg->model_name, &ctx->mc)) return PHX_EINVAL;
+    if (cfg->image_size > 0) ctx->mc.image_size = cfg->image_size;
+    ctx->device = device;
+    ctx->max_batch = cfg->max_batch > 0 ? cfg->max_batch : 1;
+    ctx->bn_mode = cfg->bn_mode;
+    ctx->score_thresh = cfg->score_thresh > 0.f ? cfg->score_thresh : 0.5f;
+    ctx->seed = cfg->seed;
+    NetBuilder nb(ctx->mc, 0);
+    nb.build();
+    ctx->weights = nb.weights();
+    ctx->wfloats = nb.weight_floats();
+    std::ostringstream js;
+    js << "[";
+    for (size_t i = 0; i < ctx->weights.size(); ++i) {
+      const WeightEntry& w = ctx->weights[i];
+      js << (i ? "," : "") << "{\"name\":\"" << json_escape(w.name) << "\",\"shape\":[";
+      for (size_t k = 0; k < w.shape.size(); ++k) js << (k ? "," : "") << w.shape[k];
+      js << "],\"offset\":" << w.offset << ",\"kind\":\"" << w.kind << "\"}";
+    }
+    js << "]";
+    ctx->manifest_json = js.str();
+    // anchors
+    int f = ctx->mc.image_size, a = 0;
+    for (int l = 1; l <= ctx->mc.max_level; ++l) {
+      f = (f - 1) / 2 + 1;
+      if (l >= ctx->mc.min_level) a += f * f * ctx->mc.num_anchors();
+    }
+    ctx->A = a;
+  } catch (const std::exception& e) {
+    return PHX_EINVAL;
+  }
+  *out = ctx.release();
+  return PHX_OK;
+}
+
+void phx_destroy(phx_ctx* ctx) { delete ctx; }
+
+const char* phx_last_error(const phx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int phx_weight_manifest(const phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
+  if (!ctx) return PHX_EINVAL;
+  size_t n = ctx->manifest_json.size() + 1;
+  if (needed) *needed = n;
+  if (buf && cap > 0) {
+    size_t c = std::min(cap - 1, ctx->manifest_json.size());
+    memcpy(buf, ctx->manifest_json.data(), c);
+    buf[c] = 0;
+  }
+  return PHX_OK;
+}
+
+size_t phx_weight_count(const phx_ctx* ctx) { return ctx ? ctx->wfloats : 0; }
+int phx_num_anchors(const phx_ctx* ctx) { return ctx ? ctx->A : 0; }
+int phx_image_size(const phx_ctx* ctx) { return ctx ? ctx->mc.image_size : 0; }
+
+int phx_load_weights(phx_ctx* ctx, const float* blob, size_t nfloats) {
+  if (!ctx || !blob) return PHX_EINVAL;
+  if (nfloats != ctx->wfloats) return fail(ctx, PHX_EINVAL, "weight blob size mismatch");
+  PHX_TRY(ctx)
+  PHX_HIP(hipSetDevice(ctx->device));
+  if (!ctx->d_w) ctx->d_w.reset(dalloc<float>(ctx->wfloats));
+  PHX_HIP(hipMemcpy(ctx->d_w.get(), blob, nfloats * sizeof(float), hipMemcpyHostToDevice));
+  // transposed copies of every 1x1 kernel: [Cout][Cin] for the forward GEMM
+  std::vector<float> wt;
+  ctx->wt_pairs.clear();
+  for (const WeightEntry& w : ctx->weights) {
+    if (w.kind != "kernel" || w.shape.size() != 4 || w.shape[0] != 1 || w.shape[1] != 1) continue;
+    const int ci = w.shape[2], co = w.shape[3];
+    ctx->wt_pairs.push_back({(long)w.offset, (long)wt.size()});
+    size_t base = wt.size();
+    wt.resize(base + (size_t)ci * co);
+    for (int i = 0; i < ci; ++i)
+      for (int o = 0; o < co; ++o) wt[base + (size_t)o * ci + i] = blob[w.offset + (size_t)i * co + o];
+  }
+  ctx->d_wt.reset(dalloc<float>(wt.size()));
+  PHX_HIP(hipMemcpy(ctx->d_wt.get(), wt.data(), wt.size() * sizeof(float), hipMemcpyHostToDevice));
+  if (!ctx->d_anchors) {
+    std::vector<float> an = make_anchors(ctx->mc);
+    if ((int)an.size() != ctx->A * 4) throw std::runtime_error("anchor generation mismatch");
+    ctx->d_anchors.reset(dalloc<float>(an.size()));
+    PHX_HIP(hipMemcpy(ctx->d_anchors.get(), an.data(), an.size() * sizeof(float),
+                      hipMemcpyHostToDevice));
+  }
+  ctx->weights_loaded = true;
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_read_weights(phx_ctx* ctx, float* blob, size_t nfloats) {
+  if (!ctx || !blob || nfloats != ctx->wfloats) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->weights_loaded) throw std::logic_error("weights not loaded");
+  PHX_HIP(hipDeviceSynchronize());
+  PHX_HIP(hipMemcpy(blob, ctx->d_w.get(), nfloats * sizeof(float), hipMemcpyDeviceToHost));
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_detect(phx_ctx* ctx, const float* images, int B, float* scores, int32_t* classes,
+               float* boxes, void* stream) {
+  if (!ctx || !images) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  check_ready(ctx, B);
+  hipStream_t s = (hipStream_t)stream;
+  Exec& E = ctx->exec_for(B);
+  run_forward(ctx, E, images, s);
+  run_pre_nms(ctx, E, s);
+  const long BA = (long)B * ctx->A;
+  if (scores) PHX_HIP(hipMemcpyAsync(scores, E.scores, BA * 4, hipMemcpyDeviceToDevice, s));
+  if (classes) PHX_HIP(hipMemcpyAsync(classes, E.classes, BA * 4, hipMemcpyDeviceToDevice, s));
+  if (boxes) PHX_HIP(hipMemcpyAsync(boxes, E.boxes, BA * 16, hipMemcpyDeviceToDevice, s));
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_first_pass(phx_ctx* ctx, const float* images, int B, float* ob, float* os, int32_t* oc,
+                   void* stream) {
+  if (!ctx || !images || !ob || !os || !oc) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  check_ready(ctx, B);
+  hipStream_t s = (hipStream_t)stream;
+  Exec& E = ctx->exec_for(B);
+  run_forward(ctx, E, images, s);
+  run_pre_nms(ctx, E, s);
+  run_nms(ctx, E, 2, ob, os, oc, s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_soft_nms(phx_ctx* ctx, const float* boxes, const float* scores, const int32_t* count,
+                 int B, int N, float* ob, float* os, int32_t* oc, void* stream) {
+  if (!ctx || !boxes || !scores || B <= 0 || N <= 0) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  hipStream_t s = (hipStream_t)stream;
+  size_t need = (size_t)B * N;
+  if (need > ctx->sn_cap) {
+    PHX_HIP(hipStreamSynchronize(s));
+    ctx->sn_ws.reset(dalloc<float>(need));
+    ctx->sn_wi.reset(dalloc<int>(need * 2));
+    ctx->sn_cap = need;
+  }
+  launch_soft_nms(boxes, scores, nullptr, 0, count, B, N, ctx->score_thresh, 0.25f, PHX_MAX_OUT,
+                  (float)ctx->mc.image_size, ob, os, oc, (float*)ctx->sn_ws.get(),
+                  (int*)ctx->sn_wi.get(), s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_brightness_match(phx_ctx* ctx, const float* src, int P, const float* tgt, int H, int W,
+                         int B, float* out, void* stream) {
+  if (!ctx || !src || !tgt || !out || B <= 0 || B > ctx->max_batch) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  hipStream_t s = (hipStream_t)stream;
+  Exec& E = ctx->exec_for(ctx->max_batch);
+  EotDims d = E.ed;
+  d.B = B;
+  d.P = P;
+  d.H = H;
+  d.W = W;
+  launch_eot_match(d, src, nullptr, tgt, out, E.ysum, E.ymean, false, s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+namespace {
+void eot_forward(phx_ctx* ctx, Exec& E, const float* images, int B, const float* boxes,
+                 const int32_t* count, const float* params, int64_t step, int gimg0,
+                 hipStream_t s) {
+  EotDims d = E.ed;
+  d.B = B;
+  launch_eot_place(d, boxes, count, params, ctx->seed, step, gimg0, E.img, E.place, E.spans, E.err,
+                   s);
+  launch_eot_match(d, params, E.img, images, E.matched, E.ysum, E.ymean, true, s);
+  launch_eot_resize(d, E.matched, E.place, E.spans, ctx->seed, step, gimg0, E.rstore, s);
+  launch_eot_composite(d, images, E.place, E.rstore, E.patched, E.owner, s);
+}
+
+// copy caller boxes [B,maxb,4] into the [B,100,4] slot layout
+void stage_boxes(Exec& E, const float* boxes, const int32_t* count, int B, int maxb,
+                 hipStream_t s) {
+  if (maxb > PHX_MAX_OUT) throw std::out_of_range("maxb > 100");
+  PHX_HIP(hipMemsetAsync(E.nms1_boxes, 0, (size_t)B * PHX_MAX_OUT * 16, s));
+  PHX_HIP(hipMemcpy2DAsync(E.nms1_boxes, PHX_MAX_OUT * 16, boxes, (size_t)maxb * 16,
+                           (size_t)maxb * 16, B, hipMemcpyDeviceToDevice, s));
+  PHX_HIP(hipMemcpyAsync(E.nms1_count, count, B * sizeof(int), hipMemcpyDeviceToDevice, s));
+}
+}  // namespace
+
+int phx_patch_images(phx_ctx* ctx, const float* images, int B, const float* boxes,
+                     const int32_t* count, int maxb, const float* params, int64_t step,
+                     int gimg0, float* out_images, float* placements, void* stream) {
+  if (!ctx || !images || !boxes || !count || !params || !out_images) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (B <= 0 || B > ctx->max_batch) throw std::out_of_range("batch exceeds max_batch");
+  hipStream_t s = (hipStream_t)stream;
+  Exec& E = ctx->exec_for(B);
+  ctx->last = &E;
+  stage_boxes(E, boxes, count, B, maxb, s);
+  eot_forward(ctx, E, images, B, E.nms1_boxes, E.nms1_count, params, step, gimg0, s);
+  const int S = ctx->mc.image_size;
+  PHX_HIP(hipMemcpyAsync(out_images, E.patched, (size_t)B * S * S * 12, hipMemcpyDeviceToDevice, s));
+  if (placements) {
+    std::vector<BoxPlace> hp((size_t)B * PHX_MAX_OUT);
+    PHX_HIP(hipStreamSynchronize(s));
+    PHX_HIP(hipMemcpy(hp.data(), E.place, hp.size() * sizeof(BoxPlace), hipMemcpyDeviceToHost));
+    std::vector<float> pl((size_t)B * maxb * 8, 0.f);
+    for (int b = 0; b < B; ++b)
+      for (int k = 0; k < maxb; ++k) {
+        const BoxPlace& P = hp[(size_t)b * PHX_MAX_OUT + k];
+        float* o = &pl[((size_t)b * maxb + k) * 8];
+        o[0] = (float)P.ymin; o[1] = (float)P.xmin; o[2] = (float)P.ps; o[3] = (float)P.diag;
+        o[4] = P.angle; o[5] = P.delta; o[6] = (float)P.valid; o[7] = 0.f;
+      }
+    PHX_HIP(hipMemcpy(placements, pl.data(), pl.size() * 4, hipMemcpyHostToDevice));
+  }
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
+                  const int32_t* count, int maxb, const float* params, int64_t step, int gimg0,
+                  int add_tv, float* grad, float* metrics, void* stream) {
+  if (!ctx || !images || !params || !grad || !metrics) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  check_ready(ctx, B);
+  hipStream_t s = (hipStream_t)stream;
+  Exec& E = ctx->exec_for(B);
+  ctx->last = &E;
+  PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
+  // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
+  run_forward(ctx, E, images, s);
+  run_pre_nms(ctx, E, s);
+  run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
+  launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
+  if (boxes) {
+    if (!count) throw std::invalid_argument("boxes without count");
+    stage_boxes(E, boxes, count, B, maxb, s);  // injected placement boxes
+  }
+  // 2. EOT paste
+  eot_forward(ctx, E, images, B, E.nms1_boxes, E.nms1_count, params, step, gimg0, s);
+  launch_eot_count(E.ed, E.place, metrics, s);
+  // 3. second pass + loss
+  run_forward(ctx, E, E.patched, s);
+  run_pre_nms(ctx, E, s);
+  launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, s);
+  launch_loss(E.mraw, B, params, E.dm, grad, metrics, s);
+  // 4. victim data-gradient -> d(patched images)
+  run_backward(ctx, E, E.patched, s);
+  // 5. ASR metric: soft-NMS over second-pass person boxes (attacker.py:203-205)
+  run_nms(ctx, E, 1, E.nms2_boxes, E.nms2_scores, E.nms2_count, s);
+  launch_count_ge(E.nms2_scores, E.nms2_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_NUM, s);
+  // 6. EOT backward -> d patch (+ TV)
+  EotDims d = E.ed;
+  d.B = B;
+  const float* dimg = E.gptr(E.prog.input);
+  launch_eot_rot_bwd(d, dimg, E.owner, E.place, E.rstore, E.dstore, s);
+  launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.dmatched, s);
+  launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
+  launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_adam_clip(phx_ctx* ctx, float* params, const float* grad, float* m, float* v, float lr,
+                  int64_t t, void* stream) {
+  if (!params || !grad || !m || !v || t < 1) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  launch_adam_clip(params, grad, m, v, PHX_NPARAM, lr, t, (hipStream_t)stream);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_debug_last_patched(phx_ctx* ctx, float* out, void* stream) {
+  if (!ctx || !out || ctx->execs.empty()) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->last) throw std::logic_error("no step has run");
+  Exec& E = *ctx->last;
+  const int S = ctx->mc.image_size;
+  PHX_HIP(hipMemcpyAsync(out, E.patched, (size_t)E.B * S * S * 12, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_debug_last_maxscores(phx_ctx* ctx, float* m, int32_t* anchor, void* stream) {
+  if (!ctx || ctx->execs.empty()) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->last) throw std::logic_error("no step has run");
+  Exec& E = *ctx->last;
+  hipStream_t s = (hipStream_t)stream;
+  if (m) PHX_HIP(hipMemcpyAsync(m, E.mraw, E.B * 4, hipMemcpyDeviceToDevice, s));
+  if (anchor) PHX_HIP(hipMemcpyAsync(anchor, E.argm, E.B * 4, hipMemcpyDeviceToDevice, s));
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// kernels.hpp — host launchers of the phx HIP kernels.  All launches are asynchronous on the
+// given stream and never allocate.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace phx {
+
+// ---- convolutions (kernels_conv.hip) ------------------------------------------------------
+// 3x3 stride-2 stem, Cin = 3: x [B,H,W,3] -> y [B,Ho,Wo,Co]; w [3,3,3,Co] (HWIO)
+void launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
+                     int Co, int pt, int pl, hipStream_t s);
+// dx [B,H,W,3] (+)= conv_transpose(dy)
+void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
+                     int Wo, int Co, int pt, int pl, bool acc, hipStream_t s);
+// C[M,N] (+)= A[M,K] * B + bias ; B given as Bt[N][K].  rowscale (optional): A[m,k] is
+// multiplied by rowscale[(m / rows_per_img) * K + k] (SE excitation folded into the load).
+void launch_gemm(const float* A, const float* Bt, const float* bias, float* C, int M, int N, int K,
+                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s);
+// depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
+void launch_dw_fwd(const float* x, const float* w, float* y, int B, int H, int W, int C, int Ho,
+                   int Wo, int k, int stride, int pt, int pl, hipStream_t s);
+void launch_dw_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
+                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s);
+void launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);
+
+// ---- normalisation / elementwise (kernels_norm.hip) ---------------------------------------
+// Per-channel batch statistics of y [M,C]: writes mean/rstd (float) and updates moving stats
+// (momentum 0.99, util_keras.py:33-35) when mmean != nullptr.  part: scratch (doubles).
+size_t bn_stats_scratch_doubles(long M, int C);
+void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
+                     float* mmean, float* mvar, float eps, hipStream_t s);
+// frozen BN: mean/rstd from moving statistics
+void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd, int C,
+                            float eps, hipStream_t s);
+// a = act(gamma * (y - mean) * rstd + beta)
+void launch_bn_apply(const float* y, const float* mean, const float* rstd, const float* gamma,
+                     const float* beta, float* a, long M, int C, int act, hipStream_t s);
+// BN backward, training mode.  Sums over M of dz and dz*xhat (dz = da * act'(z)) then
+// dy (+)= gamma*rstd*(dz - mean(dz) - xhat*mean(dz*xhat)).  frozen: dy = gamma*rstd*dz.
+void launch_bn_bwd(const float* da, const float* y, const float* mean, const float* rstd,
+                   const float* gamma, const float* beta, float* dy, long M, int C, int act,
+                   bool frozen, bool acc, double* part, float* coef, hipStream_t s);
+// squeeze-excite forward: pool[B,C] = mean_hw(x); scale[B,C]; y = x * scale
+void launch_se_fwd(const float* x, float* y, int B, int HW, int C, int Cse, const float* w1,
+                   const float* b1, const float* w2, const float* b2, int act, float* pool,
+                   float* hidden, float* scale, hipStream_t s);
+void launch_se_bwd(const float* dy, const float* x, float* dx, int B, int HW, int C, int Cse,
+                   const float* w1, const float* b1, const float* w2, const float* b2, int act,
+                   const float* pool, const float* hidden, const float* scale, float* gsum,
+                   bool acc, hipStream_t s);
+void launch_add(const float* a, const float* b, float* y, long n, hipStream_t s);
+// dst (+)= src
+void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s);
+void launch_maxpool_fwd(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+                        int k, int stride, int pt, int pl, hipStream_t s);
+void launch_maxpool_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
+                        int Ho, int Wo, int k, int stride, int pt, int pl, bool acc,
+                        hipStream_t s);
+void launch_upsample_fwd(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+                         hipStream_t s);
+void launch_upsample_bwd(const float* dy, float* dx, int B, int H, int W, int C, int Ho, int Wo,
+                         bool acc, hipStream_t s);
+// BiFPN fuse: y = act(sum_i x_i * w_i / (sum_j w_j + 1e-4)) (fastattn, w = relu(wsm)) or
+// act(sum_i x_i) (method 1)
+void launch_fuse_fwd(const float* const* xs, int nin, const float* wsm0, const float* wsm1,
+                     const float* wsm2, int method, int act, float* y, long n, hipStream_t s);
+void launch_fuse_bwd(const float* const* xs, int nin, const float* wsm0, const float* wsm1,
+                     const float* wsm2, int method, int act, const float* dy, float* const* dxs,
+                     const bool* acc, long n, hipStream_t s);
+
+// ---- detection post-processing (kernels_post.hip) -----------------------------------------
+struct LevelDesc {
+  long cls_off;   // float offset of the level's class output (relative to base)
+  long box_off;
+  int h, w;
+  int anchor0;    // first anchor index of this level
+};
+// pre_nms (postprocess.py:119-156) + person/validity filter (attacker.py:69-89, 105-113)
+// outputs per anchor: score, class, box; keep flag (bit0 = person&valid, bit1 = >= thresh)
+void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
+                    int nlev, const float* anchors, int A, int B, int nclass, int na,
+                    float img_h, float img_w, float thresh, float* scores, int* classes,
+                    float* boxes, uint8_t* keep, hipStream_t s);
+// soft-NMS (NonMaxSuppressionV5, gaussian) per image over candidates selected by keep&mask
+void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
+                     const int* count, int B, int N, float score_thresh, float soft_sigma,
+                     int max_out, float clip_hi, float* out_boxes, float* out_scores,
+                     int* out_count, float* work_score, int* work_sb, hipStream_t s);
+// per-image m_b = max(max_{keep} score, 0), tie count, and loss-gradient coefficient
+void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m,
+                      int* argmax, int* nties, hipStream_t s);
+}  // namespace phx

@@ -1,0 +1,805 @@
+// kernels_eot.hip — the expectation-over-transformation patch pipeline (Patcher,
+// attacker.py:344-498; BrightnessMatcher, brightness_matcher.py:14-73) forward and backward,
+// TV loss and the Adam update.
+//
+// Layout / parallelisation (MI355X-first, not the reference's map_fn x while_loop):
+//   * placement of every (image, box) slot in one tiny kernel; a compact list of valid boxes and
+//     a prefix of their pixel chunks lets the per-box kernels run as ONE launch whose workgroups
+//     walk (box, chunk) work items — no per-box launches, no host round trip, graph-capturable.
+//   * the sequential paste loop becomes a per-pixel fold: every output pixel walks the boxes of
+//     its image in order (v <- clip(r_k < -1 ? v : r_k)), so overlapping pastes compose exactly
+//     as the reference's tensor_scatter_nd_update chain, with full pixel parallelism.  The fold
+//     records the owning box per pixel/channel, which is all the backward needs.
+//   * the rotation gradient is TF's registered rule for ImageProjectiveTransformV3: an inverse
+//     warp of the upstream gradient with fill 0 (not the exact adjoint) [TF-recall].
+//   * resize is TF ScaleAndTranslate (triangle kernel, antialias, half-pixel centres, span
+//     weights normalised) with its exact adjoint in the backward.
+// Ops that decide discrete geometry follow TF's fp32 operation order with FMA contraction off.
+#include "common.hpp"
+#include "post.hpp"
+
+#pragma clang fp contract(off)
+
+namespace phx {
+
+// ------------------------------------------------------------------------------------------
+// RNG helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 rng(uint64_t seed, uint32_t c0, uint32_t c1, uint32_t c2,
+                                     int64_t step, uint32_t stream) {
+  return philox4x32_10(u32x4{c0, c1, c2, (uint32_t)((uint64_t)step << 8) | stream},
+                       (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+// tf.random.uniform(minval, maxval): u * (maxval - minval) + minval
+__device__ __forceinline__ float runif(uint32_t v, float lo, float hi) {
+  return u01(v) * (hi - lo) + lo;
+}
+// tf.random.normal(mean, stddev): z * stddev + mean, z by Box-Muller
+__device__ __forceinline__ float rnorm(uint32_t a, uint32_t b, float mean, float sd) {
+  float u1 = u01_open0(a), u2 = u01(b);
+  float z = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+  return z * sd + mean;
+}
+
+// ------------------------------------------------------------------------------------------
+// placement (Patcher.create, attacker.py:448-488) + print params + span tables
+// ------------------------------------------------------------------------------------------
+// workspace layout for the compact lists lives right after `place` (see EotLists below)
+struct EotLists {
+  int nvalid;
+  int total_chunks;
+};
+
+__global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __restrict__ boxes,
+                                                   const int* __restrict__ count,
+                                                   const float* __restrict__ params,
+                                                   uint64_t seed, int64_t step, int gimg0,
+                                                   ImgParams* __restrict__ img,
+                                                   BoxPlace* __restrict__ place,
+                                                   int* __restrict__ lists, int* __restrict__ err) {
+  const int t = threadIdx.x;
+  const float scale = params[PHX_NPATCH_DEV];
+  const float Hf = (float)d.H, Wf = (float)d.W;
+  for (int b = t; b < d.B; b += blockDim.x) {
+    u32x4 r = rng(seed, 0, 0, (uint32_t)(gimg0 + b), step, RNG_PRINT);
+    u32x4 r2 = rng(seed, 1, 0, (uint32_t)(gimg0 + b), step, RNG_PRINT);
+    u32x4 r3 = rng(seed, 2, 0, (uint32_t)(gimg0 + b), step, RNG_PRINT);
+    ImgParams p;
+    p.w[0] = rnorm(r.x, r.y, 0.5f, 0.1f);
+    p.w[1] = rnorm(r.z, r.w, 0.5f, 0.1f);
+    p.w[2] = rnorm(r2.x, r2.y, 0.5f, 0.1f);
+    p.b[0] = rnorm(r2.z, r2.w, 0.0f, 0.01f);
+    p.b[1] = rnorm(r3.x, r3.y, 0.0f, 0.01f);
+    p.b[2] = rnorm(r3.z, r3.w, 0.0f, 0.01f);
+    img[b] = p;
+  }
+  const int nslot = d.B * d.maxb;
+  for (int sl = t; sl < nslot; sl += blockDim.x) {
+    const int b = sl / d.maxb, k = sl % d.maxb;
+    BoxPlace P{};
+    P.valid = 0;
+    if (k < count[b]) {
+      const float* bx = boxes + (long)sl * 4;
+      const float ymin = bx[0], xmin = bx[1], ymax = bx[2], xmax = bx[3];
+      const float h = ymax - ymin, w = xmax - xmin;
+      const float longer = fmaxf(h, w);
+      const float psf = floorf(longer * scale);
+      const float diag = fminf(1.41421354f * psf, Wf);
+      u32x4 r = rng(seed, 0, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_PLACE);
+      const float tol = 0.2f;
+      const float oy = (ymin + h / 2.0f) + runif(r.x, (-tol * h) / 2.0f, (tol * h) / 2.0f);
+      const float ox = (xmin + w / 2.0f) + runif(r.y, (-tol * w) / 2.0f, (tol * w) / 2.0f);
+      float yp = fmaxf(oy - diag / 2.0f, 0.0f);
+      float xp = fmaxf(ox - diag / 2.0f, 0.0f);
+      if (yp + diag > Hf) yp = Hf - diag;
+      if (xp + diag > Wf) xp = Wf - diag;
+      P.ymin = (int)yp;
+      P.xmin = (int)xp;
+      P.ps = (int)psf;
+      P.diag = (int)diag;
+      P.valid = (psf * psf > 4.0f) && P.ps <= d.span_stride ? 1 : 0;
+      // attacker.py:430-433: top = left = floor((diag - ps) / 2)
+      P.pad = (P.diag - P.ps) >= 0 ? (P.diag - P.ps) / 2 : -(((P.ps - P.diag) + 1) / 2);
+      u32x4 q = rng(seed, 1, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_BOX);
+      P.delta = runif(q.x, -0.3f, 0.3f);
+      const float amax = 0.34906584f;  // float32(20 * pi / 180)
+      P.angle = runif(q.y, -amax, amax);
+      // tfa.image.angles_to_projective_transforms (fp32)
+      const float side = (float)P.diag;
+      const float c = cosf(P.angle), s = sinf(P.angle);
+      const float xo = ((side - 1.0f) - (c * (side - 1.0f) - s * (side - 1.0f))) / 2.0f;
+      const float yo = ((side - 1.0f) - (s * (side - 1.0f) + c * (side - 1.0f))) / 2.0f;
+      P.fwd[0] = c; P.fwd[1] = -s; P.fwd[2] = xo;
+      P.fwd[3] = s; P.fwd[4] = c;  P.fwd[5] = yo;
+      // inverse (gradient transform, image_ops _image_projective_transform_v3_grad)
+      double a = c, bb = -s, tx = xo, dd = s, e = c, ty = yo;
+      double det = a * e - bb * dd;
+      P.inv[0] = (float)(e / det);
+      P.inv[1] = (float)(-bb / det);
+      P.inv[2] = (float)((bb * ty - e * tx) / det);
+      P.inv[3] = (float)(-dd / det);
+      P.inv[4] = (float)(a / det);
+      P.inv[5] = (float)((dd * tx - a * ty) / det);
+    }
+    place[sl] = P;
+  }
+  __syncthreads();
+  // serial prefix: R offsets, compact valid list, per-image lists, chunk prefix
+  if (t == 0) {
+    int* nvalid = lists;                 // [1]
+    int* total_chunks = lists + 1;       // [1]
+    int* img_n = lists + 2;              // [B]
+    int* img_first = img_n + d.B;        // [B]  index into vlist of the image's first box
+    int* vlist = img_first + d.B;        // [B*maxb] slot ids
+    int* cprefix = vlist + nslot;        // [B*maxb+1] chunk prefix over vlist
+    long off = 0;
+    int nv = 0, nch = 0;
+    int e = 0;
+    for (int b = 0; b < d.B; ++b) {
+      img_first[b] = nv;
+      int cnt = 0;
+      for (int k = 0; k < d.maxb; ++k) {
+        BoxPlace& P = place[b * d.maxb + k];
+        if (!P.valid) continue;
+        long need = (long)P.ps * P.ps * 3;
+        if (off + need > d.rcap) {
+          P.valid = 0;
+          e = 1;
+          continue;
+        }
+        P.roff = off;
+        off += need;
+        vlist[nv] = b * d.maxb + k;
+        cprefix[nv] = nch;
+        nch += (P.ps * P.ps + 255) / 256;
+        ++nv;
+        ++cnt;
+      }
+      img_n[b] = cnt;
+    }
+    cprefix[nv] = nch;
+    *nvalid = nv;
+    *total_chunks = nch;
+    if (err) *err = e;
+  }
+}
+
+// TF ScaleAndTranslate span computation (ComputeSpansCore, triangle kernel, antialias=True,
+// translate=0) for output index i of a resize input_size -> ps.
+__device__ __forceinline__ void tf_span(int i, int ps, int in_size, SpanEntry* out) {
+  const float scale = (float)ps / (float)in_size;
+  const float inv_scale = (float)(1.0 / (double)scale);
+  const float kscale = fmaxf(inv_scale, 1.0f);
+  const float one_over_k = 1.0f / kscale;
+  const float radius = 1.0f;
+  const float sample_f = ((float)i + 0.5f) * inv_scale + (-inv_scale * 0.0f);
+  long start = (long)ceilf(sample_f - radius * kscale - 0.5f);
+  long end = (long)floorf(sample_f + radius * kscale - 0.5f);
+  start = start < 0 ? 0 : (start > in_size - 1 ? in_size - 1 : start);
+  end = (end < 0 ? 0 : (end > in_size - 1 ? in_size - 1 : end)) + 1;
+  float total = 0.0f;
+  for (long src = start; src < end; ++src) {
+    float pos = (float)src + 0.5f - sample_f;
+    float x = fabsf(pos * one_over_k);
+    total += x < 1.0f ? 1.0f - x : 0.0f;
+  }
+  out->start = (int)start;
+  out->end = (int)end;
+  out->inv_total = fabsf(total) >= 1000.0f * 1.17549435e-38f ? 1.0f / total : 0.0f;
+  out->sample_f = sample_f;
+}
+
+__device__ __forceinline__ float span_weight(const SpanEntry& sp, int src, float one_over_k) {
+  float pos = (float)src + 0.5f - sp.sample_f;
+  float x = fabsf(pos * one_over_k);
+  float w = x < 1.0f ? 1.0f - x : 0.0f;
+  return w * sp.inv_total;
+}
+
+__global__ __launch_bounds__(256) void k_eot_spans(EotDims d, const BoxPlace* __restrict__ place,
+                                                   SpanEntry* __restrict__ spans) {
+  const int sl = blockIdx.y;
+  const BoxPlace& P = place[sl];
+  if (!P.valid) return;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < P.ps; i += gridDim.x * blockDim.x)
+    tf_span(i, P.ps, d.P, &spans[(long)sl * d.span_stride + i]);
+}
+
+void launch_eot_place(const EotDims& d, const float* boxes, const int* count, const float* params,
+                      uint64_t seed, int64_t step, int gimg0, ImgParams* img, BoxPlace* place,
+                      SpanEntry* spans, int* err, hipStream_t s) {
+  int* lists = reinterpret_cast<int*>(place + (long)d.B * d.maxb);
+  hipLaunchKernelGGL(k_eot_place, dim3(1), dim3(256), 0, s, d, boxes, count, params, seed, step,
+                     gimg0, img, place, lists, err);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_spans, dim3(2, d.B * d.maxb), dim3(256), 0, s, d, place, spans);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// brightness matcher (brightness_matcher.py:43-73), fused with the print variation
+// ------------------------------------------------------------------------------------------
+struct Yuv {
+  float y, u, v;
+};
+__device__ __forceinline__ Yuv rgb2yuv(float r, float g, float b) {
+  Yuv o;
+  o.y = r * 0.299f + g * 0.587f + b * 0.114f;
+  o.u = r * -0.14714119f + g * -0.28886916f + b * 0.43601035f;
+  o.v = r * 0.61497538f + g * -0.51496512f + b * -0.10001026f;
+  return o;
+}
+constexpr float kTo01 = 127.0f / 255.0f;   // _rescale_0_1 constant
+constexpr float kBack = 255.0f / 127.0f;   // _rescale_back constant
+
+__device__ __forceinline__ float print_px(const float* patch, const ImgParams& p, long e, int c,
+                                          bool apply) {
+  float x = patch[e];
+  if (!apply) return x;
+  float v = p.w[c] * x + p.b[c];
+  return fminf(fmaxf(v, -1.0f), 1.0f);
+}
+
+// partial sums of Y: z = 0 source (printed patch), z = 1 target (image)
+__global__ __launch_bounds__(256) void k_eot_ysum(EotDims d, const float* __restrict__ src,
+                                                  long src_stride, const ImgParams* __restrict__ img,
+                                                  const float* __restrict__ tgt, int apply,
+                                                  double* __restrict__ ysum) {
+  const int b = blockIdx.y, z = blockIdx.z;
+  const long npx = z == 0 ? (long)d.P * d.P : (long)d.H * d.W;
+  const ImgParams p = img ? img[b] : ImgParams{};
+  const float* base = z == 0 ? src + (long)b * src_stride : tgt + (long)b * d.H * d.W * 3;
+  double acc = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < npx;
+       i += (long)gridDim.x * blockDim.x) {
+    float r, g, bl;
+    if (z == 0) {
+      r = (print_px(base, p, i * 3 + 0, 0, apply) + 1.0f) * kTo01;
+      g = (print_px(base, p, i * 3 + 1, 1, apply) + 1.0f) * kTo01;
+      bl = (print_px(base, p, i * 3 + 2, 2, apply) + 1.0f) * kTo01;
+    } else {
+      r = (base[i * 3 + 0] + 1.0f) * kTo01;
+      g = (base[i * 3 + 1] + 1.0f) * kTo01;
+      bl = (base[i * 3 + 2] + 1.0f) * kTo01;
+    }
+    acc += rgb2yuv(r, g, bl).y;
+  }
+  __shared__ double sh[256];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) ysum[((long)b * 2 + z) * gridDim.x + blockIdx.x] = sh[0];
+}
+
+__global__ void k_eot_ymean(EotDims d, const double* __restrict__ ysum, int chunks,
+                            float* __restrict__ ymean) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.B * 2) return;
+  double s = 0.0;
+  for (int k = 0; k < chunks; ++k) s += ysum[(long)i * chunks + k];
+  const long npx = (i % 2) == 0 ? (long)d.P * d.P : (long)d.H * d.W;
+  ymean[i] = (float)(s / (double)npx);
+}
+
+__device__ __forceinline__ void match_px(float p0, float p1, float p2, float mus, float mut,
+                                         float* o) {
+  Yuv s = rgb2yuv((p0 + 1.0f) * kTo01, (p1 + 1.0f) * kTo01, (p2 + 1.0f) * kTo01);
+  float yc = (s.y - mus) + mut;
+  float yp = fminf(fmaxf(yc, 0.0f), 1.0f);
+  float r = yp + 1.13988303f * s.v;
+  float g = yp + -0.394642334f * s.u + -0.58062185f * s.v;
+  float bl = yp + 2.03206185f * s.u;
+  o[0] = fminf(fmaxf(r, 0.0f), 1.0f) * kBack - 1.0f;
+  o[1] = fminf(fmaxf(g, 0.0f), 1.0f) * kBack - 1.0f;
+  o[2] = fminf(fmaxf(bl, 0.0f), 1.0f) * kBack - 1.0f;
+}
+
+__global__ __launch_bounds__(256) void k_eot_match(EotDims d, const float* __restrict__ src,
+                                                   long src_stride, const ImgParams* __restrict__ img,
+                                                   const float* __restrict__ ymean, int apply,
+                                                   float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const long npx = (long)d.P * d.P;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npx) return;
+  const ImgParams p = img ? img[b] : ImgParams{};
+  const float* base = src + (long)b * src_stride;
+  float o[3];
+  match_px(print_px(base, p, i * 3, 0, apply), print_px(base, p, i * 3 + 1, 1, apply),
+           print_px(base, p, i * 3 + 2, 2, apply), ymean[b * 2], ymean[b * 2 + 1], o);
+  float* op = out + ((long)b * npx + i) * 3;
+  op[0] = o[0]; op[1] = o[1]; op[2] = o[2];
+}
+
+static constexpr int kYChunks = 64;
+
+void launch_eot_match(const EotDims& d, const float* patch, const ImgParams* img, const float* tgt,
+                      float* matched, double* ysum, float* ymean, bool apply_print,
+                      hipStream_t s) {
+  // apply_print: one shared patch + per-image print params; otherwise `patch` holds one
+  // source image per batch entry.
+  long stride = apply_print ? 0 : (long)d.P * d.P * 3;
+  hipLaunchKernelGGL(k_eot_ysum, dim3(kYChunks, d.B, 2), dim3(256), 0, s, d, patch, stride, img,
+                     tgt, apply_print ? 1 : 0, ysum);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_ymean, dim3(cdiv(d.B * 2, 64)), dim3(64), 0, s, d, ysum, kYChunks,
+                     ymean);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_match, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d, patch,
+                     stride, img, ymean, apply_print ? 1 : 0, matched);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// per-box kernels walk (valid box, 256-pixel chunk) work items
+// ------------------------------------------------------------------------------------------
+struct ListView {
+  const int* nvalid;
+  const int* total_chunks;
+  const int* img_n;
+  const int* img_first;
+  const int* vlist;
+  const int* cprefix;
+};
+
+__device__ __forceinline__ ListView lists_of(const EotDims& d, const BoxPlace* place) {
+  const int* l = reinterpret_cast<const int*>(place + (long)d.B * d.maxb);
+  ListView v;
+  v.nvalid = l;
+  v.total_chunks = l + 1;
+  v.img_n = l + 2;
+  v.img_first = v.img_n + d.B;
+  v.vlist = v.img_first + d.B;
+  v.cprefix = v.vlist + d.B * d.maxb;
+  return v;
+}
+
+// binary search: largest v with cprefix[v] <= item
+__device__ __forceinline__ int find_box(const int* cprefix, int nv, int item) {
+  int lo = 0, hi = nv - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (cprefix[mid] <= item) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+constexpr int kBoxGrid = 2048;
+
+// resize (+noise +brightness): R_pre[i,j,c] = sum_y Wr[i,y] sum_x Wc[j,x] m[y,x,c] + n + delta
+__global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __restrict__ matched,
+                                                    const BoxPlace* __restrict__ place,
+                                                    const SpanEntry* __restrict__ spans,
+                                                    uint64_t seed, int64_t step, int gimg0,
+                                                    float* __restrict__ rstore) {
+  const ListView L = lists_of(d, place);
+  const int nv = *L.nvalid, total = *L.total_chunks;
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int v = find_box(L.cprefix, nv, item);
+    const int sl = L.vlist[v];
+    const BoxPlace P = place[sl];
+    const int b = sl / d.maxb, k = sl % d.maxb;
+    const int px = (item - L.cprefix[v]) * 256 + threadIdx.x;
+    if (px >= P.ps * P.ps) continue;
+    const int i = px / P.ps, j = px % P.ps;
+    const SpanEntry si = spans[(long)sl * d.span_stride + i];
+    const SpanEntry sj = spans[(long)sl * d.span_stride + j];
+    const float scale = (float)P.ps / (float)d.P;
+    const float inv_scale = (float)(1.0 / (double)scale);
+    const float one_over_k = 1.0f / fmaxf(inv_scale, 1.0f);
+    const float* m = matched + (long)b * d.P * d.P * 3;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int y = si.start; y < si.end; ++y) {
+      const float wy = span_weight(si, y, one_over_k);
+      float c0 = 0.f, c1 = 0.f, c2 = 0.f;
+      const float* row = m + (long)y * d.P * 3;
+      for (int x = sj.start; x < sj.end; ++x) {
+        const float wx = span_weight(sj, x, one_over_k);
+        c0 += wx * row[x * 3 + 0];
+        c1 += wx * row[x * 3 + 1];
+        c2 += wx * row[x * 3 + 2];
+      }
+      a0 += wy * c0;
+      a1 += wy * c1;
+      a2 += wy * c2;
+    }
+    u32x4 r = rng(seed, (uint32_t)px, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_NOISE);
+    float* o = rstore + P.roff + (long)px * 3;
+    o[0] = (a0 + runif(r.x, -0.01f, 0.01f)) + P.delta;
+    o[1] = (a1 + runif(r.y, -0.01f, 0.01f)) + P.delta;
+    o[2] = (a2 + runif(r.z, -0.01f, 0.01f)) + P.delta;
+  }
+}
+
+void launch_eot_resize(const EotDims& d, const float* matched, const BoxPlace* place,
+                       const SpanEntry* spans, uint64_t seed, int64_t step, int gimg0,
+                       float* rstore, hipStream_t s) {
+  hipLaunchKernelGGL(k_eot_resize, dim3(kBoxGrid), dim3(256), 0, s, d, matched, place, spans, seed,
+                     step, gimg0, rstore);
+  PHX_LAUNCH_CHECK();
+}
+
+// padded, clipped R sample: inside the ps x ps block -> clip(pre), pad / outside -> -2
+__device__ __forceinline__ float rread(const float* R, const BoxPlace& P, int yy, int xx, int c) {
+  int ry = yy - P.pad, rx = xx - P.pad;
+  if (yy < 0 || yy >= P.diag || xx < 0 || xx >= P.diag) return -2.0f;
+  if (ry < 0 || ry >= P.ps || rx < 0 || rx >= P.ps) return -2.0f;
+  float v = R[((long)ry * P.ps + rx) * 3 + c];
+  return fminf(fmaxf(v, -1.0f), 1.0f);
+}
+
+// TF ImageProjectiveTransform bilinear sample (fill_value for out-of-range taps)
+template <typename Read>
+__device__ __forceinline__ float tf_bilinear(float x, float y, Read rd) {
+  const float y_floor = floorf(y), x_floor = floorf(x);
+  const float y_ceil = y_floor + 1.0f, x_ceil = x_floor + 1.0f;
+  const int yf = (int)y_floor, xf = (int)x_floor, yc = (int)y_ceil, xc = (int)x_ceil;
+  const float v_yf = (x_ceil - x) * rd(yf, xf) + (x - x_floor) * rd(yf, xc);
+  const float v_yc = (x_ceil - x) * rd(yc, xf) + (x - x_floor) * rd(yc, xc);
+  return (y_ceil - y) * v_yf + (y - y_floor) * v_yc;
+}
+
+__global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* __restrict__ img_in,
+                                                       const BoxPlace* __restrict__ place,
+                                                       const float* __restrict__ rstore,
+                                                       float* __restrict__ img_out,
+                                                       int16_t* __restrict__ owner) {
+  const long npx = (long)d.H * d.W;
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)d.B * npx) return;
+  const int b = (int)(idx / npx);
+  const int p = (int)(idx % npx);
+  const int y = p / d.W, x = p % d.W;
+  const ListView L = lists_of(d, place);
+  const float* ip = img_in + idx * 3;
+  float v[3] = {ip[0], ip[1], ip[2]};
+  int16_t own[3] = {-1, -1, -1};
+  const int n = L.img_n[b], f = L.img_first[b];
+  for (int q = 0; q < n; ++q) {
+    const int sl = L.vlist[f + q];
+    const BoxPlace& P = place[sl];
+    const int qy = y - P.ymin, qx = x - P.xmin;
+    if (qy < 0 || qy >= P.diag || qx < 0 || qx >= P.diag) continue;
+    const float ox = (float)qx, oy = (float)qy;
+    const float proj = 0.0f * ox + 0.0f * oy + 1.0f;
+    const float inx = (P.fwd[0] * ox + P.fwd[1] * oy + P.fwd[2]) / proj;
+    const float iny = (P.fwd[3] * ox + P.fwd[4] * oy + P.fwd[5]) / proj;
+    const float* R = rstore + P.roff;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float r = tf_bilinear(inx, iny, [&](int yy, int xx) { return rread(R, P, yy, xx, c); });
+      if (r < -1.0f) {
+        v[c] = fminf(fmaxf(v[c], -1.0f), 1.0f);
+      } else {
+        v[c] = fminf(fmaxf(r, -1.0f), 1.0f);
+        own[c] = (int16_t)(sl % d.maxb);
+      }
+    }
+  }
+  float* op = img_out + idx * 3;
+  op[0] = v[0]; op[1] = v[1]; op[2] = v[2];
+  if (owner) {
+    owner[idx * 3 + 0] = own[0];
+    owner[idx * 3 + 1] = own[1];
+    owner[idx * 3 + 2] = own[2];
+  }
+}
+
+void launch_eot_composite(const EotDims& d, const float* img_in, const BoxPlace* place,
+                          const float* rstore, float* img_out, int16_t* owner, hipStream_t s) {
+  long n = (long)d.B * d.H * d.W;
+  hipLaunchKernelGGL(k_eot_composite, dim3(cdiv(n, 256)), dim3(256), 0, s, d, img_in, place, rstore,
+                     img_out, owner);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// backward
+// ------------------------------------------------------------------------------------------
+// dR_pre[i,j,c] = [-1 <= pre <= 1] * bilinear(inverse transform, G_k, fill 0) at padded
+// (i+pad, j+pad), where G_k = dimg restricted to pixels owned by box k.
+__global__ __launch_bounds__(256) void k_eot_rot_bwd(EotDims d, const float* __restrict__ dimg,
+                                                     const int16_t* __restrict__ owner,
+                                                     const BoxPlace* __restrict__ place,
+                                                     const float* __restrict__ rstore,
+                                                     float* __restrict__ dstore) {
+  const ListView L = lists_of(d, place);
+  const int nv = *L.nvalid, total = *L.total_chunks;
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int v = find_box(L.cprefix, nv, item);
+    const int sl = L.vlist[v];
+    const BoxPlace P = place[sl];
+    const int b = sl / d.maxb, k = sl % d.maxb;
+    const int px = (item - L.cprefix[v]) * 256 + threadIdx.x;
+    if (px >= P.ps * P.ps) continue;
+    const int i = px / P.ps, j = px % P.ps;
+    const float ox = (float)(j + P.pad), oy = (float)(i + P.pad);
+    const float proj = 0.0f * ox + 0.0f * oy + 1.0f;
+    const float inx = (P.inv[0] * ox + P.inv[1] * oy + P.inv[2]) / proj;
+    const float iny = (P.inv[3] * ox + P.inv[4] * oy + P.inv[5]) / proj;
+    const float* R = rstore + P.roff + (long)px * 3;
+    float* o = dstore + P.roff + (long)px * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float g = tf_bilinear(inx, iny, [&](int yy, int xx) -> float {
+        if (yy < 0 || yy >= P.diag || xx < 0 || xx >= P.diag) return 0.0f;
+        long e = (((long)b * d.H + (P.ymin + yy)) * d.W + (P.xmin + xx)) * 3 + c;
+        return owner[e] == k ? dimg[e] : 0.0f;
+      });
+      float pre = R[c];
+      o[c] = (pre >= -1.0f && pre <= 1.0f) ? g : 0.0f;
+    }
+  }
+}
+
+void launch_eot_rot_bwd(const EotDims& d, const float* dimg, const int16_t* owner,
+                        const BoxPlace* place, const float* rstore, float* dstore,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_eot_rot_bwd, dim3(kBoxGrid), dim3(256), 0, s, d, dimg, owner, place, rstore,
+                     dstore);
+  PHX_LAUNCH_CHECK();
+}
+
+// exact adjoint of the antialiased resize, gathered per source pixel over the image's boxes
+__global__ __launch_bounds__(256) void k_eot_resize_bwd(EotDims d, const BoxPlace* __restrict__ place,
+                                                        const SpanEntry* __restrict__ spans,
+                                                        const float* __restrict__ dstore,
+                                                        float* __restrict__ dmatched) {
+  const int b = blockIdx.y;
+  const long npx = (long)d.P * d.P;
+  long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= npx) return;
+  const int y = (int)(p / d.P), x = (int)(p % d.P);
+  const ListView L = lists_of(d, place);
+  const int n = L.img_n[b], f = L.img_first[b];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int q = 0; q < n; ++q) {
+    const int sl = L.vlist[f + q];
+    const BoxPlace& P = place[sl];
+    const float scale = (float)P.ps / (float)d.P;
+    const float inv_scale = (float)(1.0 / (double)scale);
+    const float ks = fmaxf(inv_scale, 1.0f);
+    const float one_over_k = 1.0f / ks;
+    const SpanEntry* sp = spans + (long)sl * d.span_stride;
+    int ilo = (int)floorf(((float)y - ks - 0.5f) / inv_scale - 0.5f) - 1;
+    int ihi = (int)ceilf(((float)y + ks + 1.5f) / inv_scale - 0.5f) + 1;
+    int jlo = (int)floorf(((float)x - ks - 0.5f) / inv_scale - 0.5f) - 1;
+    int jhi = (int)ceilf(((float)x + ks + 1.5f) / inv_scale - 0.5f) + 1;
+    ilo = max(ilo, 0); jlo = max(jlo, 0);
+    ihi = min(ihi, P.ps - 1); jhi = min(jhi, P.ps - 1);
+    const float* D = dstore + P.roff;
+    for (int i = ilo; i <= ihi; ++i) {
+      const SpanEntry si = sp[i];
+      if (y < si.start || y >= si.end) continue;
+      const float wy = span_weight(si, y, one_over_k);
+      if (wy == 0.0f) continue;
+      for (int j = jlo; j <= jhi; ++j) {
+        const SpanEntry sj = sp[j];
+        if (x < sj.start || x >= sj.end) continue;
+        const float w = wy * span_weight(sj, x, one_over_k);
+        const float* g = D + ((long)i * P.ps + j) * 3;
+        a0 += w * g[0];
+        a1 += w * g[1];
+        a2 += w * g[2];
+      }
+    }
+  }
+  float* o = dmatched + ((long)b * npx + p) * 3;
+  o[0] = a0; o[1] = a1; o[2] = a2;
+}
+
+void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEntry* spans,
+                           const float* dstore, float* dmatched, hipStream_t s) {
+  hipLaunchKernelGGL(k_eot_resize_bwd, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d,
+                     place, spans, dstore, dmatched);
+  PHX_LAUNCH_CHECK();
+}
+
+// brightness-matcher backward per pixel: returns d(print output) for the 3 channels given
+// dmatched and mean(dYc); also the pixel's dYc contribution.
+struct MatchBwd {
+  float dp[3];
+  float dyc;
+};
+__device__ __forceinline__ MatchBwd match_bwd_px(const float* p, float mus, float mut,
+                                                 const float* dm, float mean_dyc) {
+  Yuv s = rgb2yuv((p[0] + 1.0f) * kTo01, (p[1] + 1.0f) * kTo01, (p[2] + 1.0f) * kTo01);
+  float yc = (s.y - mus) + mut;
+  float yp = fminf(fmaxf(yc, 0.0f), 1.0f);
+  float rgb[3] = {yp + 1.13988303f * s.v, yp + -0.394642334f * s.u + -0.58062185f * s.v,
+                  yp + 2.03206185f * s.u};
+  float drgb[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+    drgb[c] = (rgb[c] >= 0.0f && rgb[c] <= 1.0f) ? dm[c] * kBack : 0.0f;
+  float dyp = drgb[0] + drgb[1] + drgb[2];
+  float du = -0.394642334f * drgb[1] + 2.03206185f * drgb[2];
+  float dv = 1.13988303f * drgb[0] + -0.58062185f * drgb[1];
+  float dyc = (yc >= 0.0f && yc <= 1.0f) ? dyp : 0.0f;
+  float dy = dyc - mean_dyc;  // d/dY through Y - mean(Y)
+  MatchBwd o;
+  o.dyc = dyc;
+  // d s_c = dY*ky_c + dU*ku_c + dV*kv_c ; dp = ds * 127/255
+  o.dp[0] = (dy * 0.299f + du * -0.14714119f + dv * 0.61497538f) * kTo01;
+  o.dp[1] = (dy * 0.587f + du * -0.28886916f + dv * -0.51496512f) * kTo01;
+  o.dp[2] = (dy * 0.114f + du * 0.43601035f + dv * -0.10001026f) * kTo01;
+  return o;
+}
+
+__global__ __launch_bounds__(256) void k_eot_dyc_sum(EotDims d, const float* __restrict__ patch,
+                                                     const ImgParams* __restrict__ img,
+                                                     const float* __restrict__ ymean,
+                                                     const float* __restrict__ dmatched,
+                                                     double* __restrict__ dsum) {
+  const int b = blockIdx.y;
+  const long npx = (long)d.P * d.P;
+  const ImgParams ip = img[b];
+  double acc = 0.0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < npx;
+       i += (long)gridDim.x * blockDim.x) {
+    float p[3];
+    for (int c = 0; c < 3; ++c) p[c] = print_px(patch, ip, i * 3 + c, c, true);
+    MatchBwd mb = match_bwd_px(p, ymean[b * 2], ymean[b * 2 + 1],
+                               dmatched + ((long)b * npx + i) * 3, 0.0f);
+    acc += mb.dyc;
+  }
+  __shared__ double sh[256];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dsum[(long)b * gridDim.x + blockIdx.x] = sh[0];
+}
+
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__global__ __launch_bounds__(256) void k_eot_patch_grad(EotDims d, const float* __restrict__ patch,
+                                                        const ImgParams* __restrict__ img,
+                                                        const float* __restrict__ ymean,
+                                                        const float* __restrict__ dmatched,
+                                                        const double* __restrict__ dsum, int chunks,
+                                                        int add_tv, float* __restrict__ grad) {
+  const long npx = (long)d.P * d.P;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npx) return;
+  float g[3] = {0.f, 0.f, 0.f};
+  for (int b = 0; b < d.B; ++b) {
+    double s = 0.0;
+    for (int k = 0; k < chunks; ++k) s += dsum[(long)b * chunks + k];
+    const float mean_dyc = (float)(s / (double)npx);
+    const ImgParams ip = img[b];
+    float p[3], pre[3];
+    for (int c = 0; c < 3; ++c) {
+      pre[c] = ip.w[c] * patch[i * 3 + c] + ip.b[c];
+      p[c] = fminf(fmaxf(pre[c], -1.0f), 1.0f);
+    }
+    MatchBwd mb = match_bwd_px(p, ymean[b * 2], ymean[b * 2 + 1],
+                               dmatched + ((long)b * npx + i) * 3, mean_dyc);
+    for (int c = 0; c < 3; ++c)
+      if (pre[c] >= -1.0f && pre[c] <= 1.0f) g[c] += mb.dp[c] * ip.w[c];
+  }
+  if (add_tv) {
+    // d/dp of 1e-5 * (sum |p[y+1]-p[y]| + sum |p[x+1]-p[x]|), abs grad = sign
+    const int y = (int)(i / d.P), x = (int)(i % d.P);
+    for (int c = 0; c < 3; ++c) {
+      const float v = patch[i * 3 + c];
+      float t = 0.f;
+      if (y > 0) t += sgnf(v - patch[(i - d.P) * 3 + c]);
+      if (y < d.P - 1) t -= sgnf(patch[(i + d.P) * 3 + c] - v);
+      if (x > 0) t += sgnf(v - patch[(i - 1) * 3 + c]);
+      if (x < d.P - 1) t -= sgnf(patch[(i + 1) * 3 + c] - v);
+      g[c] += 1e-5f * t;
+    }
+  }
+  grad[i * 3 + 0] = g[0];
+  grad[i * 3 + 1] = g[1];
+  grad[i * 3 + 2] = g[2];
+}
+
+void launch_eot_patch_bwd(const EotDims& d, const float* patch, const ImgParams* img,
+                          const float* ymean, const float* dmatched, double* dsum, float* grad,
+                          bool add_tv, hipStream_t s) {
+  hipLaunchKernelGGL(k_eot_dyc_sum, dim3(kYChunks, d.B), dim3(256), 0, s, d, patch, img, ymean,
+                     dmatched, dsum);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_patch_grad, dim3(cdiv((long)d.P * d.P, 256)), dim3(256), 0, s, d, patch,
+                     img, ymean, dmatched, dsum, kYChunks, add_tv ? 1 : 0, grad);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// total variation (tf.image.total_variation on a 3-D image, sum over everything)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tv_part(const float* __restrict__ p, int P,
+                                                 double* __restrict__ part) {
+  const long n = (long)P * P * 3;
+  double acc = 0.0;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (long)gridDim.x * blockDim.x) {
+    long px = e / 3;
+    int y = (int)(px / P), x = (int)(px % P);
+    float v = p[e];
+    if (y + 1 < P) acc += fabsf(p[e + (long)P * 3] - v);
+    if (x + 1 < P) acc += fabsf(p[e + 3] - v);
+  }
+  __shared__ double sh[256];
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) sh[threadIdx.x] += sh[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
+}
+
+__global__ void k_tv_final(const double* __restrict__ part, int n, float* __restrict__ metrics,
+                           int add) {
+  if (threadIdx.x) return;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += part[i];
+  metrics[PHX_M_TV] = (float)s;
+  if (add) metrics[PHX_M_LOSS] += 1e-5f * (float)s;
+}
+
+void launch_tv(const float* patch, int P, double* scratch, float* metrics, bool add_to_loss,
+               hipStream_t s) {
+  const int nb = 256;
+  hipLaunchKernelGGL(k_tv_part, dim3(nb), dim3(256), 0, s, patch, P, scratch);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_tv_final, dim3(1), dim3(64), 0, s, scratch, nb, metrics, add_to_loss ? 1 : 0);
+  PHX_LAUNCH_CHECK();
+}
+
+__global__ void k_eot_count(EotDims d, const BoxPlace* __restrict__ place, float* metrics) {
+  if (threadIdx.x) return;
+  const ListView L = lists_of(d, place);
+  metrics[PHX_M_NBOX] = (float)*L.nvalid;
+}
+
+void launch_eot_count(const EotDims& d, const BoxPlace* place, float* metrics, hipStream_t s) {
+  hipLaunchKernelGGL(k_eot_count, dim3(1), dim3(64), 0, s, d, place, metrics);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// Keras Adam (ResourceApplyAdam) + constraints: params = [patch | scale]
+//   alpha = lr * sqrt(1 - b2^t) / (1 - b1^t); m += (g - m)(1 - b1); v += (g^2 - v)(1 - b2)
+//   var -= m * alpha / (sqrt(v) + eps); var = clip(var)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_adam(float* __restrict__ params,
+                                              const float* __restrict__ grad,
+                                              float* __restrict__ m, float* __restrict__ v, long n,
+                                              float alpha, long npatch) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+  float g = grad[i];
+  float mi = m[i], vi = v[i];
+  mi += (g - mi) * (1.0f - b1);
+  vi += (g * g - vi) * (1.0f - b2);
+  m[i] = mi;
+  v[i] = vi;
+  float x = params[i] - (mi * alpha) / (sqrtf(vi) + eps);
+  if (i < npatch)
+    x = fminf(fmaxf(x, -1.0f), 1.0f);
+  else
+    x = fminf(fmaxf(x, 0.0f), 1.0f);
+  params[i] = x;
+}
+
+void launch_adam_clip(float* params, const float* grad, float* m, float* v, long n, float lr,
+                      int64_t t, hipStream_t s) {
+  // beta powers as Keras: pow(beta, t) in fp32
+  const float b1p = powf(0.9f, (float)t), b2p = powf(0.999f, (float)t);
+  const float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+  hipLaunchKernelGGL(k_adam, dim3(cdiv(n, 256)), dim3(256), 0, s, params, grad, m, v, n, alpha,
+                     (long)PHX_NPATCH_DEV);
+  PHX_LAUNCH_CHECK();
+}
+
+}  // namespace phx

@@ -1,0 +1,418 @@
+// kernels_post.hip — detection post-processing on the attack path:
+//   pre_nms            automl/efficientdet/tf2/postprocess.py:67-156 (level merge, per-anchor class
+//                      max/argmax, box decode anchors.py:30-58, sigmoid)
+//   person/valid mask  attacker.py:69-89, 105-113, 132-140
+//   soft-NMS           postprocess.py:159-205 -> tf.raw_ops.NonMaxSuppressionV5 (gaussian),
+//                      restated from TF's non_max_suppression_op.cc [TF-recall]
+//   loss               attacker.py:189-193 and its gradient (ragged reduce_max, maximum(.,0))
+// Arithmetic that decides discrete outcomes (masks, thresholds, argmax) is kept in TF's fp32
+// operation order with FMA contraction disabled.
+#include "common.hpp"
+#include "kernels.hpp"
+#include "post.hpp"
+
+#pragma clang fp contract(off)
+
+namespace phx {
+
+__device__ __forceinline__ float sigmoid_exact(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ------------------------------------------------------------------------------------------
+// pre_nms + masks: one lane per (image, anchor)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_base,
+                                                 const float* __restrict__ box_base,
+                                                 const LevelDesc* __restrict__ lev, int nlev,
+                                                 const float* __restrict__ anchors, int A, int B,
+                                                 int nclass, int na, float img_h, float img_w,
+                                                 float thresh, float* __restrict__ scores,
+                                                 int* __restrict__ classes,
+                                                 float* __restrict__ boxes,
+                                                 uint8_t* __restrict__ keep) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * A) return;
+  const int b = (int)(idx / A), a = (int)(idx % A);
+  int l = 0;
+  while (l + 1 < nlev && a >= lev[l + 1].anchor0) ++l;
+  const LevelDesc L = lev[l];
+  const int local = a - L.anchor0;
+  const int pix = local / na, k = local % na;
+  const long prow = (long)b * L.h * L.w + pix;
+  const float* lg = cls_base + L.cls_off + prow * (na * nclass) + (long)k * nclass;
+  float m = lg[0];
+  int am = 0;
+  for (int c = 1; c < nclass; ++c) {
+    float v = lg[c];
+    if (v > m) { m = v; am = c; }
+  }
+  const float* bx = box_base + L.box_off + prow * (na * 4) + (long)k * 4;
+  const float* an = anchors + (long)a * 4;
+  float yca = (an[0] + an[2]) / 2.0f;
+  float xca = (an[1] + an[3]) / 2.0f;
+  float ha = an[2] - an[0];
+  float wa = an[3] - an[1];
+  float ty = bx[0], tx = bx[1], th = bx[2], tw = bx[3];
+  float w = expf(tw) * wa;
+  float h = expf(th) * ha;
+  float yc = ty * ha + yca;
+  float xc = tx * wa + xca;
+  float ymin = yc - h / 2.0f, xmin = xc - w / 2.0f, ymax = yc + h / 2.0f, xmax = xc + w / 2.0f;
+  float s = sigmoid_exact(m);
+  scores[idx] = s;
+  classes[idx] = am;
+  float* ob = boxes + idx * 4;
+  ob[0] = ymin; ob[1] = xmin; ob[2] = ymax; ob[3] = xmax;
+  // filter_valid_boxes (attacker.py:69-89): boxes_h/w from the decoded box
+  float bh = ymax - ymin, bw = xmax - xmin;
+  float area = bh * bw;
+  bool valid = (bw / img_w <= 1.0f) && (bh / img_h <= 1.0f) && (area > 100.0f);
+  uint8_t kf = 0;
+  if (am == 0 && valid) {
+    kf = 1;
+    if (s >= thresh) kf |= 2;
+  }
+  keep[idx] = kf;
+}
+
+void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
+                    int nlev, const float* anchors, int A, int B, int nclass, int na,
+                    float img_h, float img_w, float thresh, float* scores, int* classes,
+                    float* boxes, uint8_t* keep, hipStream_t s) {
+  long n = (long)B * A;
+  hipLaunchKernelGGL(k_pre_nms, dim3(cdiv(n, 256)), dim3(256), 0, s, cls_base, box_base, lev_dev,
+                     nlev, anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes,
+                     keep);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// soft-NMS: one workgroup per image.  Exact restatement of NonMaxSuppressionV5's lazy
+// priority queue: pop the (score desc, index asc) maximum, decay it by every box selected
+// since its last visit (newest first, early exit at <= thresh), select if unchanged, else
+// re-queue while > thresh.  Candidate order = ragged (anchor) order.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float tf_iou(const float* bi, const float* bj) {
+  const float ymin_i = fminf(bi[0], bi[2]), xmin_i = fminf(bi[1], bi[3]);
+  const float ymax_i = fmaxf(bi[0], bi[2]), xmax_i = fmaxf(bi[1], bi[3]);
+  const float ymin_j = fminf(bj[0], bj[2]), xmin_j = fminf(bj[1], bj[3]);
+  const float ymax_j = fmaxf(bj[0], bj[2]), xmax_j = fmaxf(bj[1], bj[3]);
+  const float area_i = (ymax_i - ymin_i) * (xmax_i - xmin_i);
+  const float area_j = (ymax_j - ymin_j) * (xmax_j - xmin_j);
+  if (area_i <= 0.f || area_j <= 0.f) return 0.f;
+  const float iy0 = fmaxf(ymin_i, ymin_j), ix0 = fmaxf(xmin_i, xmin_j);
+  const float iy1 = fminf(ymax_i, ymax_j), ix1 = fminf(xmax_i, xmax_j);
+  const float inter = fmaxf(iy1 - iy0, 0.f) * fmaxf(ix1 - ix0, 0.f);
+  return inter / (area_i + area_j - inter);
+}
+
+constexpr int kNmsThreads = 256;
+
+__global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
+    const float* __restrict__ boxes, const float* __restrict__ scores,
+    const uint8_t* __restrict__ keep, int keep_mask, const int* __restrict__ count, int N,
+    float score_thresh, float scale, int max_out, float clip_hi, float* __restrict__ out_boxes,
+    float* __restrict__ out_scores, int* __restrict__ out_count, float* __restrict__ wscore,
+    int* __restrict__ wsb, int* __restrict__ widx) {
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const float* bb = boxes + (long)b * N * 4;
+  const float* sb = scores + (long)b * N;
+  float* ws = wscore + (long)b * N;
+  int* wb = wsb + (long)b * N;
+  int* wi = widx + (long)b * N;
+  const int n_in = count ? count[b] : N;
+
+  __shared__ int s_n;
+  __shared__ float sel_box[PHX_MAX_OUT_DEV][4];
+  __shared__ float sel_score[PHX_MAX_OUT_DEV];
+  __shared__ int s_nsel;
+  __shared__ float red_s[kNmsThreads];
+  __shared__ int red_i[kNmsThreads];
+  __shared__ int s_done;
+
+  // 1. ordered compaction of candidates with score > thresh (and mask)
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  for (int base = 0; base < n_in; base += kNmsThreads) {
+    int i = base + t;
+    bool ok = false;
+    if (i < n_in) {
+      ok = sb[i] > score_thresh;
+      if (keep) ok = ok && ((keep[(long)b * N + i] & keep_mask) != 0);
+    }
+    // block-wide exclusive scan of ok
+    red_i[t] = ok ? 1 : 0;
+    __syncthreads();
+    for (int off = 1; off < kNmsThreads; off <<= 1) {
+      int v = (t >= off) ? red_i[t - off] : 0;
+      __syncthreads();
+      red_i[t] += v;
+      __syncthreads();
+    }
+    int incl = red_i[t];
+    int total = red_i[kNmsThreads - 1];
+    if (ok) {
+      int pos = s_n + incl - 1;
+      wi[pos] = i;
+      ws[pos] = sb[i];
+      wb[pos] = 0;
+    }
+    __syncthreads();
+    if (t == 0) s_n += total;
+    __syncthreads();
+  }
+  const int n = s_n;
+  if (t == 0) { s_nsel = 0; s_done = 0; }
+  __syncthreads();
+
+  // 2. lazy priority-queue loop
+  while (true) {
+    if (s_nsel >= max_out) break;
+    // argmax of (score desc, index asc) over alive candidates (alive <=> score > thresh;
+    // removed candidates are marked with -inf)
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = t; i < n; i += kNmsThreads) {
+      float v = ws[i];
+      if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+    }
+    red_s[t] = best;
+    red_i[t] = bi;
+    __syncthreads();
+    for (int off = kNmsThreads / 2; off > 0; off >>= 1) {
+      if (t < off) {
+        float v = red_s[t + off];
+        int j = red_i[t + off];
+        if (v > red_s[t] || (v == red_s[t] && j < red_i[t])) { red_s[t] = v; red_i[t] = j; }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      float sc = red_s[0];
+      int c = red_i[0];
+      if (!(sc > score_thresh) || c == 0x7fffffff) {
+        s_done = 1;
+      } else {
+        const float orig = sc;
+        const float* cb = bb + (long)wi[c] * 4;
+        const int nsel = s_nsel;
+        for (int j = nsel - 1; j >= wb[c]; --j) {
+          float sim = tf_iou(cb, sel_box[j]);
+          sc *= expf(scale * sim * sim);
+          if (sc <= score_thresh) break;
+        }
+        wb[c] = nsel;
+        if (sc == orig) {
+          sel_box[nsel][0] = cb[0]; sel_box[nsel][1] = cb[1];
+          sel_box[nsel][2] = cb[2]; sel_box[nsel][3] = cb[3];
+          sel_score[nsel] = sc;
+          s_nsel = nsel + 1;
+          ws[c] = -INFINITY;
+        } else if (sc > score_thresh) {
+          ws[c] = sc;
+        } else {
+          ws[c] = -INFINITY;
+        }
+      }
+    }
+    __syncthreads();
+    if (s_done) break;
+  }
+  __syncthreads();
+  // 3. outputs: padded to max_out, boxes clipped to [0, image_size] (postprocess.py:61-64)
+  const int nsel = s_nsel;
+  for (int k = t; k < max_out; k += kNmsThreads) {
+    float* ob = out_boxes + ((long)b * max_out + k) * 4;
+    if (k < nsel) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ob[j] = fminf(fmaxf(sel_box[k][j], 0.0f), clip_hi);
+      out_scores[(long)b * max_out + k] = sel_score[k];
+    } else {
+      ob[0] = ob[1] = ob[2] = ob[3] = 0.f;
+      out_scores[(long)b * max_out + k] = 0.f;
+    }
+  }
+  if (t == 0) out_count[b] = nsel;
+}
+
+void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
+                     const int* count, int B, int N, float score_thresh, float soft_sigma,
+                     int max_out, float clip_hi, float* out_boxes, float* out_scores,
+                     int* out_count, float* work_score, int* work_sb, hipStream_t s) {
+  if (max_out > PHX_MAX_OUT_DEV) throw std::runtime_error("soft_nms: max_out too large");
+  // TF: scale = -0.5 / soft_nms_sigma (soft_nms_sigma = sigma / 2, postprocess.py:191-200)
+  float scale = soft_sigma > 0.f ? -0.5f / soft_sigma : 0.f;
+  int* widx = work_sb + (long)B * N;
+  hipLaunchKernelGGL(k_soft_nms, dim3(B), dim3(kNmsThreads), 0, s, boxes, scores, keep, keep_mask,
+                     count, N, score_thresh, scale, max_out, clip_hi, out_boxes, out_scores,
+                     out_count, work_score, work_sb, widx);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// per-image max over kept anchors (attacker.py:190): raw max (lowest() if empty) + ties
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_image_max(const float* __restrict__ scores,
+                                                   const uint8_t* __restrict__ keep, int A,
+                                                   float* __restrict__ m, int* __restrict__ argm,
+                                                   int* __restrict__ nties) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  __shared__ float rs[256];
+  __shared__ int ri[256];
+  __shared__ int rc[256];
+  float best = -FLT_MAX;
+  int bi = 0x7fffffff;
+  for (int a = t; a < A; a += 256) {
+    long e = (long)b * A + a;
+    if (keep[e] & 1) {
+      float v = scores[e];
+      if (v > best || (v == best && a < bi)) { best = v; bi = a; }
+    }
+  }
+  rs[t] = best;
+  ri[t] = bi;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) {
+      float v = rs[t + off];
+      int j = ri[t + off];
+      if (v > rs[t] || (v == rs[t] && j < ri[t])) { rs[t] = v; ri[t] = j; }
+    }
+    __syncthreads();
+  }
+  const float mx = rs[0];
+  const int mi = ri[0];
+  __syncthreads();
+  int cnt = 0;
+  if (mi != 0x7fffffff) {
+    for (int a = t; a < A; a += 256) {
+      long e = (long)b * A + a;
+      if ((keep[e] & 1) && scores[e] == mx) ++cnt;
+    }
+  }
+  rc[t] = cnt;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (t < off) rc[t] += rc[t + off];
+    __syncthreads();
+  }
+  if (t == 0) {
+    m[b] = mi == 0x7fffffff ? -FLT_MAX : mx;
+    argm[b] = mi == 0x7fffffff ? -1 : mi;
+    nties[b] = rc[0];
+  }
+}
+
+void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m, int* argmax,
+                      int* nties, hipStream_t s) {
+  hipLaunchKernelGGL(k_image_max, dim3(B), dim3(256), 0, s, scores, keep, A, m, argmax, nties);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// loss (attacker.py:189-193) + per-image dL/dm coefficient + dscale + metrics.  One block.
+//   m_b = max(raw_b, 0); loss = sum m_b^2 + sum (m_b - s)^2 (+ 1e-5 TV added by the TV kernel)
+//   dL/draw_b = (4 m_b - 2 s) if raw_b >= 0 (tf.maximum grad goes to x on ties), else 0
+// ------------------------------------------------------------------------------------------
+__global__ void k_loss(const float* __restrict__ mraw, int B, const float* __restrict__ params,
+                       int npatch, float* __restrict__ dm, float* __restrict__ grad,
+                       float* __restrict__ metrics) {
+  if (threadIdx.x != 0) return;
+  const float s = params[npatch];
+  float sum_sq = 0.f, scale_loss = 0.f, sm = 0.f, sm2 = 0.f, dsc = 0.f;
+  for (int b = 0; b < B; ++b) {
+    float raw = mraw[b];
+    float mb = fmaxf(raw, 0.0f);
+    float d = mb - s;
+    sum_sq += mb * mb;
+    scale_loss += d * d;
+    sm += mb;
+    sm2 += mb * mb;
+    dsc += -2.0f * d;
+    dm[b] = raw >= 0.0f ? (2.0f * mb + 2.0f * d) : 0.0f;
+  }
+  grad[npatch] = dsc;
+  metrics[PHX_M_LOSS] = sum_sq + scale_loss;
+  metrics[PHX_M_SCALE_LOSS] = scale_loss;
+  metrics[PHX_M_SUM_M] = sm;
+  metrics[PHX_M_SUM_M2] = sm2;
+}
+
+void launch_loss(const float* mraw, int B, const float* params, float* dm, float* grad,
+                 float* metrics, hipStream_t s) {
+  hipLaunchKernelGGL(k_loss, dim3(1), dim3(64), 0, s, mraw, B, params, PHX_NPATCH_DEV, dm, grad,
+                     metrics);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// sparse class-head backward: for every kept anchor whose score equals the image max, route
+// dL/dm through sigmoid and the class reduce_max (ties split, TF _MaxGrad) into the input of
+// the class-predict pointwise conv: dx[pixel, :] += W[:, k*ncls + c] * dlogit
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_cls_scatter(
+    const float* __restrict__ scores, const uint8_t* __restrict__ keep,
+    const float* __restrict__ mraw, const int* __restrict__ nties, const float* __restrict__ dm,
+    const float* __restrict__ cls_base, const LevelDesc* __restrict__ lev, int nlev, int A, int B,
+    int nclass, int na, const float* __restrict__ wpred /*[K][na*ncls]*/, int K,
+    float* __restrict__ dx_base, const long* __restrict__ dx_off) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * A) return;
+  const int b = (int)(idx / A), a = (int)(idx % A);
+  if (!(keep[idx] & 1)) return;
+  const float mx = mraw[b];
+  if (scores[idx] != mx || dm[b] == 0.0f) return;
+  const float ds = dm[b] / (float)nties[b];
+  const float s = scores[idx];
+  const float dl = ds * s * (1.0f - s);  // SigmoidGrad: y * (1 - y) * dy
+  int l = 0;
+  while (l + 1 < nlev && a >= lev[l + 1].anchor0) ++l;
+  const LevelDesc L = lev[l];
+  const int local = a - L.anchor0;
+  const int pix = local / na, k = local % na;
+  const long prow = (long)b * L.h * L.w + pix;
+  const float* lg = cls_base + L.cls_off + prow * (na * nclass) + (long)k * nclass;
+  float m = lg[0];
+  for (int c = 1; c < nclass; ++c) m = fmaxf(m, lg[c]);
+  int nt = 0;
+  for (int c = 0; c < nclass; ++c) nt += (lg[c] == m);
+  const float dlc = dl / (float)nt;
+  float* dx = dx_base + dx_off[l] + prow * K;
+  const int N = na * nclass;
+  for (int c = 0; c < nclass; ++c) {
+    if (lg[c] != m) continue;
+    const int col = k * nclass + c;
+    for (int j = 0; j < K; ++j) atomicAdd(dx + j, wpred[(long)j * N + col] * dlc);
+  }
+}
+
+void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* mraw,
+                        const int* nties, const float* dm, const float* cls_base,
+                        const LevelDesc* lev, int nlev, int A, int B, int nclass, int na,
+                        const float* wpred, int K, float* dx_base, const long* dx_off,
+                        hipStream_t s) {
+  long n = (long)B * A;
+  hipLaunchKernelGGL(k_cls_scatter, dim3(cdiv(n, 256)), dim3(256), 0, s, scores, keep, mraw, nties,
+                     dm, cls_base, lev, nlev, A, B, nclass, na, wpred, K, dx_base, dx_off);
+  PHX_LAUNCH_CHECK();
+}
+
+// ------------------------------------------------------------------------------------------
+// ASR counts (attacker.py:238-255): boxes with score >= 0.5 among soft-NMS outputs
+// ------------------------------------------------------------------------------------------
+__global__ void k_count_ge(const float* __restrict__ sc, const int* __restrict__ cnt, int B,
+                           int maxo, float th, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  int n = 0;
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < cnt[b]; ++k) n += sc[(long)b * maxo + k] >= th;
+  *out = (float)n;
+}
+
+void launch_count_ge(const float* sc, const int* cnt, int B, int maxo, float th, float* out,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(k_count_ge, dim3(1), dim3(64), 0, s, sc, cnt, B, maxo, th, out);
+  PHX_LAUNCH_CHECK();
+}
+
+}  // namespace phx
