@@ -1,0 +1,180 @@
+"""Benchmark: patch-optimisation images/sec (EfficientDet-D0 512px fwd+bwd) — BASELINE.json metric.
+
+One "step" = PatchAttacker.train_step on one batch: first (clean) victim pass + pre_nms + soft-NMS,
+EOT paste, second victim pass, loss, victim data-gradient, EOT backward, RCCL all-reduce of
+[d patch | d scale] (N>1), Adam + clip.  Workload = BASELINE config C2/C3: D0 512x512, 16 images
+per GPU, fp32, bn=local (batch statistics per rank), synthetic data: U(-1,1) images keyed by global
+image index, 1-3 injected person boxes per image for placement (the first pass still runs in full),
+synthetic weights (seed 0).
+
+  python bench.py                       # N=1
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# D0 @512 multiply-adds per image forward (efficientdet_arch_test.py:47-49); one step = clean fwd +
+# attack fwd + attack dgrad = 3 forward-equivalents, 2 FLOP per MAC
+D0_MACS = 2_532_997_127
+FLOP_PER_IMAGE = 3 * 2 * D0_MACS
+PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 matrix / vector peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def synth_images(global_idx, size):
+    out = np.empty((len(global_idx), size, size, 3), np.float32)
+    for i, g in enumerate(global_idx):
+        out[i] = np.random.default_rng(1234 + g).uniform(-1, 1, (size, size, 3))
+    return out
+
+
+def synth_boxes(global_idx, size):
+    """1 + (g mod 3) person boxes, height U(96,384), aspect w/h U(.35,.6), inside the image."""
+    res = []
+    for g in global_idx:
+        r = np.random.default_rng(99 + g)
+        bx = []
+        for _ in range(1 + g % 3):
+            h = r.uniform(96, 384) * size / 512
+            w = h * r.uniform(0.35, 0.6)
+            y0 = r.uniform(0, size - h)
+            x0 = r.uniform(0, size - w)
+            bx.append([y0, x0, y0 + h, x0 + w])
+        res.append(np.asarray(bx, np.float32))
+    return res
+
+
+def cpu_baseline(size, batch, threads, budget_s=30.0):
+    """The oracle's restatement of the same step (PyTorch-CPU fp32) on a bounded sample."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd import weights as W
+    from oracle import step as ST
+    torch.set_num_threads(threads)
+    ctx = _lib.Context("efficientdet-d0", size, 1)
+    man = ctx.manifest()
+    wd = W.unpack(man, W.synthetic_blob(man, seed=0))
+    idx = list(range(batch))
+    imgs = synth_images(idx, size)
+    boxes = synth_boxes(idx, size)
+    patch = np.random.default_rng(7).uniform(-1, 1, (640, 640, 3)).astype(np.float32)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        ST.attack_step(wd, imgs, patch, 0.4, boxes=boxes, seed=0, step=n, image_size=size, dtype=torch.float32)
+        n += 1
+        if time.perf_counter() - t0 > budget_s / 2 or n >= 3:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * n / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"oracle restatement (PyTorch-CPU fp32), D0 {size}x{size}, batch {batch}, {n} step(s), {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--image-size", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    from mladversarialobjectdetection_amd import distributed as ddp
+    ddp.init_from_env()
+    rank, world = ddp.rank(), ddp.world()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
+    B, S = args.batch, args.image_size
+    victim = EfficientDetVictim("efficientdet-d0", "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
+                                device=local)
+    att = PatchAttacker(victim, seed=7, device=dev)
+    gidx = list(range(rank * B, (rank + 1) * B))
+    images = torch.as_tensor(synth_images(gidx, S), device=dev)
+    boxes = synth_boxes(gidx, S)
+
+    for _ in range(args.warmup):
+        att.train_step(images, boxes=boxes)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        att.train_step(images, boxes=boxes)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(dt.item())
+    images_per_s = world * B * args.steps / elapsed
+
+    roofline = None
+    step_roof = None
+    if not args.no_profile:
+        # one extra, untimed step with per-launch-group HIP events on the launch stream
+        victim.ctx.profile(True)
+        att.train_step(images, boxes=boxes)
+        rep = victim.ctx.profile_report()
+        victim.ctx.profile(False)
+        kind, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
+        if r["flops"] > 0 and kind == "gemm":
+            ach = r["flops"] / (r["ms"] * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(ach / PEAK_FP32_TFLOPS, 4), "traffic": None, "kernel": kind,
+                        "launches": r["count"], "avg_us": round(1e3 * r["ms"] / r["count"], 2)}
+        else:
+            ach = r["bytes"] / (r["ms"] * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                        "frac": round(ach / PEAK_HBM_GBS, 4), "traffic": None, "kernel": kind,
+                        "launches": r["count"], "avg_us": round(1e3 * r["ms"] / r["count"], 2)}
+        step_ach = FLOP_PER_IMAGE * images_per_s / world / 1e12
+        step_roof = {"achieved_tflops_per_gpu": round(step_ach, 3), "frac_fp32_peak": round(step_ach / PEAK_FP32_TFLOPS, 4),
+                     "breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(rep.items(), key=lambda kv: -kv[1]["ms"])}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = min(16, len(os.sched_getaffinity(0)))
+        cpu = cpu_baseline(S, args.cpu_batch, threads)
+
+    if rank == 0:
+        line = {
+            "metric": "patch-opt images/sec (EffDet-D0 512px fwd+bwd)",
+            "value": round(images_per_s, 3),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (U(-1,1) images, 1-3 injected person boxes/image, synthetic D0 weights)",
+            "config": {"workload": f"C{2 if world == 1 else 3}: EfficientDet-D0 patch attack {S}x{S}, "
+                                   f"{B} images/GPU, bn=local", "global_batch": world * B, "image_size": S,
+                       "parallelism": f"dp{world}"},
+            "roofline": roofline,
+            "step_roofline": step_roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+
+
+if __name__ == "__main__":
+    main()

@@ -148,6 +148,12 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
 int phx_adam_clip(phx_ctx* ctx, float* params, const float* grad, float* m, float* v,
                   float lr, int64_t t, void* stream);
 
+/* Per-launch-group device timing (HIP events on the launch stream).  enable=1 clears and
+ * starts recording; phx_profile_report synchronises and writes JSON
+ * {kind: {count, ms, flops, bytes}} with the algorithmic FLOPs / bytes of the launches. */
+int phx_profile(phx_ctx* ctx, int enable);
+int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed);
+
 /* Debug / test hooks (parity tests call these; not on the timed path).
  * phx_debug_last_patched: copies the last step's patched images [B,H,W,3] (device->device). */
 int phx_debug_last_patched(phx_ctx* ctx, float* out, void* stream);

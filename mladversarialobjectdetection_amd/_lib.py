@@ -68,6 +68,8 @@ _SIGS = [
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
       c_void_p, c_void_p, c_void_p]),
     ("phx_adam_clip", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int64, c_void_p]),
+    ("phx_profile", c_int, [c_void_p, c_int]),
+    ("phx_profile_report", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
     ("phx_debug_last_patched", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_maxscores", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
 ]
@@ -139,6 +141,16 @@ class Context:
 
     def weight_count(self) -> int:
         return int(self.lib.phx_weight_count(self.h))
+
+    def profile(self, enable: bool):
+        self.lib.phx_profile(self.h, int(enable))
+
+    def profile_report(self) -> dict:
+        need = c_size_t()
+        check(self.h, self.lib.phx_profile_report(self.h, None, 0, ctypes.byref(need)), "phx_profile_report")
+        buf = ctypes.create_string_buffer(need.value)
+        check(self.h, self.lib.phx_profile_report(self.h, buf, need.value, ctypes.byref(need)), "phx_profile_report")
+        return json.loads(buf.value.decode())
 
     def call(self, name: str, *args):
         rc = getattr(self.lib, name)(self.h, *args)

@@ -1,0 +1,389 @@
+"""Host-side mirror of the reference's attack interface (attacker.py, brightness_matcher.py,
+util.get_victim_model) over the libphx C ABI.
+
+Same names, argument meaning and error behaviour as the reference where they exist:
+
+  EfficientDetVictim       util.get_victim_model (util.py:177-189) + KerasDriver (infer_lib.py:383)
+  BrightnessMatcher.call   brightness_matcher.py:43-73
+  Patcher.call             attacker.py:490-498
+  PatchAttacker            attacker.py:24-341: first_pass :91, second-pass loss and gradient in
+                           call :172-219, calc_asr :238, train_step :307, save_weights :328
+
+Every computation runs in the HIP kernels of libphx.so on PyTorch-ROCm device memory; PyTorch
+provides only allocation, streams and torch.distributed (RCCL).  Data parallelism: one process per
+GPU, each holding B/world images; the [patch | scale] gradient is SUM-all-reduced once per step
+(bn=local: statistics per rank).
+"""
+from __future__ import annotations
+
+import math
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import distributed as ddp
+from . import weights as wmod
+
+MEAN_RGB = {"efficientdet": [0.485 * 255, 0.456 * 255, 0.406 * 255], "lite": [127.0] * 3}
+STDDEV_RGB = {"efficientdet": [0.229 * 255, 0.224 * 255, 0.225 * 255], "lite": [128.0] * 3}
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+@dataclass
+class NmsConfig:
+    """hparams_config.py:258-266 (+ attacker_train.py:31 override)"""
+    method: str = "gaussian"
+    iou_thresh: float | None = None
+    score_thresh: float = 0.0
+    sigma: float | None = None
+    max_output_size: int = 100
+
+
+@dataclass
+class VictimConfig:
+    name: str
+    image_size: int
+    mean_rgb: list
+    stddev_rgb: list
+    nms_configs: NmsConfig = field(default_factory=NmsConfig)
+
+    def override(self, d: dict):
+        """Config.override (hparams_config.py:91-109) for the keys the attack uses."""
+        for k, v in d.items():
+            if k == "nms_configs":
+                for kk, vv in v.items():
+                    setattr(self.nms_configs, kk, vv)
+            else:
+                setattr(self, k, v)
+
+
+class EfficientDetVictim:
+    """The victim detector held by a libphx context (one device)."""
+
+    def __init__(self, model_name="efficientdet-d0", weights="synthetic", *, seed=0, image_size=0,
+                 max_batch=16, bn_mode="local", score_thresh=0.5, rng_seed=0, device=None,
+                 person_bias=0.0):
+        if device is None:
+            device = torch.cuda.current_device() if torch.cuda.is_available() else 0
+        self.device = device
+        self.ctx = _lib.Context(model_name, image_size, max_batch,
+                                _lib.BN_FROZEN if bn_mode == "frozen" else _lib.BN_LOCAL,
+                                score_thresh, rng_seed, device)
+        self.manifest = self.ctx.manifest()
+        if isinstance(weights, str) and weights == "synthetic":
+            blob = wmod.synthetic_blob(self.manifest, seed=seed, person_bias=person_bias)
+        else:
+            blob = np.ascontiguousarray(np.asarray(weights, dtype=np.float32))
+        self.load_weights(blob)
+        fam = "lite" if "lite" in model_name else "efficientdet"
+        self.config = VictimConfig(model_name, self.ctx.image_size, MEAN_RGB[fam], STDDEV_RGB[fam],
+                                   NmsConfig(score_thresh=score_thresh))
+        self.num_anchors = self.ctx.num_anchors
+        self.max_batch = max_batch
+
+    def load_weights(self, blob: np.ndarray):
+        blob = np.ascontiguousarray(blob, dtype=np.float32)
+        if blob.size != self.ctx.weight_count():
+            raise ValueError(f"weight blob has {blob.size} floats, manifest needs {self.ctx.weight_count()}")
+        self.ctx.call("phx_load_weights", blob.ctypes.data, blob.size)
+        self.blob = blob
+
+    def read_weights(self) -> np.ndarray:
+        out = np.empty(self.ctx.weight_count(), np.float32)
+        self.ctx.call("phx_read_weights", out.ctypes.data, out.size)
+        return out
+
+    def _check_images(self, images):
+        S = self.ctx.image_size
+        if images.dim() != 4 or tuple(images.shape[1:]) != (S, S, 3) or images.dtype != torch.float32:
+            raise ValueError(f"images must be float32 [B,{S},{S},3], got {tuple(images.shape)} {images.dtype}")
+        if not images.is_cuda:
+            raise ValueError("images must be a device tensor")
+        if images.shape[0] > self.max_batch:
+            raise ValueError("batch exceeds max_batch")
+        return images.contiguous()
+
+    def detect(self, images):
+        """EfficientDetModel.call(pre_mode=None, post_mode=None) + postprocess.pre_nms."""
+        images = self._check_images(images)
+        B, A = images.shape[0], self.num_anchors
+        scores = torch.empty(B, A, device=images.device)
+        classes = torch.empty(B, A, dtype=torch.int32, device=images.device)
+        boxes = torch.empty(B, A, 4, device=images.device)
+        self.ctx.call("phx_detect", images.data_ptr(), B, scores.data_ptr(), classes.data_ptr(),
+                      boxes.data_ptr(), _stream())
+        return boxes, scores, classes
+
+    def first_pass(self, images):
+        images = self._check_images(images)
+        B = images.shape[0]
+        ob = torch.empty(B, _lib.MAX_OUT, 4, device=images.device)
+        os_ = torch.empty(B, _lib.MAX_OUT, device=images.device)
+        oc = torch.empty(B, dtype=torch.int32, device=images.device)
+        self.ctx.call("phx_first_pass", images.data_ptr(), B, ob.data_ptr(), os_.data_ptr(), oc.data_ptr(),
+                      _stream())
+        return ob, os_, oc
+
+    def soft_nms(self, boxes, scores, count=None):
+        """postprocess.nms(padded=True) over [B,N,4] / [B,N] candidates."""
+        boxes = boxes.contiguous().float()
+        scores = scores.contiguous().float()
+        B, N = scores.shape
+        if count is None:
+            count = torch.full((B,), N, dtype=torch.int32, device=scores.device)
+        count = count.to(torch.int32).contiguous()
+        ob = torch.empty(B, _lib.MAX_OUT, 4, device=scores.device)
+        os_ = torch.empty(B, _lib.MAX_OUT, device=scores.device)
+        oc = torch.empty(B, dtype=torch.int32, device=scores.device)
+        self.ctx.call("phx_soft_nms", boxes.data_ptr(), scores.data_ptr(), count.data_ptr(), B, N,
+                      ob.data_ptr(), os_.data_ptr(), oc.data_ptr(), _stream())
+        return ob, os_, oc
+
+
+class BrightnessMatcher:
+    """brightness_matcher.BrightnessMatcher: Y-channel mean transfer patch -> scene."""
+
+    def __init__(self, victim: EfficientDetVictim):
+        self.victim = victim
+
+    def __call__(self, inputs):
+        src, tgt = inputs
+        squeeze = src.dim() == 3
+        if squeeze:
+            src, tgt = src[None], tgt[None]
+        src = src.contiguous().float()
+        tgt = tgt.contiguous().float()
+        B, Pp = src.shape[0], src.shape[1]
+        out = torch.empty_like(src)
+        self.victim.ctx.call("phx_brightness_match", src.data_ptr(), Pp, tgt.data_ptr(), tgt.shape[1],
+                             tgt.shape[2], B, out.data_ptr(), _stream())
+        return out[0] if squeeze else out
+
+    call = __call__
+
+
+def _pad_boxes(boxes, B, device):
+    """list of [n_b,4] (or a padded [B,maxb,4] + count) -> ([B,maxb,4], count[B])"""
+    if isinstance(boxes, (tuple, list)) and len(boxes) == 2 and torch.is_tensor(boxes[0]) and boxes[0].dim() == 3:
+        bx, cnt = boxes
+        return bx.contiguous().float(), cnt.to(torch.int32).contiguous()
+    maxb = max(1, max(len(b) for b in boxes))
+    if maxb > _lib.MAX_OUT:
+        raise ValueError("at most 100 boxes per image")
+    out = torch.zeros(B, maxb, 4, device=device)
+    cnt = torch.zeros(B, dtype=torch.int32, device=device)
+    for i, b in enumerate(boxes):
+        b = torch.as_tensor(np.asarray(b, dtype=np.float32)).reshape(-1, 4)
+        if len(b):
+            out[i, :len(b)] = b.to(device)
+        cnt[i] = len(b)
+    return out, cnt
+
+
+class Patcher:
+    """attacker.Patcher: EOT paste of the current patch onto every box of every image."""
+
+    def __init__(self, attacker: "PatchAttacker"):
+        self.attacker = attacker
+
+    def __call__(self, inputs, step=None):
+        boxes, images = inputs
+        a = self.attacker
+        images = a.model._check_images(images)
+        B = images.shape[0]
+        bx, cnt = _pad_boxes(boxes, B, images.device)
+        out = torch.empty_like(images)
+        self.last_placements = torch.zeros(B, bx.shape[1], 8, device=images.device)
+        a.model.ctx.call("phx_patch_images", images.data_ptr(), B, bx.data_ptr(), cnt.data_ptr(), bx.shape[1],
+                         a.params.data_ptr(), int(a.cur_step if step is None else step), a.global_offset(B),
+                         out.data_ptr(), self.last_placements.data_ptr(), _stream())
+        return out
+
+    call = __call__
+
+
+class _Mean:
+    """keras.metrics.Mean (what add_metric aggregates per epoch)."""
+
+    def __init__(self):
+        self.total, self.count = 0.0, 0
+
+    def update(self, v):
+        self.total += float(v)
+        self.count += 1
+
+    def result(self):
+        return self.total / max(self.count, 1)
+
+
+class PatchAttacker:
+    """attacker.PatchAttacker: trainable [patch | scale] optimised against the victim."""
+
+    METRICS = ("loss", "scale", "scale_loss", "tv_loss", "mean_max_score", "std_max_score", "asr",
+               "asr_to_scale")
+
+    def __init__(self, model: EfficientDetVictim, initial_patch=None, config_override=None,
+                 visualize_freq=200, *, seed=0, learning_rate=1e-2, device=None):
+        self.model = model
+        self.config = model.config
+        if config_override:
+            self.config.override(config_override)
+        dev = torch.device("cuda", model.device) if device is None else torch.device(device)
+        if initial_patch is None:
+            # np.random.uniform(-1, 1, (640, 640, 3)), scale .4 (attacker.py:42-44)
+            patch_img = np.random.default_rng(seed).uniform(-1.0, 1.0, size=(640, 640, 3))
+            scale = 0.4
+        else:
+            patch_img, scale = load_patch(initial_patch)
+        params = np.concatenate([np.asarray(patch_img, np.float32).reshape(-1), [np.float32(scale)]])
+        self.params = torch.as_tensor(params, dtype=torch.float32, device=dev).contiguous()
+        self.grad = torch.zeros_like(self.params)
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.metrics_buf = torch.zeros(_lib.NMETRIC, device=dev)
+        self.learning_rate = learning_rate
+        self.iterations = 0
+        self.cur_step = 0
+        self.visualize_freq = visualize_freq
+        self._patcher = Patcher(self)
+        self._matcher = BrightnessMatcher(model)
+        self.metrics = {k: _Mean() for k in self.METRICS}
+        self.bins = np.arange(self.config.nms_configs.score_thresh, .805, .01, dtype="float32")
+
+    # ---- variables -----------------------------------------------------------------------------
+    @property
+    def patch(self):
+        return self.params[:_lib.NPATCH].view(640, 640, 3)
+
+    @property
+    def scale(self):
+        return self.params[_lib.NPATCH]
+
+    @property
+    def _trainable_variables(self):
+        return [self.params[_lib.NPATCH:], self.patch]
+
+    def global_offset(self, B):
+        return ddp.global_offset(B)
+
+    # ---- reference methods -------------------------------------------------------------------
+    def first_pass(self, images):
+        return self.model.first_pass(images)
+
+    def call(self, images, *, training=True, boxes=None, add_tv=None):
+        """PatchAttacker.call: returns [d scale, d patch] (attacker.py:217); `boxes` optionally
+        replaces the first-pass detections for placement (injected boxes)."""
+        images = self.model._check_images(images)
+        B = images.shape[0]
+        if add_tv is None:
+            add_tv = ddp.rank() == 0  # TV counted once per global step
+        if boxes is not None:
+            bx, cnt = _pad_boxes(boxes, B, images.device)
+            bp, cp, maxb = bx.data_ptr(), cnt.data_ptr(), bx.shape[1]
+            self._keep = (bx, cnt)
+        else:
+            bp, cp, maxb = None, None, 0
+        self.model.ctx.call("phx_step_grad", images.data_ptr(), B, bp, cp, maxb, self.params.data_ptr(),
+                            int(self.cur_step), self.global_offset(B), int(bool(add_tv)), self.grad.data_ptr(),
+                            self.metrics_buf.data_ptr(), _stream())
+        self._last_B = B
+        if training:
+            return [self.grad[_lib.NPATCH:], self.grad[:_lib.NPATCH].view(640, 640, 3)]
+        return None
+
+    __call__ = call
+
+    def apply_gradients(self):
+        """optimizer.apply_gradients + variable constraints (attacker.py:315, :51-54)."""
+        self.iterations += 1
+        self.model.ctx.call("phx_adam_clip", self.params.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(),
+                            self.v.data_ptr(), float(self.learning_rate), int(self.iterations), _stream())
+
+    def allreduce_gradients(self):
+        ddp.allreduce_sum_(self.grad)
+
+    def step_metrics(self, reduce=True):
+        """Per-step values of the reference's add_metric set (attacker.py:196-207)."""
+        mb = self.metrics_buf.clone()
+        B = torch.tensor([float(self._last_B)], device=mb.device)
+        if reduce:
+            ddp.allreduce_sum_(mb)
+            ddp.allreduce_sum_(B)
+        v = mb.cpu().numpy().astype(np.float64)
+        n = float(B.item())
+        scale = float(self.scale.item())
+        mean = v[_lib.M_SUM_M] / n
+        var = max(v[_lib.M_SUM_M2] / n - mean * mean, 0.0)
+        asr = 1.0 - v[_lib.M_ASR_NUM] / (v[_lib.M_ASR_DEN] + 1e-7)
+        return {"loss": v[_lib.M_LOSS], "scale": scale, "scale_loss": v[_lib.M_SCALE_LOSS],
+                "tv_loss": v[_lib.M_TV], "mean_max_score": mean, "std_max_score": math.sqrt(var),
+                "asr": asr, "asr_to_scale": asr / scale if scale else float("inf"),
+                "patches": v[_lib.M_NBOX]}
+
+    def train_step(self, inputs, boxes=None):
+        """attacker.py:307-316: grads = self(inputs); apply_gradients; return metrics."""
+        self.call(inputs, boxes=boxes)
+        self.allreduce_gradients()
+        self.apply_gradients()
+        self.cur_step += 1
+        sm = self.step_metrics()
+        for k in self.METRICS:
+            self.metrics[k].update(sm[k])
+        return {k: m.result() for k, m in self.metrics.items()}
+
+    def reset_metrics(self):
+        for m in self.metrics.values():
+            m.total, m.count = 0.0, 0
+
+    def save_weights(self, dirpath, **kwargs):
+        """attacker.py:328-341: scale.txt, patch.png (de-normalised uint8), patch.npy (float32;
+        the reference writes patch.tiff through tifffile, not installed here)."""
+        os.makedirs(dirpath)
+        with open(os.path.join(dirpath, "scale.txt"), "w") as f:
+            f.write(str(np.float32(self.scale.item())))
+        patch = self.patch.detach().cpu().numpy()
+        np.save(os.path.join(dirpath, "patch.npy"), patch)
+        img = np.clip(patch * np.asarray(self.config.stddev_rgb) + np.asarray(self.config.mean_rgb), 0, 255)
+        try:
+            from PIL import Image
+            Image.fromarray(img.astype(np.uint8)).save(os.path.join(dirpath, "patch.png"))
+        except ImportError:  # pragma: no cover
+            pass
+
+
+def load_patch(dirpath):
+    """initial_patch=dir (attacker.py:46-48): patch.npy (or patch.tiff if tifffile exists) + scale.txt."""
+    import ast
+    p = os.path.join(dirpath, "patch.npy")
+    if os.path.exists(p):
+        patch = np.load(p, allow_pickle=False)
+    else:
+        import tifffile  # noqa: F401  (reference format)
+        patch = tifffile.imread(os.path.join(dirpath, "patch.tiff"))
+    with open(os.path.join(dirpath, "scale.txt")) as f:
+        scale = ast.literal_eval(f.read())
+    return patch, float(scale)
+
+
+class ReduceLROnPlateau:
+    """keras ReduceLROnPlateau(monitor='loss', factor=.5, patience=50, min_lr=1e-4) used by
+    attacker_train.py:70-71, stepped once per epoch."""
+
+    def __init__(self, attacker: PatchAttacker, factor=0.5, patience=50, min_lr=1e-4, min_delta=1e-4):
+        self.a, self.factor, self.patience, self.min_lr, self.min_delta = attacker, factor, patience, min_lr, min_delta
+        self.best, self.wait = float("inf"), 0
+
+    def on_epoch_end(self, loss):
+        if loss < self.best - self.min_delta:
+            self.best, self.wait = loss, 0
+        else:
+            self.wait += 1
+            if self.wait >= self.patience and self.a.learning_rate > self.min_lr:
+                self.a.learning_rate = max(self.a.learning_rate * self.factor, self.min_lr)
+                self.wait = 0

@@ -6,6 +6,7 @@
 #include <array>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -100,7 +101,33 @@ struct Exec {
 
 }  // namespace
 
+// Per-launch-group timing with HIP events on the launch stream (phx_profile): used by bench.py
+// to time the dominant kernel live; off by default (no events on the timed path).
+struct Prof {
+  struct Rec {
+    std::string kind;
+    hipEvent_t a, b;
+    double flops, bytes;
+  };
+  bool on = false;
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  hipEvent_t ev() {
+    if (used == pool.size()) {
+      hipEvent_t e;
+      PHX_HIP(hipEventCreate(&e));
+      pool.push_back(e);
+    }
+    return pool[used++];
+  }
+  ~Prof() {
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+};
+
 struct phx_ctx {
+  Prof prof;
   ModelConfig mc;
   int device = 0;
   int max_batch = 0;
@@ -192,6 +219,23 @@ int fail(phx_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;
 }
+
+struct Scope {
+  Prof* p;
+  size_t idx;
+  hipStream_t s;
+  Scope(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t st)
+      : p(ctx->prof.on ? &ctx->prof : nullptr), s(st) {
+    if (!p) return;
+    Prof::Rec r{kind, p->ev(), p->ev(), flops, bytes};
+    PHX_HIP(hipEventRecord(r.a, s));
+    p->recs.push_back(r);
+    idx = p->recs.size() - 1;
+  }
+  ~Scope() {
+    if (p) (void)hipEventRecord(p->recs[idx].b, s);
+  }
+};
 
 }  // namespace
 
@@ -326,6 +370,17 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     const Tensor& to = P.tensors[op.out];
     float* x = E.tptr(op.in[0], input);
     float* y = E.tptr(op.out, input);
+    double fl = 0, by = 4.0 * (double)(ti.numel() + to.numel());
+    const char* kind = "fwd_other";
+    switch (op.t) {
+      case OP_STEM: kind = "stem_fwd"; fl = 2.0 * to.numel() * 27; break;
+      case OP_PW: kind = "gemm"; fl = 2.0 * ti.rows() * ti.c * to.c; by += 4.0 * ti.c * to.c; break;
+      case OP_DW: kind = "dw_fwd"; fl = 2.0 * to.numel() * op.k * op.k; break;
+      case OP_BN: kind = "bn_fwd"; by = 4.0 * (2.0 * ti.numel() + to.numel()); break;
+      case OP_SE: kind = "se_fwd"; by = 4.0 * ti.numel(); break;
+      default: break;
+    }
+    Scope scope(ctx, kind, fl, by, s);
     switch (op.t) {
       case OP_STEM:
         launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s);
@@ -422,6 +477,17 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     const Tensor& to = P.tensors[op.out];
     const float* dy = E.gptr(op.out);
     float* dx = E.gptr(op.in[0]);
+    double fl = 0, by = 4.0 * (double)(ti.numel() + to.numel());
+    const char* kind = "bwd_other";
+    switch (op.t) {
+      case OP_STEM: kind = "stem_bwd"; fl = 2.0 * to.numel() * 27; break;
+      case OP_PW: kind = "gemm"; fl = 2.0 * ti.rows() * ti.c * to.c; by += 4.0 * ti.c * to.c; break;
+      case OP_DW: kind = "dw_bwd"; fl = 2.0 * to.numel() * op.k * op.k; break;
+      case OP_BN: kind = "bn_bwd"; by = 4.0 * (4.0 * ti.numel() + to.numel()); break;
+      case OP_SE: kind = "se_bwd"; by = 4.0 * 3.0 * ti.numel(); break;
+      default: break;
+    }
+    Scope scope(ctx, kind, fl, by, s);
     switch (op.t) {
       case OP_STEM:
         launch_stem_bwd(dy, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
@@ -477,6 +543,8 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
 
 void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
   const Program& P = E.prog;
+  Scope scope(ctx, "pre_nms", 0.0,
+              (double)E.B * ctx->A * (ctx->mc.num_classes + 4 + 4 + 6) * 4.0, s);
   const float S = (float)ctx->mc.image_size;
   launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
@@ -486,6 +554,7 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
 
 // postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25
 void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s) {
+  Scope scope(ctx, "soft_nms", 0.0, (double)E.B * ctx->A * 5.0, s);
   launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->score_thresh,
                   0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s);
 }
@@ -689,6 +758,7 @@ void eot_forward(phx_ctx* ctx, Exec& E, const float* images, int B, const float*
                  hipStream_t s) {
   EotDims d = E.ed;
   d.B = B;
+  Scope scope(ctx, "eot_fwd", 0.0, (double)B * (2.0 * PHX_NPATCH + 3.0 * d.H * d.W * 3) * 4.0, s);
   launch_eot_place(d, boxes, count, params, ctx->seed, step, gimg0, E.img, E.place, E.spans, E.err,
                    s);
   launch_eot_match(d, params, E.img, images, E.matched, E.ysum, E.ymean, true, s);
@@ -774,10 +844,55 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   EotDims d = E.ed;
   d.B = B;
   const float* dimg = E.gptr(E.prog.input);
+  Scope scope(ctx, "eot_bwd", 0.0, (double)B * (3.0 * PHX_NPATCH + 2.0 * d.H * d.W * 3) * 4.0, s);
   launch_eot_rot_bwd(d, dimg, E.owner, E.place, E.rstore, E.dstore, s);
   launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.dmatched, s);
   launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_profile(phx_ctx* ctx, int enable) {
+  if (!ctx) return PHX_EINVAL;
+  ctx->prof.on = enable != 0;
+  ctx->prof.recs.clear();
+  ctx->prof.used = 0;
+  return PHX_OK;
+}
+
+int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
+  if (!ctx) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  struct Agg { long n = 0; double ms = 0, flops = 0, bytes = 0; };
+  std::map<std::string, Agg> agg;
+  for (auto& r : ctx->prof.recs) {
+    PHX_HIP(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    PHX_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    Agg& a = agg[r.kind];
+    a.n++;
+    a.ms += ms;
+    a.flops += r.flops;
+    a.bytes += r.bytes;
+  }
+  std::ostringstream js;
+  js << "{";
+  bool first = true;
+  for (auto& kv : agg) {
+    js << (first ? "" : ",") << "\"" << kv.first << "\":{\"count\":" << kv.second.n
+       << ",\"ms\":" << kv.second.ms << ",\"flops\":" << kv.second.flops
+       << ",\"bytes\":" << kv.second.bytes << "}";
+    first = false;
+  }
+  js << "}";
+  std::string out = js.str();
+  if (needed) *needed = out.size() + 1;
+  if (buf && cap) {
+    size_t c = std::min(cap - 1, out.size());
+    memcpy(buf, out.data(), c);
+    buf[c] = 0;
+  }
   return PHX_OK;
   PHX_CATCH(ctx)
 }

@@ -1,0 +1,54 @@
+"""Data parallelism for the attack step.
+
+One process per GPU (torchrun; backend "nccl" = RCCL over xGMI on ROCm, "gloo" on CPU for tests).
+The global batch is split contiguously: rank r holds global images [r*B, (r+1)*B), which also keys
+the EOT RNG, so every image sees the same random draws at any GPU count.  Exactly one exchange per
+step: a SUM all-reduce of the contiguous [d patch | d scale] buffer (PHX_NPARAM floats = 4.9 MB)
+between the victim dgrad and the Adam update; the 1e-5*TV term is added by rank 0 only, so the
+reduced gradient equals the sum of per-shard reference gradients (bn=local: BN statistics per
+shard).  Metrics add one 8-float all-reduce.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def is_dist() -> bool:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+
+
+def world() -> int:
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def global_offset(local_batch: int) -> int:
+    """First global image index of this rank's shard."""
+    return rank() * local_batch
+
+
+def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
+    """In-place SUM over ranks (no-op at world size 1)."""
+    if is_dist():
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def init_from_env(backend: str | None = None):
+    """Initialise the process group from torchrun's env (MASTER_ADDR must be 127.0.0.1 here)."""
+    if not dist.is_available() or dist.is_initialized():
+        return
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend == "nccl":
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    dist.init_process_group(backend=backend)
