@@ -303,11 +303,12 @@ class Detector:
         return head("class_net", "class"), head("box_net", "box")
 
 
-def anchors(image_size, anchor_scale=4.0, num_scales=3, aspect_ratios=(1.0, 2.0, 0.5)):
+def anchors(image_size, anchor_scale=4.0, num_scales=3, aspect_ratios=(1.0, 2.0, 0.5),
+            min_level=MIN_LEVEL, max_level=MAX_LEVEL):
     """anchors.py:83-165 (Anchors._generate_boxes), float64 then float32."""
-    fs = feat_sizes(image_size)
+    fs = feat_sizes(image_size, max_level)
     boxes_all = []
-    for level in range(MIN_LEVEL, MAX_LEVEL + 1):
+    for level in range(min_level, max_level + 1):
         stride = fs[0] / float(fs[level])
         boxes_level = []
         for octave in range(num_scales):

@@ -74,7 +74,7 @@ def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0
         loss = loss + 1e-5 * tv
     gp, gs = torch.autograd.grad(loss, [patch_t, scale_t])
     grad = np.concatenate([gp.detach().numpy().reshape(-1), [gs.item()]])
-    return dict(loss=loss.item(), grad=grad, m=m.detach().numpy(), m_raw=np.array([float(v) for v in m_raw]),
+    return dict(loss=loss.item(), grad=grad, m=m.detach().numpy(), m_raw=np.array([float(v.detach()) for v in m_raw]),
                 scale_loss=scale_losses.sum().item(), tv=tv.item(), patched=patched.detach().numpy(),
                 places=places, first_pass=fp)
 
