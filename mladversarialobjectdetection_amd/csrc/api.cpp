@@ -56,6 +56,7 @@ struct Exec {
   long* dxoff_dev = nullptr;
   std::vector<long> dxoff;
   bool cls_contig = true;
+  int ntiles = 0;
   // pre_nms / nms / loss
   float *scores = nullptr, *boxes = nullptr;
   int* classes = nullptr;
@@ -269,10 +270,11 @@ Exec& phx_ctx::exec_for(int B) {
       red_need = std::max(red_need, bn_stats_scratch_doubles((long)ti.rows(), ti.c));
       coef_need = std::max(coef_need, (size_t)ti.c * 3);
     } else if (op.t == OP_SE) {
-      E.slot_a[op.slot] = E.alloc<float>((size_t)B * ti.c * 65);
+      E.slot_a[op.slot] = E.alloc<float>((size_t)B * ti.c * 2);
       E.slot_b[op.slot] = E.alloc<float>((size_t)B * op.cse);
       E.slot_c[op.slot] = E.alloc<float>((size_t)B * ti.c);
-      seg_need = std::max(seg_need, (size_t)B * ti.c * 65);
+      seg_need = std::max(seg_need, (size_t)B * ti.c * 2);
+      red_need = std::max(red_need, colred_scratch_doubles((long)ti.h * ti.w, ti.c, B));
       E.se_of_tensor[op.out] = (int)i;
     }
   }
@@ -294,6 +296,8 @@ Exec& phx_ctx::exec_for(int B) {
     d.h = tc.h;
     d.w = tc.w;
     d.anchor0 = a0;
+    d.tile0 = E.ntiles;
+    E.ntiles += pre_nms_tiles(tc.h, tc.w, na);
     a0 += tc.h * tc.w * na;
     E.lev.push_back(d);
     // input of the class-predict pointwise conv
@@ -418,7 +422,8 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       }
       case OP_SE:
         launch_se_fwd(x, nullptr, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1, W + op.b1, W + op.w2,
-                      W + op.b2, op.act, E.slot_a[op.slot], E.slot_b[op.slot], E.slot_c[op.slot], s);
+                      W + op.b2, op.act, E.slot_a[op.slot], E.slot_b[op.slot], E.slot_c[op.slot], s,
+                      E.red);
         break;
       case OP_ADD:
         launch_add(x, E.tptr(op.in[1], input), y, (long)to.numel(), s);
@@ -509,7 +514,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_SE:
         launch_se_bwd(dy, E.tptr(op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
                       W + op.b1, W + op.w2, W + op.b2, op.act, E.slot_a[op.slot],
-                      E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s);
+                      E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s, E.red);
         break;
       case OP_ADD:
         launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s);
@@ -549,7 +554,7 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
   launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
                  ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->score_thresh,
-                 E.scores, E.classes, E.boxes, E.keep, s);
+                 E.scores, E.classes, E.boxes, E.keep, E.ntiles, s);
 }
 
 // postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25

@@ -46,11 +46,12 @@ void launch_bn_bwd(const float* da, const float* y, const float* mean, const flo
 // squeeze-excite forward: pool[B,C] = mean_hw(x); scale[B,C]; y = x * scale
 void launch_se_fwd(const float* x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
-                   float* hidden, float* scale, hipStream_t s);
+                   float* hidden, float* scale, hipStream_t s, double* scratch);
 void launch_se_bwd(const float* dy, const float* x, float* dx, int B, int HW, int C, int Cse,
                    const float* w1, const float* b1, const float* w2, const float* b2, int act,
                    const float* pool, const float* hidden, const float* scale, float* gsum,
-                   bool acc, hipStream_t s);
+                   bool acc, hipStream_t s, double* scratch);
+size_t colred_scratch_doubles(long seg_rows, int C, int nseg);
 void launch_add(const float* a, const float* b, float* y, long n, hipStream_t s);
 // dst (+)= src
 void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s);
@@ -77,13 +78,15 @@ struct LevelDesc {
   long box_off;
   int h, w;
   int anchor0;    // first anchor index of this level
+  int tile0;      // first pre_nms tile of this level
 };
+int pre_nms_tiles(int h, int w, int na);
 // pre_nms (postprocess.py:119-156) + person/validity filter (attacker.py:69-89, 105-113)
 // outputs per anchor: score, class, box; keep flag (bit0 = person&valid, bit1 = >= thresh)
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
-                    float* boxes, uint8_t* keep, hipStream_t s);
+                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s);
 // soft-NMS (NonMaxSuppressionV5, gaussian) per image over candidates selected by keep&mask
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,

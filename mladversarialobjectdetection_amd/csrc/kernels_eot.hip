@@ -124,44 +124,64 @@ __global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __res
     place[sl] = P;
   }
   __syncthreads();
-  // serial prefix: R offsets, compact valid list, per-image lists, chunk prefix
-  if (t == 0) {
-    int* nvalid = lists;                 // [1]
-    int* total_chunks = lists + 1;       // [1]
-    int* img_n = lists + 2;              // [B]
-    int* img_first = img_n + d.B;        // [B]  index into vlist of the image's first box
-    int* vlist = img_first + d.B;        // [B*maxb] slot ids
-    int* cprefix = vlist + nslot;        // [B*maxb+1] chunk prefix over vlist
-    long off = 0;
-    int nv = 0, nch = 0;
-    int e = 0;
-    for (int b = 0; b < d.B; ++b) {
-      img_first[b] = nv;
-      int cnt = 0;
-      for (int k = 0; k < d.maxb; ++k) {
-        BoxPlace& P = place[b * d.maxb + k];
-        if (!P.valid) continue;
-        long need = (long)P.ps * P.ps * 3;
-        if (off + need > d.rcap) {
-          P.valid = 0;
-          e = 1;
-          continue;
-        }
-        P.roff = off;
-        off += need;
-        vlist[nv] = b * d.maxb + k;
-        cprefix[nv] = nch;
-        nch += (P.ps * P.ps + 255) / 256;
-        ++nv;
-        ++cnt;
-      }
-      img_n[b] = cnt;
+  // R offsets, compact valid list, per-image lists and chunk prefix: one workgroup scan per
+  // 256 slots with running totals
+  int* nvalid = lists;                 // [1]
+  int* total_chunks = lists + 1;       // [1]
+  int* img_n = lists + 2;              // [B]
+  int* img_first = img_n + d.B;        // [B]  index into vlist of the image's first box
+  int* vlist = img_first + d.B;        // [B*maxb] slot ids
+  int* cprefix = vlist + nslot;        // [B*maxb+1] chunk prefix over vlist
+  __shared__ long s_need[256];
+  __shared__ int s_ch[256], s_v[256];
+  __shared__ long run_off;
+  __shared__ int run_ch, run_v;
+  if (t == 0) { run_off = 0; run_ch = 0; run_v = 0; }
+  __syncthreads();
+  for (int base = 0; base < nslot; base += 256) {
+    const int sl = base + t;
+    long need = 0;
+    int ch = 0, v = 0;
+    if (sl < nslot && place[sl].valid) {
+      const int ps = place[sl].ps;
+      need = (long)ps * ps * 3;
+      ch = (ps * ps + 255) / 256;
+      v = 1;
     }
-    cprefix[nv] = nch;
-    *nvalid = nv;
-    *total_chunks = nch;
-    if (err) *err = e;
+    s_need[t] = need; s_ch[t] = ch; s_v[t] = v;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      long a1 = t >= off ? s_need[t - off] : 0;
+      int a2 = t >= off ? s_ch[t - off] : 0;
+      int a3 = t >= off ? s_v[t - off] : 0;
+      __syncthreads();
+      s_need[t] += a1; s_ch[t] += a2; s_v[t] += a3;
+      __syncthreads();
+    }
+    if (sl < nslot) {
+      const long ex_off = run_off + s_need[t] - need;
+      const int ex_ch = run_ch + s_ch[t] - ch;
+      const int ex_v = run_v + s_v[t] - v;
+      if (sl % d.maxb == 0) img_first[sl / d.maxb] = ex_v;
+      if (v) {
+        place[sl].roff = ex_off;
+        vlist[ex_v] = sl;
+        cprefix[ex_v] = ex_ch;
+      }
+    }
+    __syncthreads();
+    if (t == 255) { run_off += s_need[255]; run_ch += s_ch[255]; run_v += s_v[255]; }
+    __syncthreads();
   }
+  if (t == 0) {
+    *nvalid = run_v;
+    *total_chunks = run_ch;
+    cprefix[run_v] = run_ch;
+    if (err) *err = 0;
+  }
+  __syncthreads();
+  for (int b = t; b < d.B; b += blockDim.x)
+    img_n[b] = (b + 1 < d.B ? img_first[b + 1] : run_v) - img_first[b];
 }
 
 // TF ScaleAndTranslate span computation (ComputeSpansCore, triangle kernel, antialias=True,

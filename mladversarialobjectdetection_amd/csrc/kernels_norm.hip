@@ -11,99 +11,188 @@
 namespace phx {
 
 // ------------------------------------------------------------------------------------------
-// generic two-stage per-channel reduction over rows of [M, C]
-//   stage 1: grid.x = chunks, every block reduces its row range into part[chunk][C][2]
-//   stage 2: per channel sum over chunks
+// Column reduction over [nseg][seg_rows][C] (C % 4 == 0): every lane owns 4 consecutive channels
+// (float4 loads, 256-B+ coalesced rows), accumulates 64-row runs in fp32 then folds them into
+// fp64; workgroups reduce their rows in LDS and write fp64 partials [seg][chunk][C][2]; a second
+// kernel sums the chunks per (seg, channel) with coalesced channel-major reads and hands the two
+// sums to an epilogue functor.  BN statistics use a per-channel shift (the segment's first row) so
+// E[y^2]-E[y]^2 carries no cancellation.
 // ------------------------------------------------------------------------------------------
-static inline int red_chunks(long M) {
-  long c = (M + 255) / 256;
-  if (c > 1024) c = 1024;
-  if (c < 1) c = 1;
-  return (int)c;
+struct RedPlan {
+  int tpr;       // threads per row (= C/4, capped at 256 per workgroup)
+  int cgroups;   // channel groups (grid.y)
+  int chunks;    // row chunks per segment (grid.x)
+  long rpc;      // rows per chunk
+};
+
+static RedPlan red_plan(long seg_rows, int C, int nseg) {
+  RedPlan p;
+  int tpr_total = C / 4;
+  p.cgroups = (tpr_total + 255) / 256;
+  p.tpr = tpr_total < 256 ? tpr_total : 256;
+  int rpi = 256 / p.tpr;
+  long target_blocks = 2048;
+  long per_seg = target_blocks / (nseg * p.cgroups);
+  if (per_seg < 1) per_seg = 1;
+  long rpc = (seg_rows + per_seg - 1) / per_seg;
+  long minrows = (long)rpi * 32;
+  if (rpc < minrows) rpc = minrows;
+  rpc = (rpc + rpi - 1) / rpi * rpi;
+  p.rpc = rpc;
+  p.chunks = (int)((seg_rows + rpc - 1) / rpc);
+  return p;
 }
 
-size_t bn_stats_scratch_doubles(long M, int C) { return (size_t)red_chunks(M) * C * 2; }
+size_t colred_scratch_doubles(long seg_rows, int C, int nseg) {
+  RedPlan p = red_plan(seg_rows, C, nseg);
+  return (size_t)nseg * p.chunks * C * 2 + (size_t)nseg * C * 2;
+}
+size_t bn_stats_scratch_doubles(long M, int C) { return colred_scratch_doubles(M, C, 1); }
 
-__global__ __launch_bounds__(256) void k_bn_stats_part(const float* __restrict__ y, long M, int C,
-                                                       long rows_per_chunk,
-                                                       double* __restrict__ part) {
-  const long m0 = (long)blockIdx.x * rows_per_chunk;
-  const long m1 = min(M, m0 + rows_per_chunk);
-  __shared__ double sh[256][2];
+template <class F>
+__global__ __launch_bounds__(256) void k_colred_part(F f, long seg_rows, int C, long rpc,
+                                                     double* __restrict__ part) {
+  const int tpr_total = C >> 2;
+  const int g0 = blockIdx.y * 256;
+  const int tpr = min(tpr_total - g0, 256);
+  const int rpi = 256 / tpr;
   const int t = threadIdx.x;
-  double* out = part + (long)blockIdx.x * C * 2;
-  if (C <= 256) {
-    const int G = 256 / C;
-    const int active = G * C;
-    double s0 = 0.0, s1 = 0.0;
-    if (t < active) {
-      const int c = t % C, g = t / C;
-      for (long m = m0 + g; m < m1; m += G) {
-        double v = y[m * C + c];
-        s0 += v;
-        s1 += v * v;
+  const int rr = t / tpr, cc = t % tpr;
+  const bool active = rr < rpi;
+  const int c4 = g0 + cc;
+  const int seg = blockIdx.z;
+  const long m0 = (long)blockIdx.x * rpc;
+  const long m1 = min(seg_rows, m0 + rpc);
+  const long base = (long)seg * seg_rows;
+  double d0[4] = {0, 0, 0, 0}, d1[4] = {0, 0, 0, 0};
+  if (active) {
+    f.init(seg, c4, base);
+    long m = m0 + rr;
+    while (m < m1) {
+      float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int it = 0; it < 64 && m < m1; ++it, m += rpi) f.accum(base + m, c4, a0, a1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d0[j] += a0[j];
+        d1[j] += a1[j];
       }
     }
-    sh[t][0] = s0;
-    sh[t][1] = s1;
-    __syncthreads();
-    if (t < C) {
-      double a0 = 0.0, a1 = 0.0;
-      for (int g = 0; g < G; ++g) {
-        a0 += sh[g * C + t][0];
-        a1 += sh[g * C + t][1];
+  }
+  __shared__ double sh[256][8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sh[t][j] = d0[j];
+    sh[t][4 + j] = d1[j];
+  }
+  __syncthreads();
+  if (rr == 0) {
+    for (int r = 1; r < rpi; ++r) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        d0[j] += sh[r * tpr + cc][j];
+        d1[j] += sh[r * tpr + cc][4 + j];
       }
-      out[t * 2 + 0] = a0;
-      out[t * 2 + 1] = a1;
     }
-  } else {
-    for (int c = t; c < C; c += 256) {
-      double s0 = 0.0, s1 = 0.0;
-      for (long m = m0; m < m1; ++m) {
-        double v = y[m * C + c];
-        s0 += v;
-        s1 += v * v;
-      }
-      out[c * 2 + 0] = s0;
-      out[c * 2 + 1] = s1;
+    double* out = part + (((long)seg * gridDim.x + blockIdx.x) * C + c4 * 4) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      out[j * 2 + 0] = d0[j];
+      out[j * 2 + 1] = d1[j];
     }
   }
 }
 
-__global__ void k_bn_stats_final(const double* __restrict__ part, int chunks, long M, int C,
-                                 float* __restrict__ mean, float* __restrict__ rstd,
-                                 float* __restrict__ mmean, float* __restrict__ mvar, float eps) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, ss = 0.0;
-  for (int k = 0; k < chunks; ++k) {
-    s += part[((long)k * C + c) * 2 + 0];
-    ss += part[((long)k * C + c) * 2 + 1];
+// sums over chunks: grid (ceil(C/64), nseg), 256 lanes = 64 channels x 4 chunk lanes
+template <class E>
+__global__ __launch_bounds__(256) void k_colred_final(E e, const double* __restrict__ part,
+                                                      int chunks, int C) {
+  const int seg = blockIdx.y;
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s0 = 0.0, s1 = 0.0;
+  if (c < C) {
+    for (int k = g; k < chunks; k += 4) {
+      const double* p = part + (((long)seg * chunks + k) * C + c) * 2;
+      s0 += p[0];
+      s1 += p[1];
+    }
   }
-  double mu = s / (double)M;
-  double var = ss / (double)M - mu * mu;
-  if (var < 0.0) var = 0.0;
-  mean[c] = (float)mu;
-  rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
-  if (mmean) {
-    // Keras: moving -= (moving - batch) * (1 - momentum); the fused op reports the
-    // Bessel-corrected variance for the moving average [TF-recall].
-    double uvar = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    mmean[c] = (float)(mmean[c] - (mmean[c] - mu) * 0.01);
-    mvar[c] = (float)(mvar[c] - (mvar[c] - uvar) * 0.01);
+  __shared__ double sh[256][2];
+  sh[threadIdx.x][0] = s0;
+  sh[threadIdx.x][1] = s1;
+  __syncthreads();
+  if (g == 0 && c < C) {
+    for (int k = 1; k < 4; ++k) {
+      s0 += sh[k * 64 + cl][0];
+      s1 += sh[k * 64 + cl][1];
+    }
+    e(seg, c, s0, s1);
   }
 }
+
+template <class F, class E>
+static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hipStream_t s) {
+  if (C % 4) throw std::runtime_error("colred: C % 4 != 0");
+  RedPlan p = red_plan(seg_rows, C, nseg);
+  hipLaunchKernelGGL((k_colred_part<F>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+                     C, p.rpc, scratch);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL((k_colred_final<E>), dim3(cdiv(C, 64), nseg), dim3(256), 0, s, e, scratch,
+                     p.chunks, C);
+  PHX_LAUNCH_CHECK();
+}
+
+// ---- BN forward statistics ------------------------------------------------------------------
+struct StatsAcc {
+  const float* y;
+  int C;
+  float ref[4];
+  __device__ void init(int, int c4, long base) {
+    float4 r = *reinterpret_cast<const float4*>(y + base * C + c4 * 4);
+    ref[0] = r.x; ref[1] = r.y; ref[2] = r.z; ref[3] = r.w;
+  }
+  __device__ void accum(long m, int c4, float* a0, float* a1) const {
+    float4 v = *reinterpret_cast<const float4*>(y + m * C + c4 * 4);
+    float d[4] = {v.x - ref[0], v.y - ref[1], v.z - ref[2], v.w - ref[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      a0[j] += d[j];
+      a1[j] += d[j] * d[j];
+    }
+  }
+};
+
+struct StatsEpi {
+  const float* y;  // for the shift (row 0)
+  long M;
+  float* mean;
+  float* rstd;
+  float* mmean;
+  float* mvar;
+  float eps;
+  __device__ void operator()(int, int c, double s0, double s1) const {
+    const double ref = y[c];
+    const double dm = s0 / (double)M;            // mean - ref
+    double var = s1 / (double)M - dm * dm;
+    if (var < 0.0) var = 0.0;
+    const double mu = ref + dm;
+    mean[c] = (float)mu;
+    rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    if (mmean) {
+      // Keras: moving -= (moving - batch) * (1 - momentum); the fused op reports the
+      // Bessel-corrected variance for the moving average [TF-recall].
+      double uvar = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      mmean[c] = (float)(mmean[c] - (mmean[c] - mu) * 0.01);
+      mvar[c] = (float)(mvar[c] - (mvar[c] - uvar) * 0.01);
+    }
+  }
+};
 
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
                      float* mmean, float* mvar, float eps, hipStream_t s) {
-  int chunks = red_chunks(M);
-  long rpc = (M + chunks - 1) / chunks;
-  chunks = (int)((M + rpc - 1) / rpc);
-  hipLaunchKernelGGL(k_bn_stats_part, dim3(chunks), dim3(256), 0, s, y, M, C, rpc, part);
-  PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_bn_stats_final, dim3(cdiv(C, 256)), dim3(256), 0, s, part, chunks, M, C,
-                     mean, rstd, mmean, mvar, eps);
-  PHX_LAUNCH_CHECK();
+  StatsAcc f{y, C, {0, 0, 0, 0}};
+  StatsEpi e{y, M, mean, rstd, mmean, mvar, eps};
+  colred(f, e, M, C, 1, part, s);
 }
 
 __global__ void k_bn_frozen_stats(const float* __restrict__ mm, const float* __restrict__ mv,
@@ -151,72 +240,52 @@ void launch_bn_apply(const float* y, const float* mean, const float* rstd, const
 }
 
 // ---- BN backward ----------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_bn_bwd_part(const float* __restrict__ da,
-                                                     const float* __restrict__ y,
-                                                     const float* __restrict__ mean,
-                                                     const float* __restrict__ rstd,
-                                                     const float* __restrict__ gamma,
-                                                     const float* __restrict__ beta, long M, int C,
-                                                     int act, long rows_per_chunk,
-                                                     double* __restrict__ part) {
-  const long m0 = (long)blockIdx.x * rows_per_chunk;
-  const long m1 = min(M, m0 + rows_per_chunk);
-  __shared__ double sh[256][2];
-  const int t = threadIdx.x;
-  double* out = part + (long)blockIdx.x * C * 2;
-  auto elem = [&](long m, int c, double& s0, double& s1) {
-    float yv = y[m * C + c];
-    float xh = (yv - mean[c]) * rstd[c];
-    float dz = da[m * C + c];
-    if (act) dz *= act_grad(xh * gamma[c] + beta[c], act);
-    s0 += dz;
-    s1 += (double)dz * xh;
-  };
-  if (C <= 256) {
-    const int G = 256 / C;
-    const int active = G * C;
-    double s0 = 0.0, s1 = 0.0;
-    if (t < active) {
-      const int c = t % C, g = t / C;
-      for (long m = m0 + g; m < m1; m += G) elem(m, c, s0, s1);
-    }
-    sh[t][0] = s0;
-    sh[t][1] = s1;
-    __syncthreads();
-    if (t < C) {
-      double a0 = 0.0, a1 = 0.0;
-      for (int g = 0; g < G; ++g) {
-        a0 += sh[g * C + t][0];
-        a1 += sh[g * C + t][1];
-      }
-      out[t * 2 + 0] = a0;
-      out[t * 2 + 1] = a1;
-    }
-  } else {
-    for (int c = t; c < C; c += 256) {
-      double s0 = 0.0, s1 = 0.0;
-      for (long m = m0; m < m1; ++m) elem(m, c, s0, s1);
-      out[c * 2 + 0] = s0;
-      out[c * 2 + 1] = s1;
+struct BwdAcc {
+  const float* da;
+  const float* y;
+  const float* mean;
+  const float* rstd;
+  const float* gamma;
+  const float* beta;
+  int C, act;
+  float mu[4], rs[4], ga[4], be[4];
+  __device__ void init(int, int c4, long) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      mu[j] = mean[c4 * 4 + j];
+      rs[j] = rstd[c4 * 4 + j];
+      ga[j] = gamma[c4 * 4 + j];
+      be[j] = beta[c4 * 4 + j];
     }
   }
-}
+  __device__ void accum(long m, int c4, float* a0, float* a1) const {
+    float4 yv = *reinterpret_cast<const float4*>(y + m * C + c4 * 4);
+    float4 gv = *reinterpret_cast<const float4*>(da + m * C + c4 * 4);
+    float ys[4] = {yv.x, yv.y, yv.z, yv.w};
+    float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float xh = (ys[j] - mu[j]) * rs[j];
+      float dz = gs[j];
+      if (act) dz *= act_grad(xh * ga[j] + be[j], act);
+      a0[j] += dz;
+      a1[j] += dz * xh;
+    }
+  }
+};
 
 // coef[c] = {gamma*rstd, mean(dz), mean(dz*xhat)}
-__global__ void k_bn_bwd_final(const double* __restrict__ part, int chunks, long M, int C,
-                               const float* __restrict__ rstd, const float* __restrict__ gamma,
-                               float* __restrict__ coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s = 0.0, sx = 0.0;
-  for (int k = 0; k < chunks; ++k) {
-    s += part[((long)k * C + c) * 2 + 0];
-    sx += part[((long)k * C + c) * 2 + 1];
+struct BwdEpi {
+  long M;
+  const float* rstd;
+  const float* gamma;
+  float* coef;
+  __device__ void operator()(int, int c, double s0, double s1) const {
+    coef[c * 3 + 0] = gamma[c] * rstd[c];
+    coef[c * 3 + 1] = (float)(s0 / (double)M);
+    coef[c * 3 + 2] = (float)(s1 / (double)M);
   }
-  coef[c * 3 + 0] = gamma[c] * rstd[c];
-  coef[c * 3 + 1] = (float)(s / (double)M);
-  coef[c * 3 + 2] = (float)(sx / (double)M);
-}
+};
 
 __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ da,
                                                       const float* __restrict__ y,
@@ -259,15 +328,9 @@ void launch_bn_bwd(const float* da, const float* y, const float* mean, const flo
                    bool frozen, bool acc, double* part, float* coef, hipStream_t s) {
   if (C % 4) throw std::runtime_error("bn_bwd: C % 4");
   if (!frozen) {
-    int chunks = red_chunks(M);
-    long rpc = (M + chunks - 1) / chunks;
-    chunks = (int)((M + rpc - 1) / rpc);
-    hipLaunchKernelGGL(k_bn_bwd_part, dim3(chunks), dim3(256), 0, s, da, y, mean, rstd, gamma, beta,
-                       M, C, act, rpc, part);
-    PHX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(k_bn_bwd_final, dim3(cdiv(C, 256)), dim3(256), 0, s, part, chunks, M, C, rstd,
-                       gamma, coef);
-    PHX_LAUNCH_CHECK();
+    BwdAcc f{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}};
+    BwdEpi e{M, rstd, gamma, coef};
+    colred(f, e, M, C, 1, part, s);
   }
   long n4 = M * C / 4;
   hipLaunchKernelGGL(k_bn_bwd_apply, dim3(cdiv(n4, 256)), dim3(256), 0, s, da, y, mean, rstd, gamma,
@@ -278,48 +341,29 @@ void launch_bn_bwd(const float* da, const float* y, const float* mean, const flo
 // ------------------------------------------------------------------------------------------
 // squeeze-excite (efficientnet_model.py:184-196)
 // ------------------------------------------------------------------------------------------
-// per (image, hw-chunk): partial channel sums of f(x) into part[b][chunk][C]
-template <bool PROD>
-__global__ __launch_bounds__(256) void k_img_chan_part(const float* __restrict__ x,
-                                                       const float* __restrict__ g, int HW, int C,
-                                                       int rows_per_chunk, int chunks,
-                                                       float* __restrict__ part) {
-  const int b = blockIdx.y;
-  const long base = (long)b * HW;
-  const int m0 = blockIdx.x * rows_per_chunk;
-  const int m1 = min(HW, m0 + rows_per_chunk);
-  __shared__ float sh[256];
-  const int t = threadIdx.x;
-  float* out = part + ((long)b * chunks + blockIdx.x) * C;
-  if (C <= 256) {
-    const int G = 256 / C;
-    const int active = G * C;
-    float s0 = 0.f;
-    if (t < active) {
-      const int c = t % C, gg = t / C;
-      for (int m = m0 + gg; m < m1; m += G) {
-        long e = (base + m) * C + c;
-        s0 += PROD ? x[e] * g[e] : x[e];
-      }
+// per-image channel sums: pool (sum x) and backward (sum dy*x) through the column reduction
+struct SumAcc {
+  const float* x;
+  const float* g;  // optional second factor
+  int C;
+  __device__ void init(int, int, long) {}
+  __device__ void accum(long m, int c4, float* a0, float* a1) const {
+    float4 v = *reinterpret_cast<const float4*>(x + m * C + c4 * 4);
+    if (g) {
+      float4 w = *reinterpret_cast<const float4*>(g + m * C + c4 * 4);
+      v.x *= w.x; v.y *= w.y; v.z *= w.z; v.w *= w.w;
     }
-    sh[t] = s0;
-    __syncthreads();
-    if (t < C) {
-      float a0 = 0.f;
-      for (int gg = 0; gg < G; ++gg) a0 += sh[gg * C + t];
-      out[t] = a0;
-    }
-  } else {
-    for (int c = t; c < C; c += 256) {
-      float s0 = 0.f;
-      for (int m = m0; m < m1; ++m) {
-        long e = (base + m) * C + c;
-        s0 += PROD ? x[e] * g[e] : x[e];
-      }
-      out[c] = s0;
-    }
+    a0[0] += v.x; a0[1] += v.y; a0[2] += v.z; a0[3] += v.w;
+    (void)a1;
   }
-}
+};
+struct SumEpi {
+  float* out;  // [seg][C]
+  int C;
+  __device__ void operator()(int seg, int c, double s0, double) const {
+    out[(long)seg * C + c] = (float)s0;
+  }
+};
 
 // one block per image: pool -> fc1(+b1) -> act -> fc2(+b2) -> sigmoid
 __global__ __launch_bounds__(256) void k_se_fc(const float* __restrict__ part, int chunks, int HW,
@@ -334,9 +378,7 @@ __global__ __launch_bounds__(256) void k_se_fc(const float* __restrict__ part, i
   float* sh = sm + C;       // [Cse]
   const int b = blockIdx.x;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < chunks; ++k) s += part[((long)b * chunks + k) * C + c];
-    s = s / (float)HW;
+    float s = part[(long)b * C + c] / (float)HW;  // part: per-image channel sums
     sp[c] = s;
     pool[(long)b * C + c] = s;
   }
@@ -368,28 +410,15 @@ __global__ __launch_bounds__(256) void k_chan_scale(const float* __restrict__ x,
   reinterpret_cast<float4*>(y)[i] = make_float4(v.x * s[0], v.y * s[1], v.z * s[2], v.w * s[3]);
 }
 
-static int se_chunks(int HW, int* rpc) {
-  int chunks = (HW + 1023) / 1024;
-  if (chunks < 1) chunks = 1;
-  if (chunks > 64) chunks = 64;
-  *rpc = (HW + chunks - 1) / chunks;
-  return (HW + *rpc - 1) / *rpc;
-}
-
 void launch_se_fwd(const float* x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
-                   float* hidden, float* scale, hipStream_t s) {
-  int rpc;
-  int chunks = se_chunks(HW, &rpc);
-  // partial sums go to `y` scratch? no: use scale buffer region sized B*64*C via pool arg
-  // (caller guarantees `pool` has room for B*64*C floats followed by the final pool B*C)
-  float* part = pool + (long)B * C;
-  hipLaunchKernelGGL((k_img_chan_part<false>), dim3(chunks, B), dim3(256), 0, s, x, nullptr, HW, C,
-                     rpc, chunks, part);
-  PHX_LAUNCH_CHECK();
+                   float* hidden, float* scale, hipStream_t s, double* scratch) {
+  // per-image channel sums land after the pool vector: pool buffer = [B*C pool | B*C sums]
+  float* sums = pool + (long)B * C;
+  colred(SumAcc{x, nullptr, C}, SumEpi{sums, C}, HW, C, B, scratch, s);
   size_t shm = (size_t)(C + Cse) * sizeof(float);
-  hipLaunchKernelGGL(k_se_fc, dim3(B), dim3(256), shm, s, part, chunks, HW, C, Cse, w1, b1, w2, b2,
-                     act, pool, hidden, scale);
+  hipLaunchKernelGGL(k_se_fc, dim3(B), dim3(256), shm, s, sums, 1, HW, C, Cse, w1, b1, w2, b2, act,
+                     pool, hidden, scale);
   PHX_LAUNCH_CHECK();
   if (y) {
     long n4 = (long)B * HW * C / 4;
@@ -410,8 +439,7 @@ __global__ __launch_bounds__(256) void k_se_fc_bwd(const float* __restrict__ par
   float* dh = sm + C;    // [Cse]
   const int b = blockIdx.x;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float g = 0.f;
-    for (int k = 0; k < chunks; ++k) g += part[((long)b * chunks + k) * C + c];
+    float g = part[(long)b * C + c];  // per-image sum_hw dy * x
     float sv = scale[(long)b * C + c];
     de[c] = g * sv * (1.f - sv);
   }
@@ -456,17 +484,13 @@ __global__ __launch_bounds__(256) void k_se_bwd_apply(const float* __restrict__ 
 void launch_se_bwd(const float* dy, const float* x, float* dx, int B, int HW, int C, int Cse,
                    const float* w1, const float* b1, const float* w2, const float* b2, int act,
                    const float* pool, const float* hidden, const float* scale, float* gsum,
-                   bool acc, hipStream_t s) {
+                   bool acc, hipStream_t s, double* scratch) {
   (void)b1; (void)b2; (void)pool;
-  int rpc;
-  int chunks = se_chunks(HW, &rpc);
-  float* part = gsum + (long)B * C;  // gsum: B*C dpool followed by B*64*C partials
-  hipLaunchKernelGGL((k_img_chan_part<true>), dim3(chunks, B), dim3(256), 0, s, x, dy, HW, C, rpc,
-                     chunks, part);
-  PHX_LAUNCH_CHECK();
+  float* sums = gsum + (long)B * C;  // gsum: [B*C dpool | B*C sum_hw dy*x]
+  colred(SumAcc{x, dy, C}, SumEpi{sums, C}, HW, C, B, scratch, s);
   size_t shm = (size_t)(C + Cse) * sizeof(float);
-  hipLaunchKernelGGL(k_se_fc_bwd, dim3(B), dim3(256), shm, s, part, chunks, C, Cse, w1, w2, act,
-                     hidden, scale, gsum);
+  hipLaunchKernelGGL(k_se_fc_bwd, dim3(B), dim3(256), shm, s, sums, 1, C, Cse, w1, w2, act, hidden,
+                     scale, gsum);
   PHX_LAUNCH_CHECK();
   long n4 = (long)B * HW * C / 4;
   hipLaunchKernelGGL(k_se_bwd_apply, dim3(cdiv(n4, 256)), dim3(256), 0, s, dy, scale, gsum, dx, n4,

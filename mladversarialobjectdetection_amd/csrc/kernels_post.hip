@@ -18,8 +18,12 @@ namespace phx {
 __device__ __forceinline__ float sigmoid_exact(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------------------------------
-// pre_nms + masks: one lane per (image, anchor)
+// pre_nms + masks.  A workgroup owns a tile of 128 consecutive anchors of one (image, level):
+// their 128 x 90 logits are one contiguous 46 KB run, staged into LDS with float4 loads, then
+// lane t reduces anchor t's 90 classes (max, first argmax) and decodes its box.
 // ------------------------------------------------------------------------------------------
+constexpr int kPreTile = 128;
+
 __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_base,
                                                  const float* __restrict__ box_base,
                                                  const LevelDesc* __restrict__ lev, int nlev,
@@ -29,39 +33,49 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
                                                  int* __restrict__ classes,
                                                  float* __restrict__ boxes,
                                                  uint8_t* __restrict__ keep) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)B * A) return;
-  const int b = (int)(idx / A), a = (int)(idx % A);
+  extern __shared__ float4 smem4[];
+  float* lg_s = reinterpret_cast<float*>(smem4);
+  const int b = blockIdx.y;
   int l = 0;
-  while (l + 1 < nlev && a >= lev[l + 1].anchor0) ++l;
+  while (l + 1 < nlev && (int)blockIdx.x >= lev[l + 1].tile0) ++l;
   const LevelDesc L = lev[l];
-  const int local = a - L.anchor0;
-  const int pix = local / na, k = local % na;
-  const long prow = (long)b * L.h * L.w + pix;
-  const float* lg = cls_base + L.cls_off + prow * (na * nclass) + (long)k * nclass;
+  const int nloc = L.h * L.w * na;                      // anchors of this level per image
+  const int a0 = ((int)blockIdx.x - L.tile0) * kPreTile;  // first local anchor of the tile
+  const int n = min(kPreTile, nloc - a0);
+  const long run = ((long)b * nloc + a0) * nclass;      // float offset of the tile's logits
+  const float* src = cls_base + L.cls_off + run;
+  const int nf = n * nclass;
+  const int nf4 = nf >> 2;
+  const float4* src4 = reinterpret_cast<const float4*>(src);
+  for (int i = threadIdx.x; i < nf4; i += blockDim.x) smem4[i] = src4[i];
+  for (int i = (nf4 << 2) + threadIdx.x; i < nf; i += blockDim.x) lg_s[i] = src[i];
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t >= n) return;
+  const float* lg = lg_s + t * nclass;
   float m = lg[0];
   int am = 0;
   for (int c = 1; c < nclass; ++c) {
     float v = lg[c];
     if (v > m) { m = v; am = c; }
   }
-  const float* bx = box_base + L.box_off + prow * (na * 4) + (long)k * 4;
-  const float* an = anchors + (long)a * 4;
-  float yca = (an[0] + an[2]) / 2.0f;
-  float xca = (an[1] + an[3]) / 2.0f;
-  float ha = an[2] - an[0];
-  float wa = an[3] - an[1];
-  float ty = bx[0], tx = bx[1], th = bx[2], tw = bx[3];
-  float w = expf(tw) * wa;
-  float h = expf(th) * ha;
-  float yc = ty * ha + yca;
-  float xc = tx * wa + xca;
+  const int a = L.anchor0 + a0 + t;
+  const long idx = (long)b * A + a;
+  const float4 bx = *reinterpret_cast<const float4*>(box_base + L.box_off + ((long)b * nloc + a0 + t) * 4);
+  const float4 an = *reinterpret_cast<const float4*>(anchors + (long)a * 4);
+  float yca = (an.x + an.z) / 2.0f;
+  float xca = (an.y + an.w) / 2.0f;
+  float ha = an.z - an.x;
+  float wa = an.w - an.y;
+  float w = expf(bx.w) * wa;
+  float h = expf(bx.z) * ha;
+  float yc = bx.x * ha + yca;
+  float xc = bx.y * wa + xca;
   float ymin = yc - h / 2.0f, xmin = xc - w / 2.0f, ymax = yc + h / 2.0f, xmax = xc + w / 2.0f;
-  float s = sigmoid_exact(m);
-  scores[idx] = s;
+  float sc = sigmoid_exact(m);
+  scores[idx] = sc;
   classes[idx] = am;
-  float* ob = boxes + idx * 4;
-  ob[0] = ymin; ob[1] = xmin; ob[2] = ymax; ob[3] = xmax;
+  *reinterpret_cast<float4*>(boxes + idx * 4) = make_float4(ymin, xmin, ymax, xmax);
   // filter_valid_boxes (attacker.py:69-89): boxes_h/w from the decoded box
   float bh = ymax - ymin, bw = xmax - xmin;
   float area = bh * bw;
@@ -69,7 +83,7 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
   uint8_t kf = 0;
   if (am == 0 && valid) {
     kf = 1;
-    if (s >= thresh) kf |= 2;
+    if (sc >= thresh) kf |= 2;
   }
   keep[idx] = kf;
 }
@@ -77,13 +91,14 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
-                    float* boxes, uint8_t* keep, hipStream_t s) {
-  long n = (long)B * A;
-  hipLaunchKernelGGL(k_pre_nms, dim3(cdiv(n, 256)), dim3(256), 0, s, cls_base, box_base, lev_dev,
-                     nlev, anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes,
-                     keep);
+                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s) {
+  size_t shm = (size_t)kPreTile * nclass * sizeof(float);
+  hipLaunchKernelGGL(k_pre_nms, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,
+                     anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes, keep);
   PHX_LAUNCH_CHECK();
 }
+
+int pre_nms_tiles(int h, int w, int na) { return (h * w * na + kPreTile - 1) / kPreTile; }
 
 // ------------------------------------------------------------------------------------------
 // soft-NMS: one workgroup per image.  Exact restatement of NonMaxSuppressionV5's lazy
@@ -130,37 +145,38 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   __shared__ int red_i[kNmsThreads];
   __shared__ int s_done;
 
-  // 1. ordered compaction of candidates with score > thresh (and mask)
-  if (t == 0) s_n = 0;
+  // 1. ordered compaction of candidates with score > thresh (and mask): every lane owns a
+  //    contiguous segment, one workgroup scan of the segment counts places them
+  auto ok_at = [&](int i) -> bool {
+    bool ok = sb[i] > score_thresh;
+    if (keep) ok = ok && ((keep[(long)b * N + i] & keep_mask) != 0);
+    return ok;
+  };
+  const int per = (n_in + kNmsThreads - 1) / kNmsThreads;
+  const int lo = min(n_in, t * per), hi = min(n_in, lo + per);
+  int cnt = 0;
+  for (int i = lo; i < hi; ++i) cnt += ok_at(i) ? 1 : 0;
+  red_i[t] = cnt;
   __syncthreads();
-  for (int base = 0; base < n_in; base += kNmsThreads) {
-    int i = base + t;
-    bool ok = false;
-    if (i < n_in) {
-      ok = sb[i] > score_thresh;
-      if (keep) ok = ok && ((keep[(long)b * N + i] & keep_mask) != 0);
-    }
-    // block-wide exclusive scan of ok
-    red_i[t] = ok ? 1 : 0;
+  for (int off = 1; off < kNmsThreads; off <<= 1) {
+    int v = (t >= off) ? red_i[t - off] : 0;
     __syncthreads();
-    for (int off = 1; off < kNmsThreads; off <<= 1) {
-      int v = (t >= off) ? red_i[t - off] : 0;
-      __syncthreads();
-      red_i[t] += v;
-      __syncthreads();
-    }
-    int incl = red_i[t];
-    int total = red_i[kNmsThreads - 1];
-    if (ok) {
-      int pos = s_n + incl - 1;
-      wi[pos] = i;
-      ws[pos] = sb[i];
-      wb[pos] = 0;
-    }
-    __syncthreads();
-    if (t == 0) s_n += total;
+    red_i[t] += v;
     __syncthreads();
   }
+  {
+    int pos = red_i[t] - cnt;
+    for (int i = lo; i < hi; ++i) {
+      if (ok_at(i)) {
+        wi[pos] = i;
+        ws[pos] = sb[i];
+        wb[pos] = 0;
+        ++pos;
+      }
+    }
+  }
+  if (t == kNmsThreads - 1) s_n = red_i[t];
+  __syncthreads();
   const int n = s_n;
   if (t == 0) { s_nsel = 0; s_done = 0; }
   __syncthreads();
