@@ -50,7 +50,11 @@ struct Exec {
   double* red = nullptr;                       // BN partial sums
   float* coef = nullptr;                       // BN backward coefficients
   float* se_g = nullptr;                       // SE backward scratch
+  float* gpart = nullptr;                      // split-K GEMM partial slabs
   std::vector<int> se_of_tensor;               // tensor id -> SE op index producing it (-1)
+  std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
+  std::vector<int> bn_consumer;                // tensor id -> BN op index reading it (-1)
+  std::vector<float*> slot_d, slot_e;          // BN backward: mean(dz), mean(dz*xhat)
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -261,12 +265,23 @@ Exec& phx_ctx::exec_for(int B) {
   E.slot_c.assign(P.n_slots, nullptr);
   size_t red_need = 1, coef_need = 1, seg_need = 1;
   E.se_of_tensor.assign(P.tensors.size(), -1);
+  E.bn_of_tensor.assign(P.tensors.size(), -1);
+  E.bn_consumer.assign(P.tensors.size(), -1);
+  E.slot_d.assign(P.n_slots, nullptr);
+  E.slot_e.assign(P.n_slots, nullptr);
   for (size_t i = 0; i < P.ops.size(); ++i) {
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
     if (op.t == OP_BN) {
       E.slot_a[op.slot] = E.alloc<float>(ti.c);
       E.slot_b[op.slot] = E.alloc<float>(ti.c);
+      E.slot_c[op.slot] = E.alloc<float>(ti.c);
+      E.slot_d[op.slot] = E.alloc<float>(ti.c);
+      E.slot_e[op.slot] = E.alloc<float>(ti.c);
+      PHX_HIP(hipMemset(E.slot_d[op.slot], 0, ti.c * sizeof(float)));
+      PHX_HIP(hipMemset(E.slot_e[op.slot], 0, ti.c * sizeof(float)));
+      E.bn_of_tensor[op.out] = (int)i;
+      E.bn_consumer[op.in[0]] = (int)i;
       red_need = std::max(red_need, bn_stats_scratch_doubles((long)ti.rows(), ti.c));
       coef_need = std::max(coef_need, (size_t)ti.c * 3);
     } else if (op.t == OP_SE) {
@@ -278,6 +293,15 @@ Exec& phx_ctx::exec_for(int B) {
       E.se_of_tensor[op.out] = (int)i;
     }
   }
+  size_t gp_need = 1;
+  for (const Op& op : P.ops) {
+    if (op.t != OP_PW) continue;
+    const Tensor& ti = P.tensors[op.in[0]];
+    const Tensor& to = P.tensors[op.out];
+    gp_need = std::max(gp_need, gemm_partial_floats((int)ti.rows(), to.c, ti.c));  // forward
+    gp_need = std::max(gp_need, gemm_partial_floats((int)ti.rows(), ti.c, to.c));  // dgrad
+  }
+  E.gpart = E.alloc<float>(gp_need);
   E.red = E.alloc<double>(red_need);
   E.coef = E.alloc<float>(coef_need);
   E.se_g = E.alloc<float>(seg_need);
@@ -363,6 +387,26 @@ Exec& phx_ctx::exec_for(int B) {
 
 namespace {
 
+// How consumers see tensor t: BN outputs are virtual (BN input + per-channel transform).
+InX view(phx_ctx* ctx, const Exec& E, int t, const float* input) {
+  int bi = E.bn_of_tensor[t];
+  if (bi < 0) return InX{E.tptr(t, input), nullptr, nullptr, nullptr, 0};
+  const Op& op = E.prog.ops[bi];
+  return InX{E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_c[op.slot], ctx->w() + op.beta, op.act};
+}
+
+// The gradient w.r.t. tensor t as its producer's dgrad sees it: for a BN input the BN backward
+// is applied on load (GradX); otherwise the materialised gradient.
+GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
+  int bi = E.bn_consumer[t];
+  if (bi >= 0 && E.prog.ops[bi].bwd) {
+    const Op& op = E.prog.ops[bi];
+    return GradX{E.gptr(op.out), E.tptr(t, input), E.slot_a[op.slot], E.slot_b[op.slot],
+                 E.slot_c[op.slot], ctx->w() + op.beta, E.slot_d[op.slot], E.slot_e[op.slot], op.act};
+  }
+  return GradX{E.gptr(t), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+}
+
 // victim forward over the program (EfficientDetNet.call, efficientdet_keras.py:884-906)
 void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
   const Program& P = E.prog;
@@ -380,7 +424,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_STEM: kind = "stem_fwd"; fl = 2.0 * to.numel() * 27; break;
       case OP_PW: kind = "gemm"; fl = 2.0 * ti.rows() * ti.c * to.c; by += 4.0 * ti.c * to.c; break;
       case OP_DW: kind = "dw_fwd"; fl = 2.0 * to.numel() * op.k * op.k; break;
-      case OP_BN: kind = "bn_fwd"; by = 4.0 * (2.0 * ti.numel() + to.numel()); break;
+      case OP_BN: kind = "bn_stats"; by = 4.0 * ti.numel(); break;
       case OP_SE: kind = "se_fwd"; by = 4.0 * ti.numel(); break;
       default: break;
     }
@@ -390,58 +434,60 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s);
         break;
       case OP_PW: {
-        const float* A = x;
+        InX A = view(ctx, E, op.in[0], input);
         const float* rs = nullptr;
         int rpi = 1;
         int se = E.se_of_tensor[op.in[0]];
         if (se >= 0) {  // SE excitation folded into the GEMM's A load
           const Op& sop = P.ops[se];
-          A = E.tptr(sop.in[0], input);
+          A = view(ctx, E, sop.in[0], input);
           rs = E.slot_c[sop.slot];
           rpi = ti.h * ti.w;
         }
         launch_gemm(A, ctx->wt_of(op.w), op.b >= 0 ? W + op.b : nullptr, y, (int)ti.rows(), to.c,
-                    ti.c, false, rs, rpi, s);
+                    ti.c, false, rs, rpi, s, E.gpart);
         break;
       }
       case OP_DW:
-        launch_dw_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
+        launch_dw_fwd(view(ctx, E, op.in[0], input), W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
                       op.pad_l, s);
         break;
       case OP_BN: {
         float* mean = E.slot_a[op.slot];
         float* rstd = E.slot_b[op.slot];
+        // statistics only: the normalised output is applied by every consumer on load (InX)
         if (frozen)
-          launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, ti.c, kBnEps, s);
+          launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
+                                 E.slot_c[op.slot], ti.c, kBnEps, s);
         else
-          launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.mmean, W + op.mvar,
-                          kBnEps, s);
-        launch_bn_apply(x, mean, rstd, W + op.gamma, W + op.beta, y, (long)ti.rows(), ti.c, op.act,
-                        s);
+          launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.gamma,
+                          E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
+        (void)y;
         break;
       }
       case OP_SE:
-        launch_se_fwd(x, nullptr, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1, W + op.b1, W + op.w2,
+        launch_se_fwd(view(ctx, E, op.in[0], input), nullptr, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1, W + op.b1, W + op.w2,
                       W + op.b2, op.act, E.slot_a[op.slot], E.slot_b[op.slot], E.slot_c[op.slot], s,
                       E.red);
         break;
       case OP_ADD:
-        launch_add(x, E.tptr(op.in[1], input), y, (long)to.numel(), s);
+        launch_add(view(ctx, E, op.in[0], input), view(ctx, E, op.in[1], input), y,
+                   (long)to.numel(), to.c, s);
         break;
       case OP_MAXPOOL:
-        launch_maxpool_fwd(x, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
+        launch_maxpool_fwd(view(ctx, E, op.in[0], input), y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
                            op.pad_l, s);
         break;
       case OP_UPSAMPLE:
-        launch_upsample_fwd(x, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, s);
+        launch_upsample_fwd(view(ctx, E, op.in[0], input), y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, s);
         break;
       case OP_FUSE: {
-        const float* xs[3] = {nullptr, nullptr, nullptr};
-        for (int k = 0; k < op.nin; ++k) xs[k] = E.tptr(op.in[k], input);
+        InX xs[3] = {};
+        for (int k = 0; k < op.nin; ++k) xs[k] = view(ctx, E, op.in[k], input);
         launch_fuse_fwd(xs, op.nin, op.wsm[0] >= 0 ? W + op.wsm[0] : nullptr,
                         op.wsm[1] >= 0 ? W + op.wsm[1] : nullptr,
                         op.wsm[2] >= 0 ? W + op.wsm[2] : nullptr, op.fuse_method, op.act, y,
-                        (long)to.numel(), s);
+                        (long)to.numel(), to.c, s);
         break;
       }
     }
@@ -488,31 +534,47 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_STEM: kind = "stem_bwd"; fl = 2.0 * to.numel() * 27; break;
       case OP_PW: kind = "gemm"; fl = 2.0 * ti.rows() * ti.c * to.c; by += 4.0 * ti.c * to.c; break;
       case OP_DW: kind = "dw_bwd"; fl = 2.0 * to.numel() * op.k * op.k; break;
-      case OP_BN: kind = "bn_bwd"; by = 4.0 * (4.0 * ti.numel() + to.numel()); break;
+      case OP_BN: kind = "bn_bwd_reduce"; by = 4.0 * 2.0 * ti.numel(); break;
       case OP_SE: kind = "se_bwd"; by = 4.0 * 3.0 * ti.numel(); break;
       default: break;
     }
     Scope scope(ctx, kind, fl, by, s);
     switch (op.t) {
-      case OP_STEM:
-        launch_stem_bwd(dy, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
+      case OP_STEM: {
+        // the stem dgrad reads each dy element up to 4x: materialise the BN-backward output once
+        GradX g = gview(ctx, E, op.out, input);
+        if (g.y) {
+          const int bi = E.bn_consumer[op.out];
+          const Op& bop = P.ops[bi];
+          float* gy = E.gptr(op.out);
+          launch_bn_bwd_apply2(g, gy, (long)to.rows(), to.c, s);
+          g = GradX{gy, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+          (void)bop;
+        }
+        launch_stem_bwd(g, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
                         op.acc[0], s);
         break;
+      }
       case OP_PW:
         // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
-        launch_gemm(dy, W + op.w, nullptr, dx, (int)ti.rows(), ti.c, to.c, op.acc[0], nullptr, 1, s);
+        launch_gemm_dgrad(gview(ctx, E, op.out, input), W + op.w, dx, (int)ti.rows(), ti.c, to.c,
+                          op.acc[0], s, E.gpart);
         break;
       case OP_DW:
-        launch_dw_bwd(dy, W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride,
+        launch_dw_bwd(gview(ctx, E, op.out, input), W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride,
                       op.pad_t, op.pad_l, op.acc[0], s);
         break;
       case OP_BN:
-        launch_bn_bwd(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
-                      W + op.gamma, W + op.beta, dx, (long)ti.rows(), ti.c, op.act, frozen,
-                      op.acc[0], E.red, E.coef, s);
+        // reduction only; the apply half runs in the producer's dgrad (gview)
+        if (op.acc[0]) throw std::runtime_error("BN input with several consumers");
+        if (!frozen)
+          launch_bn_bwd_reduce(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
+                               W + op.gamma, W + op.beta, (long)ti.rows(), ti.c, op.act, E.red,
+                               E.slot_d[op.slot], E.slot_e[op.slot], s);
+        (void)dx;
         break;
       case OP_SE:
-        launch_se_bwd(dy, E.tptr(op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
+        launch_se_bwd(dy, view(ctx, E, op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
                       W + op.b1, W + op.w2, W + op.b2, op.act, E.slot_a[op.slot],
                       E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s, E.red);
         break;
@@ -521,25 +583,25 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s);
         break;
       case OP_MAXPOOL:
-        launch_maxpool_bwd(E.tptr(op.in[0], input), dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w,
+        launch_maxpool_bwd(view(ctx, E, op.in[0], input), dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w,
                            op.k, op.stride, op.pad_t, op.pad_l, op.acc[0], s);
         break;
       case OP_UPSAMPLE:
         launch_upsample_bwd(dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.acc[0], s);
         break;
       case OP_FUSE: {
-        const float* xs[3] = {nullptr, nullptr, nullptr};
+        InX xs[3] = {};
         float* dxs[3] = {nullptr, nullptr, nullptr};
         bool acc[3] = {false, false, false};
         for (int k = 0; k < op.nin; ++k) {
-          xs[k] = E.tptr(op.in[k], input);
+          xs[k] = view(ctx, E, op.in[k], input);
           dxs[k] = E.gptr(op.in[k]);
           acc[k] = op.acc[k];
         }
         launch_fuse_bwd(xs, op.nin, op.wsm[0] >= 0 ? W + op.wsm[0] : nullptr,
                         op.wsm[1] >= 0 ? W + op.wsm[1] : nullptr,
                         op.wsm[2] >= 0 ? W + op.wsm[2] : nullptr, op.fuse_method, op.act, dy, dxs,
-                        acc, (long)to.numel(), s);
+                        acc, (long)to.numel(), to.c, s);
         break;
       }
     }

@@ -48,6 +48,116 @@ __device__ __forceinline__ float act_grad(float z, int act) {
 }
 
 // ------------------------------------------------------------------------------------------
+// InX: an input tensor as its consumers see it.  The output of a training-mode batch norm is
+// never materialised: consumers read the BN input y and apply a = act((y - mu) * sc + be) on
+// load (sc = gamma * rstd, be = beta), so every BN costs one statistics pass instead of a
+// statistics pass plus a read-modify-write pass over HBM.  mu == nullptr means a raw tensor.
+// ------------------------------------------------------------------------------------------
+struct InX {
+  const float* p;
+  const float* mu;
+  const float* sc;
+  const float* be;
+  int act;
+};
+
+struct Chan4 {
+  float mu[4], sc[4], be[4];
+};
+
+__device__ __forceinline__ Chan4 inx_chan4(const InX& v, int c) {
+  Chan4 k;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    k.mu[j] = v.mu[c + j];
+    k.sc[j] = v.sc[c + j];
+    k.be[j] = v.be[c + j];
+  }
+  return k;
+}
+
+__device__ __forceinline__ float4 inx_apply4(const InX& v, const Chan4& k, float4 x) {
+  x.x = act_fwd((x.x - k.mu[0]) * k.sc[0] + k.be[0], v.act);
+  x.y = act_fwd((x.y - k.mu[1]) * k.sc[1] + k.be[1], v.act);
+  x.z = act_fwd((x.z - k.mu[2]) * k.sc[2] + k.be[2], v.act);
+  x.w = act_fwd((x.w - k.mu[3]) * k.sc[3] + k.be[3], v.act);
+  return x;
+}
+
+// element e (flat index) of channel c
+__device__ __forceinline__ float inx_load1(const InX& v, long e, int c) {
+  float x = v.p[e];
+  if (v.mu) x = act_fwd((x - v.mu[c]) * v.sc[c] + v.be[c], v.act);
+  return x;
+}
+
+// 4 consecutive channels c..c+3 at flat index e
+__device__ __forceinline__ float4 inx_load4(const InX& v, long e, int c) {
+  float4 x = *reinterpret_cast<const float4*>(v.p + e);
+  if (v.mu) x = inx_apply4(v, inx_chan4(v, c), x);
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------
+// GradX: the gradient w.r.t. a BN input y as its consumer (the producing conv's dgrad) sees
+// it.  The BN backward only reduces sum(dz) and sum(dz*xhat); the consumer rebuilds
+//   dy = sc * (dz - mdz - xhat * mdzx),  dz = da * act'(z),  z = (y-mu)*sc + be,
+//   xhat = (y - mu) * rstd
+// on load, so dy is never written to HBM.  y == nullptr means da is the gradient itself.
+// ------------------------------------------------------------------------------------------
+struct GradX {
+  const float* da;
+  const float* y;
+  const float* mu;
+  const float* rstd;
+  const float* sc;
+  const float* be;
+  const float* mdz;
+  const float* mdzx;
+  int act;
+};
+
+struct GChan4 {
+  float4 mu, rs, sc, be, m1, m2;
+};
+
+__device__ __forceinline__ GChan4 gx_chan4(const GradX& g, int c) {
+  GChan4 k;
+  k.mu = *reinterpret_cast<const float4*>(g.mu + c);
+  k.rs = *reinterpret_cast<const float4*>(g.rstd + c);
+  k.sc = *reinterpret_cast<const float4*>(g.sc + c);
+  k.be = *reinterpret_cast<const float4*>(g.be + c);
+  k.m1 = *reinterpret_cast<const float4*>(g.mdz + c);
+  k.m2 = *reinterpret_cast<const float4*>(g.mdzx + c);
+  return k;
+}
+
+__device__ __forceinline__ float gx_one(float d, float y, float mu, float rs, float sc, float be,
+                                        float m1, float m2, int act) {
+  const float yc = y - mu;
+  float dz = d;
+  if (act) dz *= act_grad(yc * sc + be, act);
+  return sc * (dz - m1 - (yc * rs) * m2);
+}
+
+__device__ __forceinline__ float4 gx_apply4(const GradX& g, const GChan4& k, float4 d, float4 y) {
+  float4 o;
+  o.x = gx_one(d.x, y.x, k.mu.x, k.rs.x, k.sc.x, k.be.x, k.m1.x, k.m2.x, g.act);
+  o.y = gx_one(d.y, y.y, k.mu.y, k.rs.y, k.sc.y, k.be.y, k.m1.y, k.m2.y, g.act);
+  o.z = gx_one(d.z, y.z, k.mu.z, k.rs.z, k.sc.z, k.be.z, k.m1.z, k.m2.z, g.act);
+  o.w = gx_one(d.w, y.w, k.mu.w, k.rs.w, k.sc.w, k.be.w, k.m1.w, k.m2.w, g.act);
+  return o;
+}
+
+// 4 consecutive channels c..c+3 at flat index e
+__device__ __forceinline__ float4 gx_load4(const GradX& g, long e, int c) {
+  float4 d = *reinterpret_cast<const float4*>(g.da + e);
+  if (!g.y) return d;
+  float4 y = *reinterpret_cast<const float4*>(g.y + e);
+  return gx_apply4(g, gx_chan4(g, c), d, y);
+}
+
+// ------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11), counter-based: identical draws for a given
 // (key, counter) on any device / GPU count.  Matches oracle/philox.py bit for bit.
 // ------------------------------------------------------------------------------------------

@@ -6,6 +6,8 @@
 #include <cstddef>
 #include <cstdint>
 
+#include "common.hpp"
+
 namespace phx {
 
 // ---- convolutions (kernels_conv.hip) ------------------------------------------------------
@@ -13,16 +15,25 @@ namespace phx {
 void launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                      int Co, int pt, int pl, hipStream_t s);
 // dx [B,H,W,3] (+)= conv_transpose(dy)
-void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
+void launch_stem_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int Ho,
                      int Wo, int Co, int pt, int pl, bool acc, hipStream_t s);
 // C[M,N] (+)= A[M,K] * B + bias ; B given as Bt[N][K].  rowscale (optional): A[m,k] is
 // multiplied by rowscale[(m / rows_per_img) * K + k] (SE excitation folded into the load).
-void launch_gemm(const float* A, const float* Bt, const float* bias, float* C, int M, int N, int K,
-                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s);
+struct GemmPlan {
+  int nt, wm, gx, gy, splits, kslice;
+};
+GemmPlan plan_gemm(int M, int N, int K);
+size_t gemm_partial_floats(int M, int N, int K);
+void launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
+                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+                 float* partial);
+// dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
+void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
+                       hipStream_t s, float* partial);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
-void launch_dw_fwd(const float* x, const float* w, float* y, int B, int H, int W, int C, int Ho,
+void launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
                    int Wo, int k, int stride, int pt, int pl, hipStream_t s);
-void launch_dw_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
+void launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
                    int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s);
 void launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);
 
@@ -31,10 +42,11 @@ void launch_transpose(const float* in, float* out, int rows, int cols, hipStream
 // (momentum 0.99, util_keras.py:33-35) when mmean != nullptr.  part: scratch (doubles).
 size_t bn_stats_scratch_doubles(long M, int C);
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
-                     float* mmean, float* mvar, float eps, hipStream_t s);
+                     const float* gamma, float* sc, float* mmean, float* mvar, float eps,
+                     hipStream_t s);
 // frozen BN: mean/rstd from moving statistics
-void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd, int C,
-                            float eps, hipStream_t s);
+void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd,
+                            const float* gamma, float* sc, int C, float eps, hipStream_t s);
 // a = act(gamma * (y - mean) * rstd + beta)
 void launch_bn_apply(const float* y, const float* mean, const float* rstd, const float* gamma,
                      const float* beta, float* a, long M, int C, int act, hipStream_t s);
@@ -43,34 +55,42 @@ void launch_bn_apply(const float* y, const float* mean, const float* rstd, const
 void launch_bn_bwd(const float* da, const float* y, const float* mean, const float* rstd,
                    const float* gamma, const float* beta, float* dy, long M, int C, int act,
                    bool frozen, bool acc, double* part, float* coef, hipStream_t s);
+// materialise a gradient view: out[M,C] = gx(view)
+void launch_bn_bwd_apply2(GradX g, float* out, long M, int C, hipStream_t s);
+// reduction half of the BN backward: mdz[c] = mean(dz), mdzx[c] = mean(dz*xhat); the apply
+// half runs inside the consumer through a GradX view
+void launch_bn_bwd_reduce(const float* da, const float* y, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, long M, int C, int act,
+                          double* part, float* mdz, float* mdzx, hipStream_t s);
 // squeeze-excite forward: pool[B,C] = mean_hw(x); scale[B,C]; y = x * scale
-void launch_se_fwd(const float* x, float* y, int B, int HW, int C, int Cse, const float* w1,
+void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
                    float* hidden, float* scale, hipStream_t s, double* scratch);
-void launch_se_bwd(const float* dy, const float* x, float* dx, int B, int HW, int C, int Cse,
+void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
                    const float* w1, const float* b1, const float* w2, const float* b2, int act,
                    const float* pool, const float* hidden, const float* scale, float* gsum,
                    bool acc, hipStream_t s, double* scratch);
 size_t colred_scratch_doubles(long seg_rows, int C, int nseg);
-void launch_add(const float* a, const float* b, float* y, long n, hipStream_t s);
+void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s);
 // dst (+)= src
 void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s);
-void launch_maxpool_fwd(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+void launch_maxpool_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
                         int k, int stride, int pt, int pl, hipStream_t s);
-void launch_maxpool_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
+void launch_maxpool_bwd(InX x, const float* dy, float* dx, int B, int H, int W, int C,
                         int Ho, int Wo, int k, int stride, int pt, int pl, bool acc,
                         hipStream_t s);
-void launch_upsample_fwd(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+void launch_upsample_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
                          hipStream_t s);
 void launch_upsample_bwd(const float* dy, float* dx, int B, int H, int W, int C, int Ho, int Wo,
                          bool acc, hipStream_t s);
 // BiFPN fuse: y = act(sum_i x_i * w_i / (sum_j w_j + 1e-4)) (fastattn, w = relu(wsm)) or
 // act(sum_i x_i) (method 1)
-void launch_fuse_fwd(const float* const* xs, int nin, const float* wsm0, const float* wsm1,
-                     const float* wsm2, int method, int act, float* y, long n, hipStream_t s);
-void launch_fuse_bwd(const float* const* xs, int nin, const float* wsm0, const float* wsm1,
+void launch_fuse_fwd(const InX* xs, int nin, const float* wsm0, const float* wsm1,
+                     const float* wsm2, int method, int act, float* y, long n, int C,
+                     hipStream_t s);
+void launch_fuse_bwd(const InX* xs, int nin, const float* wsm0, const float* wsm1,
                      const float* wsm2, int method, int act, const float* dy, float* const* dxs,
-                     const bool* acc, long n, hipStream_t s);
+                     const bool* acc, long n, int C, hipStream_t s);
 
 // ---- detection post-processing (kernels_post.hip) -----------------------------------------
 struct LevelDesc {

@@ -31,7 +31,7 @@ static RedPlan red_plan(long seg_rows, int C, int nseg) {
   p.cgroups = (tpr_total + 255) / 256;
   p.tpr = tpr_total < 256 ? tpr_total : 256;
   int rpi = 256 / p.tpr;
-  long target_blocks = 2048;
+  long target_blocks = 1024;
   long per_seg = target_blocks / (nseg * p.cgroups);
   if (per_seg < 1) per_seg = 1;
   long rpc = (seg_rows + per_seg - 1) / per_seg;
@@ -102,19 +102,19 @@ __global__ __launch_bounds__(256) void k_colred_part(F f, long seg_rows, int C, 
   }
 }
 
-// sums over chunks: grid (ceil(C/64), nseg), 256 lanes = 64 channels x 4 chunk lanes
+// sums over chunks: grid (ceil(C/16), nseg), 256 lanes = 16 channels x 16 chunk lanes
 template <class E>
 __global__ __launch_bounds__(256) void k_colred_final(E e, const double* __restrict__ part,
                                                       int chunks, int C) {
   const int seg = blockIdx.y;
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int cl = threadIdx.x & 15, g = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double s0 = 0.0, s1 = 0.0;
   if (c < C) {
-    for (int k = g; k < chunks; k += 4) {
-      const double* p = part + (((long)seg * chunks + k) * C + c) * 2;
-      s0 += p[0];
-      s1 += p[1];
+    for (int k = g; k < chunks; k += 16) {
+      const double2 p = *reinterpret_cast<const double2*>(part + (((long)seg * chunks + k) * C + c) * 2);
+      s0 += p.x;
+      s1 += p.y;
     }
   }
   __shared__ double sh[256][2];
@@ -122,9 +122,9 @@ __global__ __launch_bounds__(256) void k_colred_final(E e, const double* __restr
   sh[threadIdx.x][1] = s1;
   __syncthreads();
   if (g == 0 && c < C) {
-    for (int k = 1; k < 4; ++k) {
-      s0 += sh[k * 64 + cl][0];
-      s1 += sh[k * 64 + cl][1];
+    for (int k = 1; k < 16; ++k) {
+      s0 += sh[k * 16 + cl][0];
+      s1 += sh[k * 16 + cl][1];
     }
     e(seg, c, s0, s1);
   }
@@ -137,7 +137,7 @@ static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hi
   hipLaunchKernelGGL((k_colred_part<F>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
                      C, p.rpc, scratch);
   PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL((k_colred_final<E>), dim3(cdiv(C, 64), nseg), dim3(256), 0, s, e, scratch,
+  hipLaunchKernelGGL((k_colred_final<E>), dim3(cdiv(C, 16), nseg), dim3(256), 0, s, e, scratch,
                      p.chunks, C);
   PHX_LAUNCH_CHECK();
 }
@@ -167,6 +167,8 @@ struct StatsEpi {
   long M;
   float* mean;
   float* rstd;
+  const float* gamma;
+  float* sc;
   float* mmean;
   float* mvar;
   float eps;
@@ -177,7 +179,9 @@ struct StatsEpi {
     if (var < 0.0) var = 0.0;
     const double mu = ref + dm;
     mean[c] = (float)mu;
-    rstd[c] = (float)(1.0 / sqrt(var + (double)eps));
+    const double rs = 1.0 / sqrt(var + (double)eps);
+    rstd[c] = (float)rs;
+    sc[c] = (float)(rs * (double)gamma[c]);
     if (mmean) {
       // Keras: moving -= (moving - batch) * (1 - momentum); the fused op reports the
       // Bessel-corrected variance for the moving average [TF-recall].
@@ -189,25 +193,29 @@ struct StatsEpi {
 };
 
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
-                     float* mmean, float* mvar, float eps, hipStream_t s) {
+                     const float* gamma, float* sc, float* mmean, float* mvar, float eps,
+                     hipStream_t s) {
   StatsAcc f{y, C, {0, 0, 0, 0}};
-  StatsEpi e{y, M, mean, rstd, mmean, mvar, eps};
+  StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps};
   colred(f, e, M, C, 1, part, s);
 }
 
 __global__ void k_bn_frozen_stats(const float* __restrict__ mm, const float* __restrict__ mv,
-                                  float* __restrict__ mean, float* __restrict__ rstd, int C,
+                                  float* __restrict__ mean, float* __restrict__ rstd,
+                                  const float* __restrict__ gamma, float* __restrict__ sc, int C,
                                   float eps) {
   int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   mean[c] = mm[c];
-  rstd[c] = (float)(1.0 / sqrt((double)mv[c] + (double)eps));
+  const double rs = 1.0 / sqrt((double)mv[c] + (double)eps);
+  rstd[c] = (float)rs;
+  sc[c] = (float)(rs * (double)gamma[c]);
 }
 
-void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd, int C,
-                            float eps, hipStream_t s) {
+void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd,
+                            const float* gamma, float* sc, int C, float eps, hipStream_t s) {
   hipLaunchKernelGGL(k_bn_frozen_stats, dim3(cdiv(C, 256)), dim3(256), 0, s, mmean, mvar, mean,
-                     rstd, C, eps);
+                     rstd, gamma, sc, C, eps);
   PHX_LAUNCH_CHECK();
 }
 
@@ -323,6 +331,36 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
   *op = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+struct BwdEpi2 {
+  long M;
+  float* mdz;
+  float* mdzx;
+  __device__ void operator()(int, int c, double s0, double s1) const {
+    mdz[c] = (float)(s0 / (double)M);
+    mdzx[c] = (float)(s1 / (double)M);
+  }
+};
+
+__global__ __launch_bounds__(256) void k_gx_materialize(GradX g, float4* __restrict__ out, long n4,
+                                                        int C) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  out[i] = gx_load4(g, i * 4, (int)((i * 4) % C));
+}
+
+void launch_bn_bwd_apply2(GradX g, float* out, long M, int C, hipStream_t s) {
+  long n4 = M * C / 4;
+  hipLaunchKernelGGL(k_gx_materialize, dim3(cdiv(n4, 256)), dim3(256), 0, s, g, (float4*)out, n4, C);
+  PHX_LAUNCH_CHECK();
+}
+
+void launch_bn_bwd_reduce(const float* da, const float* y, const float* mean, const float* rstd,
+                          const float* gamma, const float* beta, long M, int C, int act,
+                          double* part, float* mdz, float* mdzx, hipStream_t s) {
+  BwdAcc f{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}};
+  colred(f, BwdEpi2{M, mdz, mdzx}, M, C, 1, part, s);
+}
+
 void launch_bn_bwd(const float* da, const float* y, const float* mean, const float* rstd,
                    const float* gamma, const float* beta, float* dy, long M, int C, int act,
                    bool frozen, bool acc, double* part, float* coef, hipStream_t s) {
@@ -343,12 +381,16 @@ void launch_bn_bwd(const float* da, const float* y, const float* mean, const flo
 // ------------------------------------------------------------------------------------------
 // per-image channel sums: pool (sum x) and backward (sum dy*x) through the column reduction
 struct SumAcc {
-  const float* x;
+  InX x;
   const float* g;  // optional second factor
   int C;
-  __device__ void init(int, int, long) {}
+  Chan4 ck;
+  __device__ void init(int, int c4, long) {
+    if (x.mu) ck = inx_chan4(x, c4 * 4);
+  }
   __device__ void accum(long m, int c4, float* a0, float* a1) const {
-    float4 v = *reinterpret_cast<const float4*>(x + m * C + c4 * 4);
+    float4 v = *reinterpret_cast<const float4*>(x.p + m * C + c4 * 4);
+    if (x.mu) v = inx_apply4(x, ck, v);
     if (g) {
       float4 w = *reinterpret_cast<const float4*>(g + m * C + c4 * 4);
       v.x *= w.x; v.y *= w.y; v.z *= w.z; v.w *= w.w;
@@ -383,11 +425,17 @@ __global__ __launch_bounds__(256) void k_se_fc(const float* __restrict__ part, i
     pool[(long)b * C + c] = s;
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < Cse; j += blockDim.x) {
-    float h = b1[j];
-    for (int c = 0; c < C; ++c) h += sp[c] * w1[c * Cse + j];
-    hidden[(long)b * Cse + j] = h;  // pre-activation
-    sh[j] = act_fwd(h, act);
+  // hidden[j] = b1[j] + sum_c pool[c] * w1[c][j]: one wave per hidden unit, lanes over c
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int j = wv; j < Cse; j += nw) {
+    float h = 0.f;
+    for (int c = lane; c < C; c += 64) h += sp[c] * w1[c * Cse + j];
+    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
+    if (lane == 0) {
+      h += b1[j];
+      hidden[(long)b * Cse + j] = h;  // pre-activation
+      sh[j] = act_fwd(h, act);
+    }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -397,34 +445,18 @@ __global__ __launch_bounds__(256) void k_se_fc(const float* __restrict__ part, i
   }
 }
 
-__global__ __launch_bounds__(256) void k_chan_scale(const float* __restrict__ x,
-                                                    const float* __restrict__ scale,
-                                                    float* __restrict__ y, long n4, int HW, int C) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  long e = i * 4;
-  int c = (int)(e % C);
-  long b = e / ((long)HW * C);
-  float4 v = reinterpret_cast<const float4*>(x)[i];
-  const float* s = scale + b * C + c;
-  reinterpret_cast<float4*>(y)[i] = make_float4(v.x * s[0], v.y * s[1], v.z * s[2], v.w * s[3]);
-}
 
-void launch_se_fwd(const float* x, float* y, int B, int HW, int C, int Cse, const float* w1,
+void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
                    float* hidden, float* scale, hipStream_t s, double* scratch) {
   // per-image channel sums land after the pool vector: pool buffer = [B*C pool | B*C sums]
   float* sums = pool + (long)B * C;
-  colred(SumAcc{x, nullptr, C}, SumEpi{sums, C}, HW, C, B, scratch, s);
+  colred(SumAcc{x, nullptr, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
   size_t shm = (size_t)(C + Cse) * sizeof(float);
   hipLaunchKernelGGL(k_se_fc, dim3(B), dim3(256), shm, s, sums, 1, HW, C, Cse, w1, b1, w2, b2, act,
                      pool, hidden, scale);
   PHX_LAUNCH_CHECK();
-  if (y) {
-    long n4 = (long)B * HW * C / 4;
-    hipLaunchKernelGGL(k_chan_scale, dim3(cdiv(n4, 256)), dim3(256), 0, s, x, scale, y, n4, HW, C);
-    PHX_LAUNCH_CHECK();
-  }
+  (void)y;  // the excitation is folded into the consuming GEMM's A load (rowscale)
 }
 
 // backward FC chain, one block per image: gsum[c] = sum_hw dy*x  ->  dpool[c]
@@ -444,10 +476,12 @@ __global__ __launch_bounds__(256) void k_se_fc_bwd(const float* __restrict__ par
     de[c] = g * sv * (1.f - sv);
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < Cse; j += blockDim.x) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int j = wv; j < Cse; j += nw) {
     float a = 0.f;
-    for (int c = 0; c < C; ++c) a += de[c] * w2[j * C + c];
-    dh[j] = a * act_grad(hidden[(long)b * Cse + j], act);
+    for (int c = lane; c < C; c += 64) a += de[c] * w2[j * C + c];
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+    if (lane == 0) dh[j] = a * act_grad(hidden[(long)b * Cse + j], act);
   }
   __syncthreads();
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -481,13 +515,13 @@ __global__ __launch_bounds__(256) void k_se_bwd_apply(const float* __restrict__ 
   *op = o;
 }
 
-void launch_se_bwd(const float* dy, const float* x, float* dx, int B, int HW, int C, int Cse,
+void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
                    const float* w1, const float* b1, const float* w2, const float* b2, int act,
                    const float* pool, const float* hidden, const float* scale, float* gsum,
                    bool acc, hipStream_t s, double* scratch) {
   (void)b1; (void)b2; (void)pool;
   float* sums = gsum + (long)B * C;  // gsum: [B*C dpool | B*C sum_hw dy*x]
-  colred(SumAcc{x, dy, C}, SumEpi{sums, C}, HW, C, B, scratch, s);
+  colred(SumAcc{x, dy, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
   size_t shm = (size_t)(C + Cse) * sizeof(float);
   hipLaunchKernelGGL(k_se_fc_bwd, dim3(B), dim3(256), shm, s, sums, 1, C, Cse, w1, w2, act, hidden,
                      scale, gsum);
@@ -501,18 +535,17 @@ void launch_se_bwd(const float* dy, const float* x, float* dx, int B, int HW, in
 // ------------------------------------------------------------------------------------------
 // elementwise
 // ------------------------------------------------------------------------------------------
-__global__ void k_add(const float4* __restrict__ a, const float4* __restrict__ b,
-                      float4* __restrict__ y, long n4) {
+__global__ void k_add(InX a, InX b, float4* __restrict__ y, long n4, int C) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  float4 u = a[i], v = b[i];
+  const int c = (int)((i * 4) % C);
+  float4 u = inx_load4(a, i * 4, c), v = inx_load4(b, i * 4, c);
   y[i] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
 }
 
-void launch_add(const float* a, const float* b, float* y, long n, hipStream_t s) {
+void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s) {
   long n4 = n / 4;
-  hipLaunchKernelGGL(k_add, dim3(cdiv(n4, 256)), dim3(256), 0, s, (const float4*)a,
-                     (const float4*)b, (float4*)y, n4);
+  hipLaunchKernelGGL(k_add, dim3(cdiv(n4, 256)), dim3(256), 0, s, a, b, (float4*)y, n4, C);
   PHX_LAUNCH_CHECK();
 }
 
@@ -536,7 +569,7 @@ void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_
 }
 
 // max pool, TF SAME with -inf padding (efficientdet_keras.py:260-276)
-__global__ void k_maxpool_fwd(const float* __restrict__ x, float* __restrict__ y, int B, int H,
+__global__ void k_maxpool_fwd(InX x, float* __restrict__ y, int B, int H,
                               int W, int C, int Ho, int Wo, int k, int st, int pt, int pl) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)B * Ho * Wo * C;
@@ -554,14 +587,14 @@ __global__ void k_maxpool_fwd(const float* __restrict__ x, float* __restrict__ y
     for (int j = 0; j < k; ++j) {
       int ix = ox * st - pl + j;
       if (ix < 0 || ix >= W) continue;
-      m = fmaxf(m, x[(((long)b * H + iy) * W + ix) * C + c]);
+      m = fmaxf(m, inx_load1(x, (((long)b * H + iy) * W + ix) * C + c, c));
     }
   }
   y[idx] = m;
 }
 
 // gradient goes to the first maximum of each window in row-major scan order
-__global__ void k_maxpool_bwd(const float* __restrict__ x, const float* __restrict__ dy,
+__global__ void k_maxpool_bwd(InX x, const float* __restrict__ dy,
                               float* __restrict__ dx, int B, int H, int W, int C, int Ho, int Wo,
                               int k, int st, int pt, int pl, int acc_flag) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -592,7 +625,7 @@ __global__ void k_maxpool_bwd(const float* __restrict__ x, const float* __restri
         for (int j = 0; j < k; ++j) {
           int xx = x0 + j;
           if (xx < 0 || xx >= W) continue;
-          float v = x[(((long)b * H + yy) * W + xx) * C + c];
+          float v = inx_load1(x, (((long)b * H + yy) * W + xx) * C + c, c);
           if (v > m) { m = v; ay = yy; ax = xx; }
         }
       }
@@ -603,7 +636,7 @@ __global__ void k_maxpool_bwd(const float* __restrict__ x, const float* __restri
   dx[idx] = g;
 }
 
-void launch_maxpool_fwd(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+void launch_maxpool_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
                         int k, int stride, int pt, int pl, hipStream_t s) {
   long total = (long)B * Ho * Wo * C;
   hipLaunchKernelGGL(k_maxpool_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho,
@@ -611,7 +644,7 @@ void launch_maxpool_fwd(const float* x, float* y, int B, int H, int W, int C, in
   PHX_LAUNCH_CHECK();
 }
 
-void launch_maxpool_bwd(const float* x, const float* dy, float* dx, int B, int H, int W, int C,
+void launch_maxpool_bwd(InX x, const float* dy, float* dx, int B, int H, int W, int C,
                         int Ho, int Wo, int k, int stride, int pt, int pl, bool acc,
                         hipStream_t s) {
   long total = (long)B * H * W * C;
@@ -627,7 +660,7 @@ __device__ __forceinline__ int nn_src(int d, float scale, int in) {
   return s < in - 1 ? s : in - 1;
 }
 
-__global__ void k_upsample_fwd(const float* __restrict__ x, float* __restrict__ y, int B, int H,
+__global__ void k_upsample_fwd(InX x, float* __restrict__ y, int B, int H,
                                int W, int C, int Ho, int Wo) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)B * Ho * Wo * C;
@@ -640,7 +673,7 @@ __global__ void k_upsample_fwd(const float* __restrict__ x, float* __restrict__ 
   int b = (int)(t / Ho);
   int sy = nn_src(oy, (float)H / (float)Ho, H);
   int sx = nn_src(ox, (float)W / (float)Wo, W);
-  y[idx] = x[(((long)b * H + sy) * W + sx) * C + c];
+  y[idx] = inx_load1(x, (((long)b * H + sy) * W + sx) * C + c, c);
 }
 
 __global__ void k_upsample_bwd(const float* __restrict__ dy, float* __restrict__ dx, int B, int H,
@@ -671,7 +704,7 @@ __global__ void k_upsample_bwd(const float* __restrict__ dy, float* __restrict__
   dx[idx] = g;
 }
 
-void launch_upsample_fwd(const float* x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+void launch_upsample_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
                          hipStream_t s) {
   long total = (long)B * Ho * Wo * C;
   hipLaunchKernelGGL(k_upsample_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho,
@@ -691,7 +724,7 @@ void launch_upsample_bwd(const float* dy, float* dx, int B, int H, int W, int C,
 // OpAfterCombine activation (:214-216).  fastattn: n_i = x_i * relu(w_i) / (sum relu(w) + 1e-4),
 // summed in order (add_n, :31-39).
 struct FuseArgs {
-  const float* x[3];
+  InX x[3];
   float* dx[3];
   int acc[3];
 };
@@ -713,38 +746,44 @@ __device__ __forceinline__ void fuse_weights(const float* w0, const float* w1, c
 
 __global__ void k_fuse_fwd(FuseArgs fa, int nin, const float* __restrict__ w0,
                            const float* __restrict__ w1, const float* __restrict__ w2, int method,
-                           int act, float* __restrict__ y, long n) {
+                           int act, float* __restrict__ y, long n, int C) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float wv[3], den;
   fuse_weights(w0, w1, w2, nin, method, wv, &den);
+  const int c = (int)(i % C);
+  const float x0 = inx_load1(fa.x[0], i, c), x1 = inx_load1(fa.x[1], i, c);
+  const float x2 = nin > 2 ? inx_load1(fa.x[2], i, c) : 0.f;
   float v;
   if (method == 0) {
-    v = fa.x[0][i] * wv[0] / den;
-    v = v + fa.x[1][i] * wv[1] / den;
-    if (nin > 2) v = v + fa.x[2][i] * wv[2] / den;
+    v = x0 * wv[0] / den;
+    v = v + x1 * wv[1] / den;
+    if (nin > 2) v = v + x2 * wv[2] / den;
   } else {
-    v = fa.x[0][i] + fa.x[1][i];
-    if (nin > 2) v = v + fa.x[2][i];
+    v = x0 + x1;
+    if (nin > 2) v = v + x2;
   }
   y[i] = act_fwd(v, act);
 }
 
 __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
                            const float* __restrict__ w1, const float* __restrict__ w2, int method,
-                           int act, const float* __restrict__ dy, long n) {
+                           int act, const float* __restrict__ dy, long n, int C) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float wv[3], den;
   fuse_weights(w0, w1, w2, nin, method, wv, &den);
+  const int c = (int)(i % C);
+  const float x0 = inx_load1(fa.x[0], i, c), x1 = inx_load1(fa.x[1], i, c);
+  const float x2 = nin > 2 ? inx_load1(fa.x[2], i, c) : 0.f;
   float v;
   if (method == 0) {
-    v = fa.x[0][i] * wv[0] / den;
-    v = v + fa.x[1][i] * wv[1] / den;
-    if (nin > 2) v = v + fa.x[2][i] * wv[2] / den;
+    v = x0 * wv[0] / den;
+    v = v + x1 * wv[1] / den;
+    if (nin > 2) v = v + x2 * wv[2] / den;
   } else {
-    v = fa.x[0][i] + fa.x[1][i];
-    if (nin > 2) v = v + fa.x[2][i];
+    v = x0 + x1;
+    if (nin > 2) v = v + x2;
   }
   float dv = dy[i] * act_grad(v, act);
   for (int k = 0; k < nin; ++k) {
@@ -755,18 +794,19 @@ __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
   }
 }
 
-void launch_fuse_fwd(const float* const* xs, int nin, const float* wsm0, const float* wsm1,
-                     const float* wsm2, int method, int act, float* y, long n, hipStream_t s) {
+void launch_fuse_fwd(const InX* xs, int nin, const float* wsm0, const float* wsm1,
+                     const float* wsm2, int method, int act, float* y, long n, int C,
+                     hipStream_t s) {
   FuseArgs fa{};
   for (int i = 0; i < nin; ++i) fa.x[i] = xs[i];
   hipLaunchKernelGGL(k_fuse_fwd, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
-                     method, act, y, n);
+                     method, act, y, n, C);
   PHX_LAUNCH_CHECK();
 }
 
-void launch_fuse_bwd(const float* const* xs, int nin, const float* wsm0, const float* wsm1,
+void launch_fuse_bwd(const InX* xs, int nin, const float* wsm0, const float* wsm1,
                      const float* wsm2, int method, int act, const float* dy, float* const* dxs,
-                     const bool* acc, long n, hipStream_t s) {
+                     const bool* acc, long n, int C, hipStream_t s) {
   FuseArgs fa{};
   for (int i = 0; i < nin; ++i) {
     fa.x[i] = xs[i];
@@ -774,7 +814,7 @@ void launch_fuse_bwd(const float* const* xs, int nin, const float* wsm0, const f
     fa.acc[i] = acc[i] ? 1 : 0;
   }
   hipLaunchKernelGGL(k_fuse_bwd, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
-                     method, act, dy, n);
+                     method, act, dy, n, C);
   PHX_LAUNCH_CHECK();
 }
 
