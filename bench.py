@@ -103,6 +103,7 @@ def main():
     victim = EfficientDetVictim("efficientdet-d0", "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
                                 device=local)
     att = PatchAttacker(victim, seed=7, device=dev)
+    ws_gb = victim.ctx.workspace_bytes(B) / 1e9
     gidx = list(range(rank * B, (rank + 1) * B))
     images = torch.as_tensor(synth_images(gidx, S), device=dev)
     boxes = synth_boxes(gidx, S)
@@ -168,6 +169,7 @@ def main():
             "data": "synthetic (U(-1,1) images, 1-3 injected person boxes/image, synthetic D0 weights)",
             "config": {"workload": f"C{2 if world == 1 else 3}: EfficientDet-D0 patch attack {S}x{S}, "
                                    f"{B} images/GPU, bn=local", "global_batch": world * B, "image_size": S,
+                       "workspace_gb_per_gpu": round(ws_gb, 3),
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "step_roofline": step_roof,

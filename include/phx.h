@@ -101,6 +101,10 @@ int phx_detect(phx_ctx* ctx, const float* images, int B, float* scores, int32_t*
                float* boxes, void* stream);
 int phx_num_anchors(const phx_ctx* ctx);
 int phx_image_size(const phx_ctx* ctx);
+/* Device bytes of the executor for batch B (activations, gradients, statistics, EOT and
+ * post-processing buffers); builds (allocates) it if it does not exist yet.  SURVEY §8b's
+ * phx_workspace_bytes; the library owns the workspace, no step allocates. */
+int phx_workspace_bytes(phx_ctx* ctx, int B, size_t* bytes);
 
 /* PatchAttacker.first_pass (attacker.py:91-116): detect + person/valid/threshold filter +
  * gaussian soft-NMS (postprocess.nms, postprocess.py:159-205 → NonMaxSuppressionV5) +

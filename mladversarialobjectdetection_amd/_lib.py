@@ -55,6 +55,7 @@ _SIGS = [
     ("phx_read_weights", c_int, [c_void_p, c_void_p, c_size_t]),
     ("phx_detect", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_num_anchors", c_int, [c_void_p]),
+    ("phx_workspace_bytes", c_int, [c_void_p, c_int, POINTER(c_size_t)]),
     ("phx_image_size", c_int, [c_void_p]),
     ("phx_first_pass", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_soft_nms", c_int,
@@ -151,6 +152,12 @@ class Context:
         buf = ctypes.create_string_buffer(need.value)
         check(self.h, self.lib.phx_profile_report(self.h, buf, need.value, ctypes.byref(need)), "phx_profile_report")
         return json.loads(buf.value.decode())
+
+    def workspace_bytes(self, batch: int) -> int:
+        """Device bytes of the executor for `batch` images (builds it if needed)."""
+        n = c_size_t(0)
+        self.call("phx_workspace_bytes", int(batch), ctypes.byref(n))
+        return int(n.value)
 
     def call(self, name: str, *args):
         rc = getattr(self.lib, name)(self.h, *args)

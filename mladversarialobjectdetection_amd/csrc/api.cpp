@@ -88,10 +88,12 @@ struct Exec {
   float* patched = nullptr;
   int16_t* owner = nullptr;
 
+  size_t bytes = 0;  // device bytes owned by this executor
   template <typename T>
   T* alloc(size_t n) {
     T* p = dalloc<T>(n);
     owned.emplace_back(p);
+    bytes += n * sizeof(T);
     return p;
   }
   float* tptr(int t, const float* input) const {
@@ -709,6 +711,16 @@ int phx_weight_manifest(const phx_ctx* ctx, char* buf, size_t cap, size_t* neede
 size_t phx_weight_count(const phx_ctx* ctx) { return ctx ? ctx->wfloats : 0; }
 int phx_num_anchors(const phx_ctx* ctx) { return ctx ? ctx->A : 0; }
 int phx_image_size(const phx_ctx* ctx) { return ctx ? ctx->mc.image_size : 0; }
+
+int phx_workspace_bytes(phx_ctx* ctx, int B, size_t* bytes) {
+  if (!ctx || !bytes || B <= 0) return PHX_EINVAL;
+  if (B > ctx->max_batch) return fail(ctx, PHX_ECAP, "batch exceeds max_batch");
+  PHX_TRY(ctx)
+  PHX_HIP(hipSetDevice(ctx->device));
+  *bytes = ctx->exec_for(B).bytes;
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
 
 int phx_load_weights(phx_ctx* ctx, const float* blob, size_t nfloats) {
   if (!ctx || !blob) return PHX_EINVAL;

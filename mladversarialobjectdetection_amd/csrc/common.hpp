@@ -30,7 +30,11 @@ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 // activations (utils.py:36-53).  swish = x*sigmoid(x) (tf.nn.swish); relu6 grad passes on
 // the open interval (0,6) (TF Relu6Grad).
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_exp_f32 + v_rcp_f32 (1 ulp each): the IEEE divide sequence would cost ~10 instructions per
+// element in every BN-view load
+__device__ __forceinline__ float sigmoidf_(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+}
 
 __device__ __forceinline__ float act_fwd(float z, int act) {
   if (act == 1) return z * sigmoidf_(z);

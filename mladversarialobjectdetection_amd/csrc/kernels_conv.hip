@@ -411,210 +411,6 @@ void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, 
     gemm_run(0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial);
 }
 
-// ------------------------------------------------------------------------------------------
-// depthwise conv (TF SAME), one lane per (output pixel, 4 channels)
-// ------------------------------------------------------------------------------------------
-
-
-// ------------------------------------------------------------------------------------------
-// LDS-tiled depthwise conv.  A workgroup owns OTH x OTW output pixels x (4*CG) channels: it
-// stages the input tile (+halo) once into LDS with the consumer-side BN + activation applied
-// once per element (not once per tap), then every lane produces OTH outputs of one column for
-// 4 channels.  LDS image [row][col][cg] of float4: a wave's reads are contiguous 16-B slots.
-// ------------------------------------------------------------------------------------------
-struct DwTile {
-  int cg, px, oth, otw, rin, cin;
-};
-
-static DwTile dw_tile(int C, int k, int stride) {
-  DwTile t;
-  const int c4 = C / 4;
-  t.cg = (c4 % 8 == 0) ? 8 : (c4 % 4 == 0) ? 4 : (c4 % 2 == 0) ? 2 : 1;
-  t.px = 256 / t.cg;
-  t.otw = t.px;
-  t.oth = stride == 1 ? 4 : 2;
-  t.rin = (t.oth - 1) * stride + k;
-  t.cin = (t.otw - 1) * stride + k;
-  return t;
-}
-
-// XCD-aware block order: the NCG channel-group blocks of one pixel tile get linear ids
-// L, L+8, L+16, ... (the same XCD under round-robin dispatch, back to back), so the NHWC lines
-// each of them reads 16*CG bytes of are served from that XCD's L2 for the others.
-__device__ __forceinline__ void dw_block_map(int L, int ncg, int* tile, int* cg) {
-  const int grp = L / (8 * ncg), rem = L % (8 * ncg);
-  *cg = rem / 8;
-  *tile = grp * 8 + rem % 8;
-}
-
-__global__ __launch_bounds__(256) void k_dw_fwd_tiled(InX xv, const float* __restrict__ w,
-                                                      float* __restrict__ y, int H, int W, int C,
-                                                      int Ho, int Wo, int k, int stride, int pt,
-                                                      int pl, DwTile T, int tiles_x, int ntiles,
-                                                      int ncg) {
-  extern __shared__ float4 tile[];
-  const int b = blockIdx.z;
-  int tl, cgi;
-  dw_block_map(blockIdx.x, ncg, &tl, &cgi);
-  if (tl >= ntiles) return;
-  const int ty = tl / tiles_x, tx = tl % tiles_x;
-  const int oy0 = ty * T.oth, ox0 = tx * T.otw;
-  const int iy0 = oy0 * stride - pt, ix0 = ox0 * stride - pl;
-  const bool xf = xv.mu != nullptr;
-  const int n = T.rin * T.cin * T.cg;
-  const int cg = threadIdx.x % T.cg, px = threadIdx.x / T.cg;
-  const int ox = ox0 + px;
-  {
-    const int c0 = cgi * T.cg * 4;
-    for (int e = threadIdx.x; e < n; e += 256) {
-      const int ecg = e % T.cg;
-      const int pcol = (e / T.cg) % T.cin;
-      const int prow = e / (T.cg * T.cin);
-      const int iy = iy0 + prow, ix = ix0 + pcol;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        const int c = c0 + ecg * 4;
-        v = *reinterpret_cast<const float4*>(xv.p + (((long)b * H + iy) * W + ix) * C + c);
-        if (xf) v = inx_apply4(xv, inx_chan4(xv, c), v);
-      }
-      tile[e] = v;
-    }
-    __syncthreads();
-    if (ox < Wo) {
-      const int c = c0 + cg * 4;
-      float4 acc[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int i = 0; i < k; ++i) {
-        for (int j = 0; j < k; ++j) {
-          const float4 wv = *reinterpret_cast<const float4*>(w + (i * k + j) * C + c);
-          const int pcol = px * stride + j;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (r < T.oth) {
-              const float4 xv4 = tile[((r * stride + i) * T.cin + pcol) * T.cg + cg];
-              acc[r].x += xv4.x * wv.x;
-              acc[r].y += xv4.y * wv.y;
-              acc[r].z += xv4.z * wv.z;
-              acc[r].w += xv4.w * wv.w;
-            }
-          }
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int oy = oy0 + r;
-        if (r < T.oth && oy < Ho)
-          *reinterpret_cast<float4*>(y + (((long)b * Ho + oy) * Wo + ox) * C + c) = acc[r];
-      }
-    }
-    __syncthreads();
-  }
-}
-
-void launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho, int Wo,
-                   int k, int stride, int pt, int pl, hipStream_t s) {
-  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
-  DwTile T = dw_tile(C, k, stride);
-  const int tiles_x = cdiv(Wo, T.otw), tiles_y = cdiv(Ho, T.oth);
-  const int ntiles = tiles_x * tiles_y, ncg = C / (4 * T.cg);
-  size_t shm = (size_t)T.rin * T.cin * T.cg * sizeof(float4);
-  dim3 g(cdiv(ntiles, 8) * 8 * ncg, 1, B);
-  hipLaunchKernelGGL(k_dw_fwd_tiled, g, dim3(256), shm, s, x, w, y, H, W, C, Ho, Wo, k, stride, pt, pl,
-                     T, tiles_x, ntiles, ncg);
-  PHX_LAUNCH_CHECK();
-}
-
-// dgrad of the depthwise conv, gathered per input pixel: the workgroup stages the dy window its
-// OTH x OTW input pixels need (gradient view applied once per element) and sums the taps.
-static inline int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
-__device__ __forceinline__ int floor_div_d(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
-
-__global__ __launch_bounds__(256) void k_dw_bwd_tiled(GradX g, const float* __restrict__ w,
-                                                      float* __restrict__ dx, int H, int W, int C,
-                                                      int Ho, int Wo, int k, int stride, int pt,
-                                                      int pl, DwTile T, int rin, int cin,
-                                                      int tiles_x, int ntiles, int ncg,
-                                                      int acc_flag) {
-  extern __shared__ float4 tile[];
-  const int b = blockIdx.z;
-  int tl, cgi;
-  dw_block_map(blockIdx.x, ncg, &tl, &cgi);
-  if (tl >= ntiles) return;
-  const int ty = tl / tiles_x, tx = tl % tiles_x;
-  const int iy0 = ty * T.oth, ix0 = tx * T.otw;  // this tile's input-space pixels
-  const int oy_lo = floor_div_d(iy0 + pt - (k - 1), stride);
-  const int ox_lo = floor_div_d(ix0 + pl - (k - 1), stride);
-  const int n = rin * cin * T.cg;
-  const int cg = threadIdx.x % T.cg, px = threadIdx.x / T.cg;
-  const int ix = ix0 + px;
-  {
-    const int c0 = cgi * T.cg * 4;
-    for (int e = threadIdx.x; e < n; e += 256) {
-      const int ecg = e % T.cg;
-      const int pcol = (e / T.cg) % cin;
-      const int prow = e / (T.cg * cin);
-      const int oy = oy_lo + prow, ox = ox_lo + pcol;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo)
-        v = gx_load4(g, (((long)b * Ho + oy) * Wo + ox) * C + c0 + ecg * 4, c0 + ecg * 4);
-      tile[e] = v;
-    }
-    __syncthreads();
-    if (ix < W) {
-      const int c = c0 + cg * 4;
-      for (int r = 0; r < T.oth; ++r) {
-        const int iy = iy0 + r;
-        if (iy >= H) break;
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int i = 0; i < k; ++i) {
-          const int tyy = iy + pt - i;
-          if (tyy < 0) break;
-          if (tyy % stride) continue;
-          const int oy = tyy / stride;
-          if (oy >= Ho) continue;
-          for (int j = 0; j < k; ++j) {
-            const int txx = ix + pl - j;
-            if (txx < 0) break;
-            if (txx % stride) continue;
-            const int ox = txx / stride;
-            if (ox >= Wo) continue;
-            const float4 gv = tile[((oy - oy_lo) * cin + (ox - ox_lo)) * T.cg + cg];
-            const float4 wv = *reinterpret_cast<const float4*>(w + (i * k + j) * C + c);
-            acc.x += gv.x * wv.x;
-            acc.y += gv.y * wv.y;
-            acc.z += gv.z * wv.z;
-            acc.w += gv.w * wv.w;
-          }
-        }
-        float4* o = reinterpret_cast<float4*>(dx + (((long)b * H + iy) * W + ix) * C + c);
-        if (acc_flag) {
-          float4 pv = *o;
-          acc.x += pv.x; acc.y += pv.y; acc.z += pv.z; acc.w += pv.w;
-        }
-        *o = acc;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-void launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
-                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s) {
-  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
-  DwTile T = dw_tile(C, k, stride);
-  T.oth = 4;
-  const int rin = (T.oth - 1 + k - 1) / stride + 2;
-  const int cin = (T.otw - 1 + k - 1) / stride + 2;
-  const int tiles_x = cdiv(W, T.otw), tiles_y = cdiv(H, T.oth);
-  const int ntiles = tiles_x * tiles_y, ncg = C / (4 * T.cg);
-  size_t shm = (size_t)rin * cin * T.cg * sizeof(float4);
-  dim3 g(cdiv(ntiles, 8) * 8 * ncg, 1, B);
-  hipLaunchKernelGGL(k_dw_bwd_tiled, g, dim3(256), shm, s, dy, w, dx, H, W, C, Ho, Wo, k, stride, pt, pl,
-                     T, rin, cin, tiles_x, ntiles, ncg, acc ? 1 : 0);
-  PHX_LAUNCH_CHECK();
-}
-
 __global__ void k_transpose(const float* __restrict__ in, float* __restrict__ out, int rows,
                             int cols) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;

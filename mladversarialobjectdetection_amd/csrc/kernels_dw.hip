@@ -1,0 +1,386 @@
+// kernels_dw.hip — depthwise k x k convolution (TF SAME) forward and data-gradient for gfx950.
+//
+// Reference: DepthwiseConv2D in MBConvBlock (efficientnet_model.py:224-417), the separable convs of
+// BiFPN (efficientdet_keras.py:201-221) and of the class/box heads (efficientdet_keras.py:414-471);
+// TF SAME padding.
+//
+// Design.  Depthwise conv is HBM-bound (k*k MACs per 8 bytes moved), so each workgroup owns one
+// spatial tile x one slice of 4*CG channels and:
+//   * stages the input window (tile + halo) into LDS exactly once, applying the producer BN +
+//     activation (InX) or the consumer-side BN backward (GradX) once per element, with the
+//     per-channel parameters hoisted into registers (a lane's channel group never changes);
+//   * issues the staging loads four at a time before any use, so one block keeps 4 x 256
+//     16-byte loads in flight instead of a dependent chain;
+//   * keeps the k*k filter taps of its 4 channels in registers and walks RPT output rows per
+//     lane with a sliding window over the staged rows (each LDS float4 is read once per lane
+//     and feeds every output row that uses it);
+//   * sizes the tile to the image: OTW = min(256/CG, Wout) columns and the remaining lanes take
+//     further row groups, so the 4x4..16x16 BiFPN / head levels do not idle 3/4 of the block.
+// Block order is XCD-aware: the NCG channel slices of one spatial tile are dispatched
+// back-to-back on the same XCD, so the NHWC lines they each read a 16*CG-byte piece of are L2 hits
+// for the others.
+#include <stdexcept>
+
+#include "kernels.hpp"
+
+namespace phx {
+
+struct DwGeom {
+  int H, W, C;      // conv input  (fwd: x; bwd: dx)
+  int Ho, Wo;       // conv output (fwd: y; bwd: dy)
+  int pt, pl;
+  int lcg;          // log2(CG)
+  int otw, oth;     // tile (in the space of the tensor this launch writes)
+  int nrg;          // row groups per block
+  int rin, cin;     // staged window
+  int tiles_x, ntiles, ncg;
+  int per;          // work items per XCD
+};
+
+// XCD-aware work split: the ntiles*ncg (tile, channel slice) items, tile-major, are cut into
+// 8 contiguous ranges of `per` items, one per XCD (dispatch is round-robin: block L -> XCD L%8),
+// so the ncg slices of a tile run back to back on one XCD and share its L2, and every XCD gets
+// work even when a level has fewer than 8 tiles.  Returns false for the padding blocks.
+__device__ __forceinline__ bool dw_block_map(int L, int per, int ncg, int nwork, int* tile,
+                                             int* cg) {
+  const int w = (L & 7) * per + (L >> 3);
+  if ((L >> 3) >= per || w >= nwork) return false;
+  *tile = w / ncg;
+  *cg = w - *tile * ncg;
+  return true;
+}
+
+// ---- staging sources ---------------------------------------------------------------------
+struct StageInX {
+  using Raw = float4;
+  InX v;
+  Chan4 k;
+  bool f;
+  __device__ __forceinline__ void init(const InX& x, int c) {
+    v = x;
+    f = x.mu != nullptr;
+    if (f) k = inx_chan4(x, c);
+  }
+  __device__ __forceinline__ Raw zero() const { return make_float4(0.f, 0.f, 0.f, 0.f); }
+  __device__ __forceinline__ Raw load(long e) const {
+    return *reinterpret_cast<const float4*>(v.p + e);
+  }
+  __device__ __forceinline__ float4 finish(const Raw& x) const {
+    return f ? inx_apply4(v, k, x) : x;
+  }
+};
+
+struct StageGradX {
+  struct Raw {
+    float4 d, y;
+  };
+  GradX g;
+  GChan4 k;
+  __device__ __forceinline__ void init(const GradX& x, int c) {
+    g = x;
+    if (g.y) k = gx_chan4(g, c);
+  }
+  __device__ __forceinline__ Raw zero() const {
+    return Raw{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+  }
+  __device__ __forceinline__ Raw load(long e) const {
+    Raw r;
+    r.d = *reinterpret_cast<const float4*>(g.da + e);
+    if (g.y) r.y = *reinterpret_cast<const float4*>(g.y + e);
+    return r;
+  }
+  __device__ __forceinline__ float4 finish(const Raw& r) const {
+    return g.y ? gx_apply4(g, k, r.d, r.y) : r.d;
+  }
+};
+
+__device__ __forceinline__ void fma4(float4& a, const float4& x, const float4& w) {
+  a.x = fmaf(x.x, w.x, a.x);
+  a.y = fmaf(x.y, w.y, a.y);
+  a.z = fmaf(x.z, w.z, a.z);
+  a.w = fmaf(x.w, w.w, a.w);
+}
+
+// filter taps: K=3 kernels hold their 9 taps in registers; K=5 kernels read the 25 taps of
+// their 4 channels from LDS (all lanes of one channel group hit the same address, so the read
+// is a broadcast) — 100 VGPRs of taps would halve occupancy.
+template <int K>
+struct Taps {
+  static constexpr bool kLds = false;
+  float4 r[kLds ? 1 : K * K];
+  const float4* l;
+  int cg, CG;
+  __device__ __forceinline__ void stage(float4* wt, const float* w, int C, int cgi, int lcg) {
+    if constexpr (kLds) {
+      const int n = (K * K) << lcg;
+      for (int e = threadIdx.x; e < n; e += 256) {
+        const int t = e >> lcg, k = e & ((1 << lcg) - 1);
+        wt[e] = *reinterpret_cast<const float4*>(w + (long)t * C + (((cgi << lcg) + k) << 2));
+      }
+    }
+  }
+  __device__ __forceinline__ void init(const float4* wt, const float* w, int C, int c, int cg_,
+                                       int lcg) {
+    cg = cg_;
+    CG = 1 << lcg;
+    l = wt;
+    if constexpr (!kLds) {
+#pragma unroll
+      for (int t = 0; t < K * K; ++t) r[t] = *reinterpret_cast<const float4*>(w + (long)t * C + c);
+    }
+  }
+  __device__ __forceinline__ float4 operator()(int t) const {
+    if constexpr (kLds) return l[t * CG + cg];
+    else return r[t];
+  }
+};
+
+// stage rows [r0, r0+rin) x cols [c0, c0+cin) of the NHWC source (sh x sw) into LDS
+template <class Src>
+__device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, int sh, int sw, int C,
+                                         int r0, int c0, int chan, const DwGeom& g) {
+  const int CG = 1 << g.lcg;
+  const int npx = g.rin * g.cin;
+  const int pstep = 256 >> g.lcg;
+  const int ecg = threadIdx.x & (CG - 1);
+  int p = threadIdx.x >> g.lcg;
+  for (; p < npx; p += 4 * pstep) {
+    typename Src::Raw v[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int pp = p + u * pstep;
+      const int prow = pp / g.cin, pcol = pp - prow * g.cin;
+      const int iy = r0 + prow, ix = c0 + pcol;
+      ok[u] = pp < npx && iy >= 0 && iy < sh && ix >= 0 && ix < sw;
+      v[u] = ok[u] ? src.load((((long)b * sh + iy) * sw + ix) * C + chan) : src.zero();
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int pp = p + u * pstep;
+      if (pp < npx) tile[(pp << g.lcg) + ecg] = ok[u] ? src.finish(v[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+// ---- forward: y[oy][ox] = sum_ij a[oy*S - pt + i][ox*S - pl + j] * w[i][j] ----------------
+template <int K, int S, int RPT>
+__global__ __launch_bounds__(256) void k_dw_fwd(InX xv, const float* __restrict__ w,
+                                                float* __restrict__ y, DwGeom g) {
+  extern __shared__ float4 tile[];
+  const int b = blockIdx.z;
+  int tl, cgi;
+  if (!dw_block_map(blockIdx.x, g.per, g.ncg, g.ntiles * g.ncg, &tl, &cgi)) return;
+  const int CG = 1 << g.lcg;
+  const int ty = tl / g.tiles_x, tx = tl - ty * g.tiles_x;
+  const int oy0 = ty * g.oth, ox0 = tx * g.otw;
+  const int cg = threadIdx.x & (CG - 1), q = threadIdx.x >> g.lcg;
+  const int col = q % g.otw, rg = q / g.otw;
+  const int c = (cgi * CG + cg) * 4;
+
+  StageInX src;
+  src.init(xv, c);
+  float4* wt = tile + g.rin * g.cin * CG;
+  Taps<K> wr;
+  wr.stage(wt, w, g.C, cgi, g.lcg);
+  dw_stage(tile, src, b, g.H, g.W, g.C, oy0 * S - g.pt, ox0 * S - g.pl, c, g);
+  __syncthreads();
+
+  const int ox = ox0 + col;
+  const int row0 = rg * RPT;  // first local output row of this lane
+  if (rg >= g.nrg || ox >= g.Wo || oy0 + row0 >= g.Ho) return;
+  wr.init(wt, w, g.C, c, cg, g.lcg);
+  float4 acc[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int NR = (RPT - 1) * S + K;
+  const float4* base = tile + ((row0 * S) * g.cin + col * S) * CG + cg;
+#pragma unroll
+  for (int ir = 0; ir < NR; ++ir) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const float4 v = base[(ir * g.cin + j) * CG];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) {
+        const int i = ir - r * S;
+        if (i >= 0 && i < K) fma4(acc[r], v, wr(i * K + j));
+      }
+    }
+    if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);  // stream rows: bound live VGPRs
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int oy = oy0 + row0 + r;
+    if (oy < g.Ho) *reinterpret_cast<float4*>(y + (((long)b * g.Ho + oy) * g.Wo + ox) * g.C + c) = acc[r];
+  }
+}
+
+// ---- data gradient: dx[iy][ix] = sum over (i,j) with (iy+pt-i) and (ix+pl-j) divisible by S of
+//      dy[(iy+pt-i)/S][(ix+pl-j)/S] * w[i][j]  (the adjoint of the forward above) ---------------
+template <int K, int S, int RPT>
+__global__ __launch_bounds__(256) void k_dw_bwd(GradX gv, const float* __restrict__ w,
+                                                float* __restrict__ dx, DwGeom g, int acc_flag) {
+  extern __shared__ float4 tile[];
+  const int b = blockIdx.z;
+  int tl, cgi;
+  if (!dw_block_map(blockIdx.x, g.per, g.ncg, g.ntiles * g.ncg, &tl, &cgi)) return;
+  const int CG = 1 << g.lcg;
+  const int ty = tl / g.tiles_x, tx = tl - ty * g.tiles_x;
+  const int iy0 = ty * g.oth, ix0 = tx * g.otw;  // input-space tile origin
+  const int cg = threadIdx.x & (CG - 1), q = threadIdx.x >> g.lcg;
+  const int col = q % g.otw, rg = q / g.otw;
+  const int c = (cgi * CG + cg) * 4;
+  // dy window origin: floor((iy0 + pt - (K-1)) / S)
+  const int ay = iy0 + g.pt - (K - 1), ax = ix0 + g.pl - (K - 1);
+  const int oy_lo = S == 1 ? ay : (ay >= 0 ? ay / S : -((-ay + S - 1) / S));
+  const int ox_lo = S == 1 ? ax : (ax >= 0 ? ax / S : -((-ax + S - 1) / S));
+
+  StageGradX src;
+  src.init(gv, c);
+  float4* wt = tile + g.rin * g.cin * CG;
+  Taps<K> wr;
+  wr.stage(wt, w, g.C, cgi, g.lcg);
+  dw_stage(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
+  __syncthreads();
+
+  const int ix = ix0 + col;
+  const int row0 = rg * RPT;
+  if (rg >= g.nrg || ix >= g.W || iy0 + row0 >= g.H) return;
+  wr.init(wt, w, g.C, c, cg, g.lcg);
+  float4 acc[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if constexpr (S == 1) {
+    // local dy row of (output row r, tap i) = row0 + r + (K-1-i): a sliding window as forward
+    constexpr int NR = RPT + K - 1;
+    const float4* base = tile + (row0 * g.cin + col) * CG + cg;
+#pragma unroll
+    for (int ir = 0; ir < NR; ++ir) {
+#pragma unroll
+      for (int jj = 0; jj < K; ++jj) {
+        const float4 v = base[(ir * g.cin + jj) * CG];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+          const int ii = ir - r;  // = K-1-i
+          if (ii >= 0 && ii < K) fma4(acc[r], v, wr((K - 1 - ii) * K + (K - 1 - jj)));
+        }
+      }
+      if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    const int u0 = ix + g.pl;  // column parity decides which taps land on a dy sample
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const int t0 = iy0 + row0 + r + g.pt;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const int t = t0 - i;
+        if (t & 1) continue;
+        const int lr = (t >> 1) - oy_lo;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+          const int u = u0 - j;
+          if (u & 1) continue;
+          const int lc = (u >> 1) - ox_lo;
+          fma4(acc[r], tile[(lr * g.cin + lc) * CG + cg], wr(i * K + j));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int iy = iy0 + row0 + r;
+    if (iy >= g.H) continue;
+    float4* o = reinterpret_cast<float4*>(dx + (((long)b * g.H + iy) * g.W + ix) * g.C + c);
+    float4 a = acc[r];
+    if (acc_flag) {
+      const float4 p = *o;
+      a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+    }
+    *o = a;
+  }
+}
+
+// ---- host planning -------------------------------------------------------------------------
+static int dw_lcg(int C) {
+  const int c4 = C / 4;
+  return (c4 % 8 == 0) ? 3 : (c4 % 4 == 0) ? 2 : (c4 % 2 == 0) ? 1 : 0;
+}
+
+// tile over an output space of (oh x ow) written by this launch
+static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k, int s, int rpt,
+                      bool bwd) {
+  DwGeom g{};
+  g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo; g.pt = pt; g.pl = pl;
+  g.lcg = dw_lcg(C);
+  const int px = 256 >> g.lcg;
+  const int oh = bwd ? H : Ho, ow = bwd ? W : Wo;
+  g.otw = ow < px ? ow : px;
+  g.nrg = px / g.otw;
+  const int need = (oh + rpt - 1) / rpt;  // row groups that cover the whole image
+  if (g.nrg > need) g.nrg = need;
+  g.oth = g.nrg * rpt;
+  if (!bwd) {
+    g.rin = (g.oth - 1) * s + k;
+    g.cin = (g.otw - 1) * s + k;
+  } else {
+    g.rin = (g.oth - 1 + k - 1) / s + 2;
+    g.cin = (g.otw - 1 + k - 1) / s + 2;
+    if (s == 1) {
+      g.rin = g.oth + k - 1;
+      g.cin = g.otw + k - 1;
+    }
+  }
+  g.tiles_x = cdiv(ow, g.otw);
+  g.ntiles = g.tiles_x * cdiv(oh, g.oth);
+  g.ncg = C / (4 << g.lcg);
+  g.per = cdiv((long)g.ntiles * g.ncg, 8);
+  return g;
+}
+
+static size_t dw_lds(const DwGeom& g, int k) {
+  return ((size_t)g.rin * g.cin + (k > 3 ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
+}
+
+template <int K, int S>
+static void dw_fwd_go(InX x, const float* w, float* y, int B, const DwGeom& g, hipStream_t s) {
+  constexpr int RPT = S == 1 ? 4 : 2;
+  dim3 grid(8 * g.per, 1, B);
+  hipLaunchKernelGGL((k_dw_fwd<K, S, RPT>), grid, dim3(256), dw_lds(g, K), s, x, w, y, g);
+}
+
+void launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho, int Wo,
+                   int k, int stride, int pt, int pl, hipStream_t s) {
+  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
+  const int rpt = stride == 1 ? 4 : 2;
+  DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false);
+  if (dw_lds(g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
+  if (k == 3 && stride == 1) dw_fwd_go<3, 1>(x, w, y, B, g, s);
+  else if (k == 3 && stride == 2) dw_fwd_go<3, 2>(x, w, y, B, g, s);
+  else if (k == 5 && stride == 1) dw_fwd_go<5, 1>(x, w, y, B, g, s);
+  else if (k == 5 && stride == 2) dw_fwd_go<5, 2>(x, w, y, B, g, s);
+  else throw std::invalid_argument("dw: unsupported kernel/stride");
+  PHX_LAUNCH_CHECK();
+}
+
+template <int K, int S>
+static void dw_bwd_go(GradX dy, const float* w, float* dx, int B, const DwGeom& g, bool acc,
+                      hipStream_t s) {
+  dim3 grid(8 * g.per, 1, B);
+  hipLaunchKernelGGL((k_dw_bwd<K, S, 4>), grid, dim3(256), dw_lds(g, K), s, dy, w, dx, g, acc ? 1 : 0);
+}
+
+void launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
+                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s) {
+  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
+  DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, true);
+  if (dw_lds(g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
+  if (k == 3 && stride == 1) dw_bwd_go<3, 1>(dy, w, dx, B, g, acc, s);
+  else if (k == 3 && stride == 2) dw_bwd_go<3, 2>(dy, w, dx, B, g, acc, s);
+  else if (k == 5 && stride == 1) dw_bwd_go<5, 1>(dy, w, dx, B, g, acc, s);
+  else if (k == 5 && stride == 2) dw_bwd_go<5, 2>(dy, w, dx, B, g, acc, s);
+  else throw std::invalid_argument("dw: unsupported kernel/stride");
+  PHX_LAUNCH_CHECK();
+}
+
+}  // namespace phx
