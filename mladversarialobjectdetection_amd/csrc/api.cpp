@@ -292,6 +292,7 @@ Exec& phx_ctx::exec_for(int B) {
       E.slot_c[op.slot] = E.alloc<float>((size_t)B * ti.c);
       seg_need = std::max(seg_need, (size_t)B * ti.c * 2);
       red_need = std::max(red_need, colred_scratch_doubles((long)ti.h * ti.w, ti.c, B));
+      red_need = std::max(red_need, se_scratch_doubles(B, ti.c, op.cse));
       E.se_of_tensor[op.out] = (int)i;
     }
   }
@@ -540,20 +541,21 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_SE: kind = "se_bwd"; by = 4.0 * 3.0 * ti.numel(); break;
       default: break;
     }
+    // algorithmic bytes of a dgrad: a gradient view also reads the BN input; accumulation
+    // re-reads the destination
+    if (op.t == OP_PW || op.t == OP_DW) {
+      const int bi = E.bn_consumer[op.out];
+      if (bi >= 0 && P.ops[bi].bwd) by += 4.0 * (double)to.numel();
+      if (op.acc[0]) by += 4.0 * (double)ti.numel();
+    }
     Scope scope(ctx, kind, fl, by, s);
     switch (op.t) {
       case OP_STEM: {
         // the stem dgrad reads each dy element up to 4x: materialise the BN-backward output once
         GradX g = gview(ctx, E, op.out, input);
-        if (g.y) {
-          const int bi = E.bn_consumer[op.out];
-          const Op& bop = P.ops[bi];
-          float* gy = E.gptr(op.out);
-          launch_bn_bwd_apply2(g, gy, (long)to.rows(), to.c, s);
-          g = GradX{gy, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
-          (void)bop;
-        }
-        launch_stem_bwd(g, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
+        float* gy = E.gptr(op.out);
+        if (g.y) launch_bn_bwd_apply2(g, gy, (long)to.rows(), to.c, s);
+        launch_stem_bwd(g.y ? gy : g.da, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
                         op.acc[0], s);
         break;
       }
@@ -577,7 +579,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       case OP_SE:
         launch_se_bwd(dy, view(ctx, E, op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
-                      W + op.b1, W + op.w2, W + op.b2, op.act, E.slot_a[op.slot],
+                      W + op.b1, ctx->wt_of(op.w2), W + op.b2, op.act, E.slot_a[op.slot],
                       E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s, E.red);
         break;
       case OP_ADD:
@@ -943,7 +945,9 @@ int phx_profile(phx_ctx* ctx, int enable) {
 int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   if (!ctx) return PHX_EINVAL;
   PHX_TRY(ctx)
-  struct Agg { long n = 0; double ms = 0, flops = 0, bytes = 0; };
+  // per launch group: measured time and the roofline time of its algorithmic work at the MI355X
+  // peaks (HBM 8 TB/s, fp32 MFMA 157.3 TFLOP/s); roof = sum over launches of max(hbm, mfma)
+  struct Agg { long n = 0; double ms = 0, flops = 0, bytes = 0, hbm_ms = 0, mfma_ms = 0, roof_ms = 0; };
   std::map<std::string, Agg> agg;
   for (auto& r : ctx->prof.recs) {
     PHX_HIP(hipEventSynchronize(r.b));
@@ -954,6 +958,10 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
     a.ms += ms;
     a.flops += r.flops;
     a.bytes += r.bytes;
+    const double th = r.bytes / 8.0e12 * 1e3, tm = r.flops / 157.3e12 * 1e3;
+    a.hbm_ms += th;
+    a.mfma_ms += tm;
+    a.roof_ms += std::max(th, tm);
   }
   std::ostringstream js;
   js << "{";
@@ -961,7 +969,8 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   for (auto& kv : agg) {
     js << (first ? "" : ",") << "\"" << kv.first << "\":{\"count\":" << kv.second.n
        << ",\"ms\":" << kv.second.ms << ",\"flops\":" << kv.second.flops
-       << ",\"bytes\":" << kv.second.bytes << "}";
+       << ",\"bytes\":" << kv.second.bytes << ",\"hbm_ms\":" << kv.second.hbm_ms
+       << ",\"mfma_ms\":" << kv.second.mfma_ms << ",\"roof_ms\":" << kv.second.roof_ms << "}";
     first = false;
   }
   js << "}";

@@ -14,8 +14,8 @@ namespace phx {
 // 3x3 stride-2 stem, Cin = 3: x [B,H,W,3] -> y [B,Ho,Wo,Co]; w [3,3,3,Co] (HWIO)
 void launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                      int Co, int pt, int pl, hipStream_t s);
-// dx [B,H,W,3] (+)= conv_transpose(dy)
-void launch_stem_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int Ho,
+// dx [B,H,W,3] (+)= conv_transpose(dy); dy is a materialised gradient [B,Ho,Wo,Co]
+void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
                      int Wo, int Co, int pt, int pl, bool acc, hipStream_t s);
 // C[M,N] (+)= A[M,K] * B + bias ; B given as Bt[N][K].  rowscale (optional): A[m,k] is
 // multiplied by rowscale[(m / rows_per_img) * K + k] (SE excitation folded into the load).
@@ -66,11 +66,14 @@ void launch_bn_bwd_reduce(const float* da, const float* y, const float* mean, co
 void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
                    float* hidden, float* scale, hipStream_t s, double* scratch);
+// w2t: the expand kernel transposed to [C][Cse]
 void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
-                   const float* w1, const float* b1, const float* w2, const float* b2, int act,
+                   const float* w1, const float* b1, const float* w2t, const float* b2, int act,
                    const float* pool, const float* hidden, const float* scale, float* gsum,
                    bool acc, hipStream_t s, double* scratch);
 size_t colred_scratch_doubles(long seg_rows, int C, int nseg);
+// squeeze partials of the SE MLP (they reuse the colred scratch)
+size_t se_scratch_doubles(int B, int C, int Cse);
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s);
 // dst (+)= src
 void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s);

@@ -18,102 +18,163 @@ namespace phx {
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------
-// stem: 3x3 stride 2, Cin = 3
+// stem: 3x3 stride 2, Cin = 3 (efficientnet_model.py:507-528).  Every EfficientDet image side is
+// even, so TF SAME pads (0 top/left, 1 bottom/right) — the kernels rely on pt = pl = 0.  The
+// filter index of every multiply is wave-uniform, so the 27*CO taps stream through scalar
+// registers (s_load) and each lane keeps all CO output channels of its pixel in VGPRs.
 // ------------------------------------------------------------------------------------------
+template <int CO>
 __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
                                                   const float* __restrict__ w,
                                                   float* __restrict__ y, int B, int H, int W,
-                                                  int Ho, int Wo, int Co, int pt, int pl) {
-  const int C4 = Co >> 2;
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)B * Ho * Wo * C4;
-  if (idx >= total) return;
-  int c4 = (int)(idx % C4);
-  long p = idx / C4;
-  int ox = (int)(p % Wo);
-  long t = p / Wo;
-  int oy = (int)(t % Ho);
-  int b = (int)(t / Ho);
-  const int co = c4 * 4;
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+                                                  int Ho, int Wo) {
+  long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= (long)B * Ho * Wo) return;
+  const int ox = (int)(p % Wo);
+  const long t = p / Wo;
+  const int oy = (int)(t % Ho), b = (int)(t / Ho);
+  float acc[CO];
+#pragma unroll
+  for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+#pragma unroll
   for (int i = 0; i < 3; ++i) {
-    int iy = oy * 2 - pt + i;
-    if (iy < 0 || iy >= H) continue;
+    const int iy = oy * 2 + i;
+    if (iy >= H) continue;
+#pragma unroll
     for (int j = 0; j < 3; ++j) {
-      int ix = ox * 2 - pl + j;
-      if (ix < 0 || ix >= W) continue;
+      const int ix = ox * 2 + j;
+      if (ix >= W) continue;
       const float* xp = x + (((long)b * H + iy) * W + ix) * 3;
 #pragma unroll
       for (int ci = 0; ci < 3; ++ci) {
-        float xv = xp[ci];
-        float4 wv = *reinterpret_cast<const float4*>(w + ((i * 3 + j) * 3 + ci) * Co + co);
-        acc.x += xv * wv.x;
-        acc.y += xv * wv.y;
-        acc.z += xv * wv.z;
-        acc.w += xv * wv.w;
+        const float xv = xp[ci];
+        const float* wp = w + ((i * 3 + j) * 3 + ci) * CO;
+#pragma unroll
+        for (int c = 0; c < CO; ++c) acc[c] = fmaf(xv, wp[c], acc[c]);
       }
     }
   }
-  *reinterpret_cast<float4*>(y + p * Co + co) = acc;
+  float4* yp = reinterpret_cast<float4*>(y + p * CO);
+#pragma unroll
+  for (int c = 0; c < CO / 4; ++c) yp[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
 }
 
-__global__ __launch_bounds__(256) void k_stem_bwd(GradX dy,
+// dgrad per 2x2 input quad (2Y+a, 2X+c): with pt = pl = 0, input row 2Y takes filter row 0 from
+// output row Y and row 2 from Y-1, row 2Y+1 takes filter row 1 from Y (same for columns), so
+// every (dy pixel, tap) pairing is fixed at compile time and the taps stay wave-uniform.
+template <int CO>
+__global__ __launch_bounds__(256) void k_stem_bwd(const float* __restrict__ dy,
                                                   const float* __restrict__ w,
                                                   float* __restrict__ dx, int B, int H, int W,
-                                                  int Ho, int Wo, int Co, int pt, int pl,
-                                                  int acc_flag) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)B * H * W;
-  if (idx >= total) return;
-  int ix = (int)(idx % W);
-  long t = idx / W;
-  int iy = (int)(t % H);
-  int b = (int)(t / H);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-  for (int i = 0; i < 3; ++i) {
-    int ty = iy + pt - i;
-    if (ty < 0 || (ty & 1)) continue;
-    int oy = ty >> 1;
-    if (oy >= Ho) continue;
-    for (int j = 0; j < 3; ++j) {
-      int tx = ix + pl - j;
-      if (tx < 0 || (tx & 1)) continue;
-      int ox = tx >> 1;
-      if (ox >= Wo) continue;
-      const long gbase = (((long)b * Ho + oy) * Wo + ox) * Co;
-      const float* wp = w + (i * 3 + j) * 3 * Co;
-      for (int co = 0; co < Co; co += 4) {
-        float4 gv = gx_load4(dy, gbase + co, co);
-        float4 w0 = *reinterpret_cast<const float4*>(wp + co);
-        float4 w1 = *reinterpret_cast<const float4*>(wp + Co + co);
-        float4 w2 = *reinterpret_cast<const float4*>(wp + 2 * Co + co);
-        a0 += gv.x * w0.x + gv.y * w0.y + gv.z * w0.z + gv.w * w0.w;
-        a1 += gv.x * w1.x + gv.y * w1.y + gv.z * w1.z + gv.w * w1.w;
-        a2 += gv.x * w2.x + gv.y * w2.y + gv.z * w2.z + gv.w * w2.w;
+                                                  int Ho, int Wo, int acc_flag) {
+  const int Hq = H >> 1, Wq = W >> 1;
+  long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= (long)B * Hq * Wq) return;
+  const int X = (int)(q % Wq);
+  const long t = q / Wq;
+  const int Y = (int)(t % Hq), b = (int)(t / Hq);
+  float o[2][2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) o[a][c][ci] = 0.f;
+  // the four dy pixels (Y - dyo, X - dxo)
+#pragma unroll
+  for (int dyo = 0; dyo < 2; ++dyo) {
+#pragma unroll
+    for (int dxo = 0; dxo < 2; ++dxo) {
+      const int oy = Y - dyo, ox = X - dxo;
+      if (oy < 0 || ox < 0 || oy >= Ho || ox >= Wo) continue;
+      float g[CO];
+      const float4* gp = reinterpret_cast<const float4*>(dy + (((long)b * Ho + oy) * Wo + ox) * CO);
+#pragma unroll
+      for (int c = 0; c < CO / 4; ++c) {
+        const float4 v = gp[c];
+        g[4 * c] = v.x; g[4 * c + 1] = v.y; g[4 * c + 2] = v.z; g[4 * c + 3] = v.w;
+      }
+      // rows: dyo = 0 -> (a=0,i=0), (a=1,i=1); dyo = 1 -> (a=0,i=2).  Columns alike.
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int i = dyo ? 2 : a;
+        if (dyo && a) continue;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int j = dxo ? 2 : c;
+          if (dxo && c) continue;
+#pragma unroll
+          for (int ci = 0; ci < 3; ++ci) {
+            const float* wp = w + ((i * 3 + j) * 3 + ci) * CO;
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int k = 0; k < CO; k += 2) {
+              s0 = fmaf(g[k], wp[k], s0);
+              s1 = fmaf(g[k + 1], wp[k + 1], s1);
+            }
+            o[a][c][ci] += s0 + s1;
+          }
+        }
       }
     }
   }
-  float* o = dx + idx * 3;
-  if (acc_flag) {
-    o[0] += a0; o[1] += a1; o[2] += a2;
-  } else {
-    o[0] = a0; o[1] = a1; o[2] = a2;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    float2* op = reinterpret_cast<float2*>(dx + (((long)b * H + 2 * Y + a) * W + 2 * X) * 3);
+    float2 v0 = make_float2(o[a][0][0], o[a][0][1]);
+    float2 v1 = make_float2(o[a][0][2], o[a][1][0]);
+    float2 v2 = make_float2(o[a][1][1], o[a][1][2]);
+    if (acc_flag) {
+      const float2 p0 = op[0], p1 = op[1], p2 = op[2];
+      v0.x += p0.x; v0.y += p0.y; v1.x += p1.x; v1.y += p1.y; v2.x += p2.x; v2.y += p2.y;
+    }
+    op[0] = v0;
+    op[1] = v1;
+    op[2] = v2;
   }
 }
+
+template <template <int> class Launch, class... Args>
+static void stem_dispatch(int Co, Args... args) {
+  switch (Co) {
+    case 32: Launch<32>::go(args...); break;
+    case 40: Launch<40>::go(args...); break;
+    case 48: Launch<48>::go(args...); break;
+    case 56: Launch<56>::go(args...); break;
+    case 64: Launch<64>::go(args...); break;
+    default: throw std::invalid_argument("stem: unsupported output channels");
+  }
+}
+
+template <int CO>
+struct StemFwd {
+  static void go(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
+                 hipStream_t s) {
+    long total = (long)B * Ho * Wo;
+    hipLaunchKernelGGL((k_stem_fwd<CO>), dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo);
+  }
+};
+template <int CO>
+struct StemBwd {
+  static void go(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho, int Wo,
+                 int acc, hipStream_t s) {
+    long total = (long)B * (H / 2) * (W / 2);
+    hipLaunchKernelGGL((k_stem_bwd<CO>), dim3(cdiv(total, 256)), dim3(256), 0, s, dy, w, dx, B, H, W, Ho,
+                       Wo, acc);
+  }
+};
 
 void launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                      int Co, int pt, int pl, hipStream_t s) {
-  long total = (long)B * Ho * Wo * (Co / 4);
-  hipLaunchKernelGGL(k_stem_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo,
-                     Co, pt, pl);
+  if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
+  stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, s);
   PHX_LAUNCH_CHECK();
 }
 
-void launch_stem_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int Ho,
+void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
                      int Wo, int Co, int pt, int pl, bool acc, hipStream_t s) {
-  long total = (long)B * H * W;
-  hipLaunchKernelGGL(k_stem_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, w, dx, B, H, W, Ho,
-                     Wo, Co, pt, pl, acc ? 1 : 0);
+  if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
+  stem_dispatch<StemBwd>(Co, dy, w, dx, B, H, W, Ho, Wo, acc ? 1 : 0, s);
   PHX_LAUNCH_CHECK();
 }
 

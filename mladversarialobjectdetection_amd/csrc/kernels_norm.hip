@@ -407,44 +407,121 @@ struct SumEpi {
   }
 };
 
-// one block per image: pool -> fc1(+b1) -> act -> fc2(+b2) -> sigmoid
-__global__ __launch_bounds__(256) void k_se_fc(const float* __restrict__ part, int chunks, int HW,
-                                               int C, int Cse, const float* __restrict__ w1,
-                                               const float* __restrict__ b1,
-                                               const float* __restrict__ w2,
-                                               const float* __restrict__ b2, int act,
-                                               float* __restrict__ pool, float* __restrict__ hidden,
-                                               float* __restrict__ scale) {
-  extern __shared__ float sm[];
-  float* sp = sm;           // [C]
-  float* sh = sm + C;       // [Cse]
-  const int b = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float s = part[(long)b * C + c] / (float)HW;  // part: per-image channel sums
-    sp[c] = s;
-    pool[(long)b * C + c] = s;
-  }
-  __syncthreads();
-  // hidden[j] = b1[j] + sum_c pool[c] * w1[c][j]: one wave per hidden unit, lanes over c
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int j = wv; j < Cse; j += nw) {
-    float h = 0.f;
-    for (int c = lane; c < C; c += 64) h += sp[c] * w1[c * Cse + j];
-    for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
-    if (lane == 0) {
-      h += b1[j];
-      hidden[(long)b * Cse + j] = h;  // pre-activation
-      sh[j] = act_fwd(h, act);
+// The SE MLP ([B,C] -> [B,Cse] -> [B,C], efficientnet_model.py:184-196) is tiny but latency-
+// bound, so it is spread over many workgroups in two launches:
+//   squeeze  grid (G = ceil(C/64), B): part[b][g][j] = sum over the g-th 64-channel slice of
+//            v[b][c] * m[c][j]; lanes run over j (coalesced rows of m), the 4 waves take 16
+//            channels each with all 16 loads in flight, and meet in LDS;
+//   excite   grid (ceil(C/256), B): every block re-sums the G partials of its image (Cse values),
+//            then one lane per channel runs the expand row.
+constexpr int kSeSlice = 64;
+
+static int se_groups(int C) { return (C + kSeSlice - 1) / kSeSlice; }
+
+size_t se_scratch_doubles(int B, int C, int Cse) {
+  return ((size_t)B * se_groups(C) * Cse + 1) / 2 + 1;
+}
+
+// MODE 0: v = sums * inv (pool, also written out); MODE 1: v = gsum * s * (1 - s)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_se_squeeze(const float* __restrict__ a,
+                                                    const float* __restrict__ sv, float inv, int C,
+                                                    int N, const float* __restrict__ m,
+                                                    float* __restrict__ part,
+                                                    float* __restrict__ pool) {
+  __shared__ float v[kSeSlice];
+  __shared__ float red[256];
+  const int g = blockIdx.x, b = blockIdx.y, G = gridDim.x;
+  const int c0 = g * kSeSlice, n = min(kSeSlice, C - c0);
+  if (threadIdx.x < kSeSlice) {
+    float x = 0.f;
+    if ((int)threadIdx.x < n) {
+      const long i = (long)b * C + c0 + threadIdx.x;
+      if (MODE == 0) {
+        x = a[i] * inv;
+        pool[i] = x;
+      } else {
+        const float sg = sv[i];
+        x = a[i] * sg * (1.f - sg);
+      }
     }
+    v[threadIdx.x] = x;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float e = b2[c];
-    for (int j = 0; j < Cse; ++j) e += sh[j] * w2[j * C + c];
-    scale[(long)b * C + c] = sigmoidf_(e);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float* mr = m + (long)(c0 + wv * 16) * N;
+  for (int j0 = 0; j0 < N; j0 += 64) {
+    const int j = j0 + lane;
+    float acc = 0.f;
+    if (j < N) {
+      float t[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t[r] = (wv * 16 + r < n) ? mr[(long)r * N + j] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc = fmaf(v[wv * 16 + r], t[r], acc);
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (wv == 0 && j < N)
+      part[((long)b * G + g) * N + j] = red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane];
+    __syncthreads();
   }
 }
 
+// forward excite: hidden = b1 + sum_g part; h = act(hidden); scale = sigmoid(b2 + h . w2[:, c])
+__global__ __launch_bounds__(256) void k_se_excite(const float* __restrict__ part, int G, int C,
+                                                   int N, const float* __restrict__ b1,
+                                                   const float* __restrict__ w2,
+                                                   const float* __restrict__ b2, int act,
+                                                   float* __restrict__ hidden,
+                                                   float* __restrict__ scale) {
+  extern __shared__ float sh[];  // [N]
+  const int b = blockIdx.y;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    float h = b1[j];
+    for (int g = 0; g < G; ++g) h += part[((long)b * G + g) * N + j];
+    if (blockIdx.x == 0) hidden[(long)b * N + j] = h;  // pre-activation, kept for backward
+    sh[j] = act_fwd(h, act);
+  }
+  __syncthreads();
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float e[4] = {b2[c], 0.f, 0.f, 0.f};
+  int j = 0;
+  for (; j + 3 < N; j += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = fmaf(sh[j + u], w2[(long)(j + u) * C + c], e[u]);
+  }
+  for (; j < N; ++j) e[0] = fmaf(sh[j], w2[(long)j * C + c], e[0]);
+  scale[(long)b * C + c] = sigmoidf_((e[0] + e[1]) + (e[2] + e[3]));
+}
+
+// backward excite: dh = (sum_g part) * act'(hidden); dpool[c] = dh . w1[c, :]
+__global__ __launch_bounds__(256) void k_se_excite_bwd(const float* __restrict__ part, int G,
+                                                       int C, int N,
+                                                       const float* __restrict__ w1, int act,
+                                                       const float* __restrict__ hidden,
+                                                       float* __restrict__ dpool) {
+  extern __shared__ float dh[];  // [N]
+  const int b = blockIdx.y;
+  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+    float d = 0.f;
+    for (int g = 0; g < G; ++g) d += part[((long)b * G + g) * N + j];
+    dh[j] = d * act_grad(hidden[(long)b * N + j], act);
+  }
+  __syncthreads();
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float* wr = w1 + (long)c * N;
+  float e[4] = {0.f, 0.f, 0.f, 0.f};
+  int j = 0;
+  for (; j + 3 < N; j += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = fmaf(dh[j + u], wr[j + u], e[u]);
+  }
+  for (; j < N; ++j) e[0] = fmaf(dh[j], wr[j], e[0]);
+  dpool[(long)b * C + c] = (e[0] + e[1]) + (e[2] + e[3]);
+}
 
 void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
@@ -452,43 +529,16 @@ void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* 
   // per-image channel sums land after the pool vector: pool buffer = [B*C pool | B*C sums]
   float* sums = pool + (long)B * C;
   colred(SumAcc{x, nullptr, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
-  size_t shm = (size_t)(C + Cse) * sizeof(float);
-  hipLaunchKernelGGL(k_se_fc, dim3(B), dim3(256), shm, s, sums, 1, HW, C, Cse, w1, b1, w2, b2, act,
-                     pool, hidden, scale);
+  // the colred scratch is free again once the sums are out: it holds the squeeze partials
+  float* part = reinterpret_cast<float*>(scratch);
+  const int G = se_groups(C);
+  hipLaunchKernelGGL(k_se_squeeze<0>, dim3(G, B), dim3(256), 0, s, sums, nullptr, 1.0f / (float)HW, C,
+                     Cse, w1, part, pool);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(C, 256), B), dim3(256), Cse * sizeof(float), s, part, G, C,
+                     Cse, b1, w2, b2, act, hidden, scale);
   PHX_LAUNCH_CHECK();
   (void)y;  // the excitation is folded into the consuming GEMM's A load (rowscale)
-}
-
-// backward FC chain, one block per image: gsum[c] = sum_hw dy*x  ->  dpool[c]
-__global__ __launch_bounds__(256) void k_se_fc_bwd(const float* __restrict__ part, int chunks,
-                                                   int C, int Cse, const float* __restrict__ w1,
-                                                   const float* __restrict__ w2, int act,
-                                                   const float* __restrict__ hidden,
-                                                   const float* __restrict__ scale,
-                                                   float* __restrict__ dpool) {
-  extern __shared__ float sm[];
-  float* de = sm;        // [C]  d(pre-sigmoid)
-  float* dh = sm + C;    // [Cse]
-  const int b = blockIdx.x;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float g = part[(long)b * C + c];  // per-image sum_hw dy * x
-    float sv = scale[(long)b * C + c];
-    de[c] = g * sv * (1.f - sv);
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int j = wv; j < Cse; j += nw) {
-    float a = 0.f;
-    for (int c = lane; c < C; c += 64) a += de[c] * w2[j * C + c];
-    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
-    if (lane == 0) dh[j] = a * act_grad(hidden[(long)b * Cse + j], act);
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float a = 0.f;
-    for (int j = 0; j < Cse; ++j) a += dh[j] * w1[c * Cse + j];
-    dpool[(long)b * C + c] = a;
-  }
 }
 
 __global__ __launch_bounds__(256) void k_se_bwd_apply(const float* __restrict__ dy,
@@ -516,15 +566,19 @@ __global__ __launch_bounds__(256) void k_se_bwd_apply(const float* __restrict__ 
 }
 
 void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
-                   const float* w1, const float* b1, const float* w2, const float* b2, int act,
+                   const float* w1, const float* b1, const float* w2t, const float* b2, int act,
                    const float* pool, const float* hidden, const float* scale, float* gsum,
                    bool acc, hipStream_t s, double* scratch) {
   (void)b1; (void)b2; (void)pool;
   float* sums = gsum + (long)B * C;  // gsum: [B*C dpool | B*C sum_hw dy*x]
   colred(SumAcc{x, dy, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
-  size_t shm = (size_t)(C + Cse) * sizeof(float);
-  hipLaunchKernelGGL(k_se_fc_bwd, dim3(B), dim3(256), shm, s, sums, 1, C, Cse, w1, w2, act, hidden,
-                     scale, gsum);
+  float* part = reinterpret_cast<float*>(scratch);
+  const int G = se_groups(C);
+  hipLaunchKernelGGL(k_se_squeeze<1>, dim3(G, B), dim3(256), 0, s, sums, scale, 1.0f, C, Cse, w2t, part,
+                     nullptr);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_se_excite_bwd, dim3(cdiv(C, 256), B), dim3(256), Cse * sizeof(float), s, part, G,
+                     C, Cse, w1, act, hidden, gsum);
   PHX_LAUNCH_CHECK();
   long n4 = (long)B * HW * C / 4;
   hipLaunchKernelGGL(k_se_bwd_apply, dim3(cdiv(n4, 256)), dim3(256), 0, s, dy, scale, gsum, dx, n4,
