@@ -1,0 +1,80 @@
+"""Summarise rocprofv3 PMC passes (scripts/gpu_pmc.sh) into per-kind HBM traffic per launch.
+
+HBM bytes = 2 * FETCH_SIZE + WRITE_SIZE (both in KiB), per MI355X_MICROARCH.md's HBM section: on gfx950
+FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) coalesced reads; WRITE_SIZE is exact for
+16-B stores.  Kinds match the library profiler's launch groups; `launches` counts the group's primary
+kernel.
+
+    python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_traffic.json
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+KINDS = [  # (kind, substring, primary?)
+    ("gemm", "k_gemm<", True), ("gemm", "k_gemm_splitk_reduce", False),
+    ("dw_fwd", "k_dw_fwd<", True), ("dw_bwd", "k_dw_bwd<", True),
+    ("bn_stats", "k_colred_part<phx::StatsAcc>", True), ("bn_stats", "k_colred_final<phx::StatsEpi>", False),
+    ("bn_bwd_reduce", "k_colred_part<phx::BwdAcc>", True), ("bn_bwd_reduce", "k_colred_final<phx::BwdEpi2>", False),
+    ("se_pool", "k_colred_part<phx::SumAcc>", True), ("se_pool", "k_colred_final<phx::SumEpi>", False),
+]
+
+
+def kind_of(name):
+    for k, sub, prim in KINDS:
+        if sub in name:
+            return k, prim
+    return None, False
+
+
+def load(d, counter):
+    rows = list(csv.DictReader(open(f"{d}/run_counter_collection.csv")))
+    out = {}
+    for r in rows:
+        if r["Counter_Name"] == counter:
+            out[int(r["Dispatch_Id"])] = (r["Kernel_Name"], float(r["Counter_Value"]))
+    return out
+
+
+def main(fd, wd, dst):
+    f, w = load(fd, "FETCH_SIZE"), load(wd, "WRITE_SIZE")
+    agg = defaultdict(lambda: {"launches": 0, "fetch_kib": 0.0, "write_kib": 0.0})
+    per_kernel = defaultdict(lambda: {"n": 0, "fetch_kib": 0.0})
+    for did, (name, v) in f.items():
+        k, prim = kind_of(name)
+        per_kernel[name]["n"] += 1
+        per_kernel[name]["fetch_kib"] += v
+        if k is None:
+            continue
+        agg[k]["fetch_kib"] += v
+        agg[k]["launches"] += int(prim)
+    # the two passes are separate runs of the same deterministic program: match by kernel order
+    for did, (name, v) in w.items():
+        k, _ = kind_of(name)
+        if k is not None:
+            agg[k]["write_kib"] += v
+        per_kernel[name].setdefault("write_kib", 0.0)
+        per_kernel[name]["write_kib"] = per_kernel[name].get("write_kib", 0.0) + v
+    kinds = {}
+    for k, a in agg.items():
+        byt = (2.0 * a["fetch_kib"] + a["write_kib"]) * 1024.0
+        kinds[k] = {"launches": a["launches"], "hbm_bytes": byt,
+                    "bytes_per_launch": round(byt / max(1, a["launches"])),
+                    "read_bytes": 2.0 * a["fetch_kib"] * 1024.0, "write_bytes": a["write_kib"] * 1024.0}
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
+                     "python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile",
+           "correction": "bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB), gfx950 half-counted wide reads",
+           "kinds": kinds}
+    with open(dst, "w") as fh:
+        json.dump(res, fh, indent=1)
+    with open(dst.replace(".json", "_kernels.csv"), "w") as fh:
+        fh.write("kernel,dispatches,fetch_kib_x2,write_kib\n")
+        for name, a in sorted(per_kernel.items(), key=lambda kv: -kv[1]["fetch_kib"]):
+            fh.write(f"\"{name[:120]}\",{a['n']},{2 * a['fetch_kib']:.1f},{a.get('write_kib', 0.0):.1f}\n")
+    for k, v in sorted(kinds.items()):
+        print(f"{k:14s} launches {v['launches']:5d}  MB/launch {v['bytes_per_launch'] / 1e6:9.3f}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
