@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import math
 import os
+from collections.abc import Mapping
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -176,14 +177,15 @@ def _pad_boxes(boxes, B, device):
     maxb = max(1, max(len(b) for b in boxes))
     if maxb > _lib.MAX_OUT:
         raise ValueError("at most 100 boxes per image")
-    out = torch.zeros(B, maxb, 4, device=device)
-    cnt = torch.zeros(B, dtype=torch.int32, device=device)
+    # padded on the host, then one transfer: [B*maxb*4 boxes | B counts] as raw 32-bit words
+    out = np.zeros((B, maxb, 4), np.float32)
+    cnt = np.zeros(B, np.int32)
     for i, b in enumerate(boxes):
-        b = torch.as_tensor(np.asarray(b, dtype=np.float32)).reshape(-1, 4)
-        if len(b):
-            out[i, :len(b)] = b.to(device)
+        b = np.asarray(b, dtype=np.float32).reshape(-1, 4)
+        out[i, :len(b)] = b
         cnt[i] = len(b)
-    return out, cnt
+    flat = torch.as_tensor(np.concatenate([out.reshape(-1).view(np.int32), cnt])).to(device)
+    return flat[:out.size].view(torch.float32).view(B, maxb, 4), flat[out.size:]
 
 
 class Patcher:
@@ -222,6 +224,30 @@ class _Mean:
         return self.total / max(self.count, 1)
 
 
+class _StepMetrics(Mapping):
+    """The {name: running mean} dict train_step returns, evaluated on first access."""
+
+    def __init__(self, attacker, sid):
+        self._a, self._sid, self._d = attacker, sid, None
+
+    def _get(self):
+        if self._d is None:
+            self._a._flush_metrics()
+            snap = self._a._snapshots.get(self._sid)
+            # a reset_metrics() after this step dropped its snapshot: report the current means
+            self._d = dict(snap) if snap is not None else {k: m.result() for k, m in self._a.metrics.items()}
+        return self._d
+
+    def __getitem__(self, k):
+        return self._get()[k]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
+
+
 class PatchAttacker:
     """attacker.PatchAttacker: trainable [patch | scale] optimised against the victim."""
 
@@ -254,6 +280,11 @@ class PatchAttacker:
         self._patcher = Patcher(self)
         self._matcher = BrightnessMatcher(model)
         self.metrics = {k: _Mean() for k in self.METRICS}
+        self._pending = []      # (step id, device metric row) not yet folded into self.metrics
+        self._snapshots = {}    # step id -> running-mean dict after that step
+        self._step_id = 0
+        self._bconst = {}
+        self._last_B = 0
         self.bins = np.arange(self.config.nms_configs.score_thresh, .805, .01, dtype="float32")
 
     # ---- variables -----------------------------------------------------------------------------
@@ -308,38 +339,80 @@ class PatchAttacker:
     def allreduce_gradients(self):
         ddp.allreduce_sum_(self.grad)
 
-    def step_metrics(self, reduce=True):
-        """Per-step values of the reference's add_metric set (attacker.py:196-207)."""
-        mb = self.metrics_buf.clone()
-        B = torch.tensor([float(self._last_B)], device=mb.device)
-        if reduce:
-            ddp.allreduce_sum_(mb)
-            ddp.allreduce_sum_(B)
-        v = mb.cpu().numpy().astype(np.float64)
-        n = float(B.item())
-        scale = float(self.scale.item())
+    def _metric_row(self):
+        """Device row [metrics_buf | batch | scale] of the step just run (scale before the update,
+        as the reference's add_metric(self._scale_regressor) inside call, attacker.py:197)."""
+        B = self._last_B
+        bt = self._bconst.get(B)
+        if bt is None:
+            bt = self._bconst[B] = torch.tensor([float(B)], device=self.params.device)
+        return torch.cat([self.metrics_buf, bt, self.params[_lib.NPATCH:]])
+
+    @staticmethod
+    def _derive(v):
+        """add_metric values (attacker.py:196-207) from a rank-summed [metrics | n | scale] row."""
+        n, scale = float(v[_lib.NMETRIC]), float(v[_lib.NMETRIC + 1])
         mean = v[_lib.M_SUM_M] / n
         var = max(v[_lib.M_SUM_M2] / n - mean * mean, 0.0)
         asr = 1.0 - v[_lib.M_ASR_NUM] / (v[_lib.M_ASR_DEN] + 1e-7)
-        return {"loss": v[_lib.M_LOSS], "scale": scale, "scale_loss": v[_lib.M_SCALE_LOSS],
-                "tv_loss": v[_lib.M_TV], "mean_max_score": mean, "std_max_score": math.sqrt(var),
+        return {"loss": float(v[_lib.M_LOSS]), "scale": scale, "scale_loss": float(v[_lib.M_SCALE_LOSS]),
+                "tv_loss": float(v[_lib.M_TV]), "mean_max_score": mean, "std_max_score": math.sqrt(var),
                 "asr": asr, "asr_to_scale": asr / scale if scale else float("inf"),
-                "patches": v[_lib.M_NBOX]}
+                "patches": float(v[_lib.M_NBOX])}
+
+    def _reduce_rows(self, rows):
+        """Sum per-rank metric rows over ranks (the replicated scale column is kept as is)."""
+        m = torch.stack(rows)
+        if ddp.is_dist():
+            scale = m[:, -1].clone()
+            ddp.allreduce_sum_(m)
+            m[:, -1] = scale
+        return m.cpu().numpy().astype(np.float64)
+
+    def step_metrics(self, reduce=True):
+        """Per-step values of the reference's add_metric set (attacker.py:196-207) for the step
+        just run (synchronises with the device)."""
+        row = self._metric_row()
+        v = self._reduce_rows([row]) if reduce else row[None].cpu().numpy().astype(np.float64)
+        return self._derive(v[0])
+
+    def _flush_metrics(self):
+        """Fold the queued per-step rows into the Keras-style running means: one all-reduce and one
+        device->host copy for all of them, so train_step itself never waits on the GPU."""
+        if not self._pending:
+            return
+        ids = [i for i, _ in self._pending]
+        rows = self._reduce_rows([r for _, r in self._pending])
+        self._pending.clear()
+        for sid, v in zip(ids, rows):
+            sm = self._derive(v)
+            for k in self.METRICS:
+                self.metrics[k].update(sm[k])
+            self._snapshots[sid] = {k: m.result() for k, m in self.metrics.items()}
+        for old in [k for k in self._snapshots if k < ids[-1] - 1024]:
+            del self._snapshots[old]
 
     def train_step(self, inputs, boxes=None):
-        """attacker.py:307-316: grads = self(inputs); apply_gradients; return metrics."""
+        """attacker.py:307-316: grads = self(inputs); apply_gradients; return metrics.  The metric
+        dict is evaluated lazily (like the tensors Keras returns): reading it synchronises."""
         self.call(inputs, boxes=boxes)
+        sid = self._step_id
+        self._step_id += 1
+        self._pending.append((sid, self._metric_row()))
+        if len(self._pending) >= 256:  # bound the queue when nobody reads the metrics
+            self._flush_metrics()
         self.allreduce_gradients()
         self.apply_gradients()
         self.cur_step += 1
-        sm = self.step_metrics()
-        for k in self.METRICS:
-            self.metrics[k].update(sm[k])
-        return {k: m.result() for k, m in self.metrics.items()}
+        return _StepMetrics(self, sid)
 
     def reset_metrics(self):
+        """Keras reset at epoch boundaries: queued steps are folded first (they belong to the
+        finished epoch)."""
+        self._flush_metrics()
         for m in self.metrics.values():
             m.total, m.count = 0.0, 0
+        self._snapshots = {}
 
     def save_weights(self, dirpath, **kwargs):
         """attacker.py:328-341: scale.txt, patch.png (de-normalised uint8), patch.npy (float32;

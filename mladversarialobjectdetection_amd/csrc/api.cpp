@@ -55,6 +55,12 @@ struct Exec {
   std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
   std::vector<int> bn_consumer;                // tensor id -> BN op index reading it (-1)
   std::vector<float*> slot_d, slot_e;          // BN backward: mean(dz), mean(dz*xhat)
+  // BN statistics fused into the producing kernel (StatSink): channel-major partials and their
+  // row counts; fused_bn[i]: BN op i takes its statistics from its producer
+  float2* spart = nullptr;
+  float* scnt = nullptr;
+  std::vector<char> fused_bn;
+  std::vector<int> stat_P;                     // tensor id -> partial rows written by its producer
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -296,6 +302,30 @@ Exec& phx_ctx::exec_for(int B) {
       E.se_of_tensor[op.out] = (int)i;
     }
   }
+  // fused statistics: a BN whose input is produced by the op right before it (stem, 1x1 conv,
+  // depthwise conv) gets its batch statistics from that producer's epilogue
+  E.fused_bn.assign(P.ops.size(), 0);
+  E.stat_P.assign(P.tensors.size(), 0);
+  size_t sp_need = 1, sc_need = 1;
+  if (bn_mode == PHX_BN_LOCAL) {
+    for (size_t i = 1; i < P.ops.size(); ++i) {
+      const Op& op = P.ops[i];
+      const Op& pr = P.ops[i - 1];
+      if (op.t != OP_BN || pr.out != op.in[0]) continue;
+      const Tensor& ti = P.tensors[pr.in[0]];
+      const Tensor& to = P.tensors[pr.out];
+      int np = 0;
+      if (pr.t == OP_STEM) np = cdiv((long)to.rows(), 256);
+      else if (pr.t == OP_PW && to.c % 4 == 0) np = gemm_stat_partials((int)ti.rows(), to.c, ti.c);
+      else if (pr.t == OP_DW) np = dw_stat_partials(ti.n, ti.h, ti.w, ti.c, to.h, to.w, pr.k, pr.stride, pr.pad_t, pr.pad_l);
+      if (np <= 0) continue;
+      E.fused_bn[i] = 1;
+      sp_need = std::max(sp_need, (size_t)np * to.c);
+      sc_need = std::max(sc_need, (size_t)np);
+    }
+  }
+  E.spart = E.alloc<float2>(sp_need);
+  E.scnt = E.alloc<float>(sc_need);
   size_t gp_need = 1;
   for (const Op& op : P.ops) {
     if (op.t != OP_PW) continue;
@@ -431,10 +461,15 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_SE: kind = "se_fwd"; by = 4.0 * ti.numel(); break;
       default: break;
     }
+    // the BN right after this op takes its statistics from this launch (StatSink)
+    const bool sink_on = i + 1 < P.ops.size() && E.fused_bn[i + 1];
+    const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0} : StatSink{};
+    if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
     Scope scope(ctx, kind, fl, by, s);
+    int np = 0;
     switch (op.t) {
       case OP_STEM:
-        launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s);
+        np = launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s, sink);
         break;
       case OP_PW: {
         InX A = view(ctx, E, op.in[0], input);
@@ -447,13 +482,13 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
           rs = E.slot_c[sop.slot];
           rpi = ti.h * ti.w;
         }
-        launch_gemm(A, ctx->wt_of(op.w), op.b >= 0 ? W + op.b : nullptr, y, (int)ti.rows(), to.c,
-                    ti.c, false, rs, rpi, s, E.gpart);
+        np = launch_gemm(A, ctx->wt_of(op.w), op.b >= 0 ? W + op.b : nullptr, y, (int)ti.rows(), to.c,
+                         ti.c, false, rs, rpi, s, E.gpart, sink);
         break;
       }
       case OP_DW:
-        launch_dw_fwd(view(ctx, E, op.in[0], input), W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
-                      op.pad_l, s);
+        np = launch_dw_fwd(view(ctx, E, op.in[0], input), W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k,
+                           op.stride, op.pad_t, op.pad_l, s, sink);
         break;
       case OP_BN: {
         float* mean = E.slot_a[op.slot];
@@ -462,6 +497,9 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         if (frozen)
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
                                  E.slot_c[op.slot], ti.c, kBnEps, s);
+        else if (E.fused_bn[i])
+          launch_bn_finalize(E.spart, E.scnt, E.stat_P[op.in[0]], (long)ti.rows(), ti.c, mean, rstd,
+                             W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
         else
           launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.gamma,
                           E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
@@ -494,6 +532,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       }
     }
+    if (sink_on) E.stat_P[op.out] = np;
   }
 }
 

@@ -162,6 +162,39 @@ __device__ __forceinline__ float4 gx_load4(const GradX& g, long e, int c) {
 }
 
 // ------------------------------------------------------------------------------------------
+// StatSink: training-mode BN batch statistics computed by the kernel that PRODUCES the BN input
+// (GEMM epilogue, depthwise conv, stem), so the statistics cost no extra pass over HBM.  Each
+// producer workgroup reduces the rows it wrote to a per-channel (sum, M2) pair — M2 about the
+// workgroup's own mean, so no cancellation — and stores it as partial p of channel c at
+// part[c*P + p] (cnt[p] = rows covered).  Channel-major, so k_bn_finalize reads each channel's P
+// partials contiguously (one workgroup per channel, fp64, fixed order: bit-reproducible), then
+// writes mean / rstd / gamma*rstd and updates the moving statistics.
+// ------------------------------------------------------------------------------------------
+struct StatSink {
+  float2* part;  // [C][P] (sum, M2); nullptr = no statistics wanted
+  float* cnt;    // [P]
+  int C;
+  int P;         // partial rows (set by the producer's launcher)
+};
+
+__device__ __forceinline__ void sink_put(const StatSink& k, long p, int c, float n, float mean,
+                                         float m2) {
+  k.part[(long)c * k.P + p] = make_float2(n * mean, m2);
+}
+
+// (n, mean, M2) += (nb, mb, m2b)
+__device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb,
+                                           float m2b) {
+  const float nt = n + nb;
+  if (nb <= 0.f) return;
+  const float f = nb / nt;
+  const float d = mb - mean;
+  mean = fmaf(d, f, mean);
+  m2 += m2b + d * d * n * f;
+  n = nt;
+}
+
+// ------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11), counter-based: identical draws for a given
 // (key, counter) on any device / GPU count.  Matches oracle/philox.py bit for bit.
 // ------------------------------------------------------------------------------------------

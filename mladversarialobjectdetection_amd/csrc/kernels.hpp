@@ -12,8 +12,9 @@ namespace phx {
 
 // ---- convolutions (kernels_conv.hip) ------------------------------------------------------
 // 3x3 stride-2 stem, Cin = 3: x [B,H,W,3] -> y [B,Ho,Wo,Co]; w [3,3,3,Co] (HWIO)
-void launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                     int Co, int pt, int pl, hipStream_t s);
+// returns the number of StatSink partial rows written (sink.part == nullptr: no statistics)
+int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
+                    int Co, int pt, int pl, hipStream_t s, StatSink sink = StatSink{});
 // dx [B,H,W,3] (+)= conv_transpose(dy); dy is a materialised gradient [B,Ho,Wo,Co]
 void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
                      int Wo, int Co, int pt, int pl, bool acc, hipStream_t s);
@@ -24,15 +25,19 @@ struct GemmPlan {
 };
 GemmPlan plan_gemm(int M, int N, int K);
 size_t gemm_partial_floats(int M, int N, int K);
-void launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
-                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-                 float* partial);
+// returns the StatSink partial rows written (see gemm_stat_partials)
+int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
+                bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+                float* partial, StatSink sink = StatSink{});
+int gemm_stat_partials(int M, int N, int K);
 // dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
 void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                        hipStream_t s, float* partial);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
-void launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
-                   int Wo, int k, int stride, int pt, int pl, hipStream_t s);
+int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
+                  int Wo, int k, int stride, int pt, int pl, hipStream_t s,
+                  StatSink sink = StatSink{});
+int dw_stat_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl);
 void launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
                    int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s);
 void launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);
@@ -44,6 +49,10 @@ size_t bn_stats_scratch_doubles(long M, int C);
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
                      const float* gamma, float* sc, float* mmean, float* mvar, float eps,
                      hipStream_t s);
+// training-mode BN statistics from the P producer partials of a StatSink (k_bn_finalize)
+void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
+                        float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
+                        float eps, hipStream_t s);
 // frozen BN: mean/rstd from moving statistics
 void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd,
                             const float* gamma, float* sc, int C, float eps, hipStream_t s);

@@ -23,13 +23,18 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // filter index of every multiply is wave-uniform, so the 27*CO taps stream through scalar
 // registers (s_load) and each lane keeps all CO output channels of its pixel in VGPRs.
 // ------------------------------------------------------------------------------------------
-template <int CO>
+template <int CO, bool STATS>
 __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
                                                   const float* __restrict__ w,
                                                   float* __restrict__ y, int B, int H, int W,
-                                                  int Ho, int Wo) {
+                                                  int Ho, int Wo, StatSink sink) {
   long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= (long)B * Ho * Wo) return;
+  const long total = (long)B * Ho * Wo;
+  if (STATS) {
+    if (p >= total) p = total - 1;  // keep every lane for the block reduction (masked below)
+  } else if (p >= total) {
+    return;
+  }
   const int ox = (int)(p % Wo);
   const long t = p / Wo;
   const int oy = (int)(t % Ho), b = (int)(t / Ho);
@@ -57,6 +62,39 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
   float4* yp = reinterpret_cast<float4*>(y + p * CO);
 #pragma unroll
   for (int c = 0; c < CO / 4; ++c) yp[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+  if constexpr (STATS) {
+    // block statistics through an LDS transpose: G row groups x CO channels, two passes
+    constexpr int G = 256 / CO, RG = (256 + G - 1) / G;
+    __shared__ float tl[256][CO + 1];
+    __shared__ float gm[G][CO], g2[G][CO], gn[G];
+#pragma unroll
+    for (int c = 0; c < CO; ++c) tl[threadIdx.x][c] = acc[c];
+    __syncthreads();
+    const int nval = (int)min<long>(256, total - (long)blockIdx.x * 256);
+    const int t = threadIdx.x, c = t % CO, gi = t / CO;
+    if (gi < G) {
+      const int r0 = gi * RG, r1 = min(nval, r0 + RG);
+      float sm = 0.f;
+      for (int r = r0; r < r1; ++r) sm += tl[r][c];
+      const float n = (float)max(0, r1 - r0);
+      const float m = n > 0.f ? sm / n : 0.f;
+      float q = 0.f;
+      for (int r = r0; r < r1; ++r) {
+        const float d = tl[r][c] - m;
+        q = fmaf(d, d, q);
+      }
+      gm[gi][c] = m;
+      g2[gi][c] = q;
+      if (c == 0) gn[gi] = n;
+    }
+    __syncthreads();
+    if (t < CO) {
+      float tn = 0.f, tm = 0.f, t2 = 0.f;
+      for (int k = 0; k < G; ++k) chan_merge(tn, tm, t2, gn[k], gm[k][t], g2[k][t]);
+      sink_put(sink, blockIdx.x, t, tn, tm, t2);
+      if (t == 0) sink.cnt[blockIdx.x] = tn;
+    }
+  }
 }
 
 // dgrad per 2x2 input quad (2Y+a, 2X+c): with pt = pl = 0, input row 2Y takes filter row 0 from
@@ -149,9 +187,13 @@ static void stem_dispatch(int Co, Args... args) {
 template <int CO>
 struct StemFwd {
   static void go(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                 hipStream_t s) {
+                 StatSink sink, hipStream_t s) {
     long total = (long)B * Ho * Wo;
-    hipLaunchKernelGGL((k_stem_fwd<CO>), dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo);
+    sink.P = cdiv(total, 256);
+    if (sink.part)
+      hipLaunchKernelGGL((k_stem_fwd<CO, true>), dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
+    else
+      hipLaunchKernelGGL((k_stem_fwd<CO, false>), dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
   }
 };
 template <int CO>
@@ -164,11 +206,12 @@ struct StemBwd {
   }
 };
 
-void launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                     int Co, int pt, int pl, hipStream_t s) {
+int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
+                    int Co, int pt, int pl, hipStream_t s, StatSink sink) {
   if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
-  stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, s);
+  stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, sink, s);
   PHX_LAUNCH_CHECK();
+  return cdiv((long)B * Ho * Wo, 256);
 }
 
 void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
@@ -241,13 +284,78 @@ __device__ __forceinline__ void gemm_load(GemmFrag<NT>& f, const InX& Ax, const 
                                : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-template <int NT, int WM, int MODE>
+// Column statistics of a block's C tile for the BN that consumes it (StatSink).  Lane (q, r) of a
+// wave holds rows 4q+j (j < 4) of column r in each of its 2 x NT accumulator tiles: a column's 32
+// wave rows sit in 8 registers of 4 lanes (r, r+16, r+32, r+48).  Two passes over the registers
+// (mean, then M2 about it) plus xor-shuffles give each wave (n, mean, M2) per column; the WM
+// waves that share columns are merged through LDS (Chan) and written as partial row blockIdx.x.
+template <int NT, int WM>
+__device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const float* __restrict__ bias,
+                                           int M, int N, int m_base, int n_base, int wave, int wm,
+                                           int wn, int lane, const StatSink& sink) {
+  __shared__ float2 wstat[4][16 * NT];
+  __shared__ float wcnt[4];
+  const int q = lane >> 4, r = lane & 15;
+  const float n = (float)max(0, min(32, M - m_base));
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = n_base + nt * 16 + r;
+    const float b = (bias && col < N) ? bias[col] : 0.f;
+    float s = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (m_base + mt * 16 + 4 * q + j < M) s += acc[mt][nt][j] + b;
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    const float mean = n > 0.f ? s / n : 0.f;
+    float m2 = 0.f;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (m_base + mt * 16 + 4 * q + j < M) {
+          const float d = acc[mt][nt][j] + b - mean;
+          m2 = fmaf(d, d, m2);
+        }
+    m2 += __shfl_xor(m2, 16);
+    m2 += __shfl_xor(m2, 32);
+    if (q == 0) wstat[wave][nt * 16 + r] = make_float2(mean, m2);
+  }
+  if (lane == 0) wcnt[wave] = n;
+  __syncthreads();
+  if (wm == 0) {
+    for (int cl = lane; cl < 16 * NT; cl += 64) {
+      const int col = n_base + cl;
+      if (col >= N) continue;
+      float tn = 0.f, tm = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        const int wv = wn * WM + w;
+        const float2 v = wstat[wv][cl];
+        chan_merge(tn, tm, t2, wcnt[wv], v.x, v.y);
+      }
+      sink_put(sink, blockIdx.x, col, tn, tm, t2);
+    }
+    if (wn == 0 && lane == 0) {
+      float tn = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) tn += wcnt[w];
+      sink.cnt[blockIdx.x] = tn;
+    }
+  }
+}
+
+// STATS: the BN batch statistics of C (bias included) are reduced in the epilogue into partial
+// row blockIdx.x of the StatSink (one (sum, M2) per column over the block's 32*WM rows).
+template <int NT, int WM, int MODE, bool STATS>
 __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __restrict__ Bt,
                                               const float* __restrict__ bias,
                                               float* __restrict__ C, int M, int N, int K,
                                               int acc_flag, const float* __restrict__ rowscale,
                                               int rows_per_img, int kslice,
-                                              float* __restrict__ partial) {
+                                              float* __restrict__ partial, StatSink sink) {
   constexpr int WN = 4 / WM;
   constexpr int LDW = 16 * NT + 4;  // LDS row pitch (floats) of a wave's staging tile
   __shared__ float stage[4][16 * LDW];
@@ -302,6 +410,8 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
     }
     if (more) cur = nxt;
   }
+
+  if constexpr (STATS) gemm_stats<NT, WM>(acc, bias, M, N, m_base, n_base, wave, wm, wn, lane, sink);
 
   // epilogue: accumulator element j of tile (mt,nt) is row 4q+j, col r.  Stage 16 rows at a
   // time through LDS and store row segments with 16-B lanes.
@@ -373,14 +483,81 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(const float* __restr
   C[i] = v;
 }
 
-template <int WM, int MODE>
-static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, InX A, GradX G, const float* Bt,
-                             const float* bias, float* C, int M, int N, int K, int accf,
-                             const float* rs, int rpi, int kslice, float* part) {
-#define PHX_G(NT_)                                                                          \
-  case NT_:                                                                                 \
-    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE>), g, dim3(256), 0, s, A, G, Bt, bias, C, M, N, K, \
-                       accf, rs, rpi, kslice, part);                                        \
+// split-K reduction with the BN column statistics of the result (forward GEMMs feeding a BN):
+// block b owns rows [b*RB, (b+1)*RB); lane t owns column quad t % N4 of every (256/N4)-th row,
+// keeps shifted sums (shift = its first value) and the block merges its lanes (Chan) into
+// partial row b of the StatSink.  N4 = N/4 <= 256.
+__global__ __launch_bounds__(256) void k_gemm_splitk_reduce_stats(const float* __restrict__ partial,
+                                                                  int S, int M, int N, int RB,
+                                                                  const float* __restrict__ bias,
+                                                                  float* __restrict__ C,
+                                                                  StatSink sink) {
+  __shared__ float4 sm[256], s2[256];
+  __shared__ float sn[256];
+  const int N4 = N >> 2, rpi = 256 / N4;
+  const int t = threadIdx.x, c4 = t % N4, rs = t / N4;
+  const int r0 = blockIdx.x * RB, r1 = min(M, r0 + RB);
+  const long MN = (long)M * N;
+  float n = 0.f;
+  float4 sh = make_float4(0.f, 0.f, 0.f, 0.f), a = sh, q = sh;
+  if (rs < rpi) {
+    const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + c4 * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int r = r0 + rs; r < r1; r += rpi) {
+      const long e = (long)r * N + c4 * 4;
+      float4 v = bv;
+      for (int k = 0; k < S; ++k) {
+        const float4 p = *reinterpret_cast<const float4*>(partial + k * MN + e);
+        v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+      }
+      *reinterpret_cast<float4*>(C + e) = v;
+      if (n == 0.f) sh = v;
+      const float4 d = make_float4(v.x - sh.x, v.y - sh.y, v.z - sh.z, v.w - sh.w);
+      a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
+      q.x = fmaf(d.x, d.x, q.x); q.y = fmaf(d.y, d.y, q.y); q.z = fmaf(d.z, d.z, q.z); q.w = fmaf(d.w, d.w, q.w);
+      n += 1.f;
+    }
+  }
+  // (n, mean, M2) of this lane
+  const float inv = n > 0.f ? 1.f / n : 0.f;
+  sm[t] = make_float4(sh.x + a.x * inv, sh.y + a.y * inv, sh.z + a.z * inv, sh.w + a.w * inv);
+  s2[t] = make_float4(q.x - a.x * a.x * inv, q.y - a.y * a.y * inv, q.z - a.z * a.z * inv, q.w - a.w * a.w * inv);
+  sn[t] = n;
+  __syncthreads();
+  if (rs == 0) {
+    float tn[4] = {0.f, 0.f, 0.f, 0.f}, tm[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < rpi; ++k) {
+      const int u = k * N4 + c4;
+      const float4 m = sm[u], v = s2[u];
+      chan_merge(tn[0], tm[0], t2[0], sn[u], m.x, fmaxf(v.x, 0.f));
+      chan_merge(tn[1], tm[1], t2[1], sn[u], m.y, fmaxf(v.y, 0.f));
+      chan_merge(tn[2], tm[2], t2[2], sn[u], m.z, fmaxf(v.z, 0.f));
+      chan_merge(tn[3], tm[3], t2[3], sn[u], m.w, fmaxf(v.w, 0.f));
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sink_put(sink, blockIdx.x, c4 * 4 + j, tn[j], tm[j], t2[j]);
+    if (c4 == 0) sink.cnt[blockIdx.x] = tn[0];
+  }
+}
+
+struct GemmCall {
+  InX A;
+  GradX G;
+  const float* Bt;
+  const float* bias;
+  float* C;
+  int M, N, K, accf;
+  const float* rs;
+  int rpi, kslice;
+  float* part;
+  StatSink sink;
+};
+
+template <int WM, int MODE, bool STATS>
+static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, const GemmCall& a) {
+#define PHX_G(NT_)                                                                                 \
+  case NT_:                                                                                        \
+    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE, STATS>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias, \
+                       a.C, a.M, a.N, a.K, a.accf, a.rs, a.rpi, a.kslice, a.part, a.sink);         \
     break;
   switch (nt) {
     PHX_G(1) PHX_G(2) PHX_G(3) PHX_G(4) PHX_G(5) PHX_G(6) PHX_G(7) PHX_G(8)
@@ -389,13 +566,11 @@ static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, InX A, GradX G, cons
 #undef PHX_G
 }
 
-template <int MODE>
-static void gemm_dispatch(int wm, int nt, dim3 g, hipStream_t s, InX A, GradX G, const float* Bt,
-                          const float* bias, float* C, int M, int N, int K, int accf,
-                          const float* rs, int rpi, int kslice, float* part) {
-  if (wm == 4) gemm_dispatch_nt<4, MODE>(nt, g, s, A, G, Bt, bias, C, M, N, K, accf, rs, rpi, kslice, part);
-  else if (wm == 2) gemm_dispatch_nt<2, MODE>(nt, g, s, A, G, Bt, bias, C, M, N, K, accf, rs, rpi, kslice, part);
-  else gemm_dispatch_nt<1, MODE>(nt, g, s, A, G, Bt, bias, C, M, N, K, accf, rs, rpi, kslice, part);
+template <int MODE, bool STATS>
+static void gemm_dispatch(int wm, int nt, dim3 g, hipStream_t s, const GemmCall& a) {
+  if (wm == 4) gemm_dispatch_nt<4, MODE, STATS>(nt, g, s, a);
+  else if (wm == 2) gemm_dispatch_nt<2, MODE, STATS>(nt, g, s, a);
+  else gemm_dispatch_nt<1, MODE, STATS>(nt, g, s, a);
 }
 
 GemmPlan plan_gemm(int M, int N, int K) {
@@ -431,45 +606,69 @@ size_t gemm_partial_floats(int M, int N, int K) {
   return p.splits > 1 ? (size_t)p.splits * M * N : 0;
 }
 
-static void gemm_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M,
-                     int N, int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-                     float* partial) {
+// rows per block of the split-K reduce-with-statistics kernel
+static int splitk_stats_rb(int M, int N) {
+  const int rpi = 256 / (N / 4);
+  return rpi * std::max(1, cdiv(M, (long)rpi * 256));
+}
+
+// 0: the statistics cannot be fused into this GEMM (split-K with N > 1024)
+int gemm_stat_partials(int M, int N, int K) {
+  GemmPlan p = plan_gemm(M, N, K);
+  if (p.splits > 1) return N <= 1024 ? cdiv(M, splitk_stats_rb(M, N)) : 0;
+  return p.gx;
+}
+
+static int gemm_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M,
+                    int N, int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+                    float* partial, StatSink sink) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
   GemmPlan p = plan_gemm(M, N, K);
   float* part = p.splits > 1 ? partial : nullptr;
   if (p.splits > 1 && !partial) throw std::runtime_error("gemm: split-K needs a partial buffer");
+  const bool stats = sink.part != nullptr;
+  if (stats && (acc || mode == 3 || (N & 3) || (p.splits > 1 && N > 1024)))
+    throw std::runtime_error("gemm: unsupported statistics epilogue");
+  const bool kstats = stats && p.splits == 1;
+  if (stats) sink.P = p.splits > 1 ? cdiv(M, splitk_stats_rb(M, N)) : p.gx;
   dim3 g(p.gx, p.gy, p.splits);
-  const int af = acc ? 1 : 0;
+  GemmCall a{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
+             p.kslice, part, sink};
   switch (mode) {
-    case 0: gemm_dispatch<0>(p.wm, p.nt, g, s, A, G, Bt, bias, C, M, N, K, af, nullptr, 1, p.kslice, part); break;
-    case 1: gemm_dispatch<1>(p.wm, p.nt, g, s, A, G, Bt, bias, C, M, N, K, af, nullptr, 1, p.kslice, part); break;
-    case 2: gemm_dispatch<2>(p.wm, p.nt, g, s, A, G, Bt, bias, C, M, N, K, af, rowscale, rows_per_img, p.kslice, part); break;
-    default: gemm_dispatch<3>(p.wm, p.nt, g, s, A, G, Bt, bias, C, M, N, K, af, nullptr, 1, p.kslice, part); break;
+    case 0: kstats ? gemm_dispatch<0, true>(p.wm, p.nt, g, s, a) : gemm_dispatch<0, false>(p.wm, p.nt, g, s, a); break;
+    case 1: kstats ? gemm_dispatch<1, true>(p.wm, p.nt, g, s, a) : gemm_dispatch<1, false>(p.wm, p.nt, g, s, a); break;
+    case 2: kstats ? gemm_dispatch<2, true>(p.wm, p.nt, g, s, a) : gemm_dispatch<2, false>(p.wm, p.nt, g, s, a); break;
+    default: gemm_dispatch<3, false>(p.wm, p.nt, g, s, a); break;
   }
   PHX_LAUNCH_CHECK();
   if (p.splits > 1) {
+    if (stats) {
+      const int rb = splitk_stats_rb(M, N);
+      hipLaunchKernelGGL(k_gemm_splitk_reduce_stats, dim3(cdiv(M, rb)), dim3(256), 0, s, partial,
+                         p.splits, M, N, rb, bias, C, sink);
+      PHX_LAUNCH_CHECK();
+      return cdiv(M, rb);
+    }
     long mn = (long)M * N;
     hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, p.splits, mn,
-                       N, bias, C, af);
+                       N, bias, C, a.accf);
     PHX_LAUNCH_CHECK();
   }
+  return p.gx;
 }
 
-void launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
-                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-                 float* partial) {
+int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
+                bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+                float* partial, StatSink sink) {
   if (rowscale && !A.mu) throw std::runtime_error("gemm: rowscale requires a BN view");
   const int mode = rowscale ? 2 : (A.mu ? 1 : 0);
-  gemm_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial);
+  return gemm_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink);
 }
 
 void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                        hipStream_t s, float* partial) {
   InX raw{A.da, nullptr, nullptr, nullptr, 0};
-  if (A.y)
-    gemm_run(3, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial);
-  else
-    gemm_run(0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial);
+  gemm_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{});
 }
 
 __global__ void k_transpose(const float* __restrict__ in, float* __restrict__ out, int rows,

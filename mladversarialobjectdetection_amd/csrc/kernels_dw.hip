@@ -163,10 +163,70 @@ __device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, in
   }
 }
 
+// Per-channel (sum, M2) of the RPT x 4 outputs a lane holds, reduced over the block's lanes of the
+// same channel group (xor-shuffles inside a wave, then the 4 waves through LDS) and written as
+// partial row p of the StatSink.  Two register passes (mean, then M2 about it).
+__device__ __forceinline__ float4 dw_xor_sum(float4 v, int lcg) {
+  for (int o = 1 << lcg; o < 64; o <<= 1) {
+    v.x += __shfl_xor(v.x, o);
+    v.y += __shfl_xor(v.y, o);
+    v.z += __shfl_xor(v.z, o);
+    v.w += __shfl_xor(v.w, o);
+  }
+  return v;
+}
+
+template <int RPT>
+__device__ __forceinline__ void dw_stats(const float4 (&acc)[RPT], unsigned vmask, int lcg, int c,
+                                         long p, const StatSink& sink) {
+  __shared__ float4 wm_[4][8], w2_[4][8];
+  __shared__ float wn_[4][8];
+  const int CG = 1 << lcg, cg = threadIdx.x & (CG - 1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float n = (float)__popc(vmask);
+  for (int o = CG; o < 64; o <<= 1) n += __shfl_xor(n, o);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r)
+    if (vmask >> r & 1) { s.x += acc[r].x; s.y += acc[r].y; s.z += acc[r].z; s.w += acc[r].w; }
+  s = dw_xor_sum(s, lcg);
+  const float inv = n > 0.f ? 1.f / n : 0.f;
+  const float4 m = make_float4(s.x * inv, s.y * inv, s.z * inv, s.w * inv);
+  float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r)
+    if (vmask >> r & 1) {
+      const float dx = acc[r].x - m.x, dy = acc[r].y - m.y, dz = acc[r].z - m.z, dw = acc[r].w - m.w;
+      q.x = fmaf(dx, dx, q.x); q.y = fmaf(dy, dy, q.y); q.z = fmaf(dz, dz, q.z); q.w = fmaf(dw, dw, q.w);
+    }
+  q = dw_xor_sum(q, lcg);
+  if (lane < CG) {
+    wm_[wave][cg] = m;
+    w2_[wave][cg] = q;
+    wn_[wave][cg] = n;
+  }
+  __syncthreads();
+  if (threadIdx.x < CG) {
+    float tn[4] = {0.f, 0.f, 0.f, 0.f}, tm[4] = {0.f, 0.f, 0.f, 0.f}, t2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float4 a = wm_[w][cg], b = w2_[w][cg];
+      const float nn = wn_[w][cg];
+      chan_merge(tn[0], tm[0], t2[0], nn, a.x, b.x);
+      chan_merge(tn[1], tm[1], t2[1], nn, a.y, b.y);
+      chan_merge(tn[2], tm[2], t2[2], nn, a.z, b.z);
+      chan_merge(tn[3], tm[3], t2[3], nn, a.w, b.w);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sink_put(sink, p, c + j, tn[j], tm[j], t2[j]);
+    if (threadIdx.x == 0) sink.cnt[p] = tn[0];
+  }
+}
+
 // ---- forward: y[oy][ox] = sum_ij a[oy*S - pt + i][ox*S - pl + j] * w[i][j] ----------------
-template <int K, int S, int RPT>
+template <int K, int S, int RPT, bool STATS>
 __global__ __launch_bounds__(256) void k_dw_fwd(InX xv, const float* __restrict__ w,
-                                                float* __restrict__ y, DwGeom g) {
+                                                float* __restrict__ y, DwGeom g, StatSink sink) {
   extern __shared__ float4 tile[];
   const int b = blockIdx.z;
   int tl, cgi;
@@ -188,31 +248,39 @@ __global__ __launch_bounds__(256) void k_dw_fwd(InX xv, const float* __restrict_
 
   const int ox = ox0 + col;
   const int row0 = rg * RPT;  // first local output row of this lane
-  if (rg >= g.nrg || ox >= g.Wo || oy0 + row0 >= g.Ho) return;
-  wr.init(wt, w, g.C, c, cg, g.lcg);
+  const bool active = rg < g.nrg && ox < g.Wo && oy0 + row0 < g.Ho;
+  if (!STATS && !active) return;
   float4 acc[RPT];
 #pragma unroll
   for (int r = 0; r < RPT; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-  constexpr int NR = (RPT - 1) * S + K;
-  const float4* base = tile + ((row0 * S) * g.cin + col * S) * CG + cg;
+  if (active) {
+    wr.init(wt, w, g.C, c, cg, g.lcg);
+    constexpr int NR = (RPT - 1) * S + K;
+    const float4* base = tile + ((row0 * S) * g.cin + col * S) * CG + cg;
 #pragma unroll
-  for (int ir = 0; ir < NR; ++ir) {
+    for (int ir = 0; ir < NR; ++ir) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const float4 v = base[(ir * g.cin + j) * CG];
+      for (int j = 0; j < K; ++j) {
+        const float4 v = base[(ir * g.cin + j) * CG];
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const int i = ir - r * S;
-        if (i >= 0 && i < K) fma4(acc[r], v, wr(i * K + j));
+        for (int r = 0; r < RPT; ++r) {
+          const int i = ir - r * S;
+          if (i >= 0 && i < K) fma4(acc[r], v, wr(i * K + j));
+        }
       }
+      if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);  // stream rows: bound live VGPRs
     }
-    if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);  // stream rows: bound live VGPRs
   }
+  unsigned vmask = 0;
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int oy = oy0 + row0 + r;
-    if (oy < g.Ho) *reinterpret_cast<float4*>(y + (((long)b * g.Ho + oy) * g.Wo + ox) * g.C + c) = acc[r];
+    if (active && oy < g.Ho) {
+      vmask |= 1u << r;
+      *reinterpret_cast<float4*>(y + (((long)b * g.Ho + oy) * g.Wo + ox) * g.C + c) = acc[r];
+    }
   }
+  if constexpr (STATS) dw_stats<RPT>(acc, vmask, g.lcg, c, (long)b * g.ntiles + tl, sink);
 }
 
 // ---- data gradient: dx[iy][ix] = sum over (i,j) with (iy+pt-i) and (ix+pl-j) divisible by S of
@@ -343,24 +411,36 @@ static size_t dw_lds(const DwGeom& g, int k) {
 }
 
 template <int K, int S>
-static void dw_fwd_go(InX x, const float* w, float* y, int B, const DwGeom& g, hipStream_t s) {
+static void dw_fwd_go(InX x, const float* w, float* y, int B, const DwGeom& g, StatSink sink,
+                      hipStream_t s) {
   constexpr int RPT = S == 1 ? 4 : 2;
+  sink.P = B * g.ntiles;
   dim3 grid(8 * g.per, 1, B);
-  hipLaunchKernelGGL((k_dw_fwd<K, S, RPT>), grid, dim3(256), dw_lds(g, K), s, x, w, y, g);
+  if (sink.part)
+    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true>), grid, dim3(256), dw_lds(g, K), s, x, w, y, g, sink);
+  else
+    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false>), grid, dim3(256), dw_lds(g, K), s, x, w, y, g, sink);
 }
 
-void launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho, int Wo,
-                   int k, int stride, int pt, int pl, hipStream_t s) {
+int dw_stat_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl) {
+  const int rpt = stride == 1 ? 4 : 2;
+  DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false);
+  return B * g.ntiles;
+}
+
+int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho, int Wo,
+                  int k, int stride, int pt, int pl, hipStream_t s, StatSink sink) {
   if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
   const int rpt = stride == 1 ? 4 : 2;
   DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false);
   if (dw_lds(g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  if (k == 3 && stride == 1) dw_fwd_go<3, 1>(x, w, y, B, g, s);
-  else if (k == 3 && stride == 2) dw_fwd_go<3, 2>(x, w, y, B, g, s);
-  else if (k == 5 && stride == 1) dw_fwd_go<5, 1>(x, w, y, B, g, s);
-  else if (k == 5 && stride == 2) dw_fwd_go<5, 2>(x, w, y, B, g, s);
+  if (k == 3 && stride == 1) dw_fwd_go<3, 1>(x, w, y, B, g, sink, s);
+  else if (k == 3 && stride == 2) dw_fwd_go<3, 2>(x, w, y, B, g, sink, s);
+  else if (k == 5 && stride == 1) dw_fwd_go<5, 1>(x, w, y, B, g, sink, s);
+  else if (k == 5 && stride == 2) dw_fwd_go<5, 2>(x, w, y, B, g, sink, s);
   else throw std::invalid_argument("dw: unsupported kernel/stride");
   PHX_LAUNCH_CHECK();
+  return B * g.ntiles;
 }
 
 template <int K, int S>

@@ -5,6 +5,8 @@
 // util_keras.py:29-66, eps 1e-3, momentum 0.99): y_hat = (y - mu_B) * rsqrt(var_B + eps), biased
 // batch variance over (N,H,W).  Reductions accumulate in fp64 so the statistics carry no
 // cancellation error at M ~ 1e6 rows.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -173,7 +175,7 @@ struct StatsEpi {
   float* mvar;
   float eps;
   __device__ void operator()(int, int c, double s0, double s1) const {
-    const double ref = y[c];
+    const double ref = y ? (double)y[c] : 0.0;
     const double dm = s0 / (double)M;            // mean - ref
     double var = s1 / (double)M - dm * dm;
     if (var < 0.0) var = 0.0;
@@ -198,6 +200,64 @@ void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, f
   StatsAcc f{y, C, {0, 0, 0, 0}};
   StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps};
   colred(f, e, M, C, 1, part, s);
+}
+
+// ---- BN statistics from producer partials (StatSink) ----------------------------------------
+// One workgroup per channel: its P partials are contiguous (channel-major), each lane folds a
+// strided subset into fp64 (S1 = sum x, S2 = sum x^2 rebuilt per partial as M2 + sum^2/n), the
+// 256 lane pairs meet in an LDS tree, and the StatsEpi epilogue (shift 0) finishes the channel.
+// Fixed summation order: the statistics are bit-reproducible run to run.
+__global__ __launch_bounds__(256) void k_bn_finalize(const float2* __restrict__ part,
+                                                     const float* __restrict__ cnt, int P,
+                                                     StatsEpi e) {
+  __shared__ double r1[256], r2[256];
+  const int c = blockIdx.x, t = threadIdx.x;
+  const float2* pc = part + (long)c * P;
+  double s1 = 0.0, s2 = 0.0;
+  int p = t;
+  for (; p + 768 < P; p += 1024) {
+    float2 v[4];
+    float n[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = pc[p + 256 * u];
+      n[u] = cnt[p + 256 * u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (n[u] > 0.f) {
+        s1 += (double)v[u].x;
+        s2 += (double)v[u].y + (double)v[u].x * (double)v[u].x / (double)n[u];
+      }
+  }
+  for (; p < P; p += 256) {
+    const float2 v = pc[p];
+    const float n = cnt[p];
+    if (n > 0.f) {
+      s1 += (double)v.x;
+      s2 += (double)v.y + (double)v.x * (double)v.x / (double)n;
+    }
+  }
+  r1[t] = s1;
+  r2[t] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      r1[t] += r1[t + o];
+      r2[t] += r2[t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) e(0, c, r1[0], r2[0]);
+}
+
+void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
+                        float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
+                        float eps, hipStream_t s) {
+  // StatsEpi's shift is 0 here: S1, S2 are plain sums of x and x^2 in fp64
+  StatsEpi e{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps};
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(256), 0, s, part, cnt, P, e);
+  PHX_LAUNCH_CHECK();
 }
 
 __global__ void k_bn_frozen_stats(const float* __restrict__ mm, const float* __restrict__ mv,
