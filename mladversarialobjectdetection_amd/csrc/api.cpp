@@ -61,6 +61,7 @@ struct Exec {
   float* scnt = nullptr;
   std::vector<char> fused_bn;
   std::vector<int> stat_P;                     // tensor id -> partial rows written by its producer
+  std::vector<uint8_t*> pool_amax;             // op id -> max-pool argmax taps (MAXPOOL ops)
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -79,6 +80,7 @@ struct Exec {
   int* nms2_count = nullptr;
   float *mraw = nullptr, *dm = nullptr;
   int *argm = nullptr, *nties = nullptr;
+  int* imax_scratch = nullptr;
   // EOT
   EotDims ed{};
   ImgParams* img = nullptr;
@@ -326,6 +328,9 @@ Exec& phx_ctx::exec_for(int B) {
   }
   E.spart = E.alloc<float2>(sp_need);
   E.scnt = E.alloc<float>(sc_need);
+  E.pool_amax.assign(P.ops.size(), nullptr);
+  for (size_t i = 0; i < P.ops.size(); ++i)
+    if (P.ops[i].t == OP_MAXPOOL) E.pool_amax[i] = E.alloc<uint8_t>(P.tensors[P.ops[i].out].numel());
   size_t gp_need = 1;
   for (const Op& op : P.ops) {
     if (op.t != OP_PW) continue;
@@ -385,6 +390,7 @@ Exec& phx_ctx::exec_for(int B) {
   E.dm = E.alloc<float>(B);
   E.argm = E.alloc<int>(B);
   E.nties = E.alloc<int>(B);
+  E.imax_scratch = E.alloc<int>(image_max_scratch_ints(B));
   // EOT
   const int S = mc.image_size;
   E.ed.B = B;
@@ -516,7 +522,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
                    (long)to.numel(), to.c, s);
         break;
       case OP_MAXPOOL:
-        launch_maxpool_fwd(view(ctx, E, op.in[0], input), y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
+        launch_maxpool_fwd(view(ctx, E, op.in[0], input), y, E.pool_amax[i], ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
                            op.pad_l, s);
         break;
       case OP_UPSAMPLE:
@@ -626,7 +632,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s);
         break;
       case OP_MAXPOOL:
-        launch_maxpool_bwd(view(ctx, E, op.in[0], input), dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w,
+        launch_maxpool_bwd(E.pool_amax[i], dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w,
                            op.k, op.stride, op.pad_t, op.pad_l, op.acc[0], s);
         break;
       case OP_UPSAMPLE:
@@ -953,7 +959,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s);
   run_pre_nms(ctx, E, s);
-  launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, s);
+  launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, grad, metrics, s);
   // 4. victim data-gradient -> d(patched images)
   run_backward(ctx, E, E.patched, s);

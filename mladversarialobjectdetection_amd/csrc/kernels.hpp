@@ -86,9 +86,11 @@ size_t se_scratch_doubles(int B, int C, int Cse);
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s);
 // dst (+)= src
 void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s);
-void launch_maxpool_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+// amax: per output element, the window tap (row-major) holding the maximum; the backward
+// routes each dy there (TF MaxPoolGrad)
+void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int C, int Ho, int Wo,
                         int k, int stride, int pt, int pl, hipStream_t s);
-void launch_maxpool_bwd(InX x, const float* dy, float* dx, int B, int H, int W, int C,
+void launch_maxpool_bwd(const uint8_t* amax, const float* dy, float* dx, int B, int H, int W, int C,
                         int Ho, int Wo, int k, int stride, int pt, int pl, bool acc,
                         hipStream_t s);
 void launch_upsample_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
@@ -126,5 +128,6 @@ void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* kee
                      int* out_count, float* work_score, int* work_sb, hipStream_t s);
 // per-image m_b = max(max_{keep} score, 0), tie count, and loss-gradient coefficient
 void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m,
-                      int* argmax, int* nties, hipStream_t s);
+                      int* argmax, int* nties, int* scratch, hipStream_t s);
+size_t image_max_scratch_ints(int B);
 }  // namespace phx

@@ -72,7 +72,17 @@ __global__ __launch_bounds__(256) void k_colred_part(F f, long seg_rows, int C, 
     long m = m0 + rr;
     while (m < m1) {
       float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-      for (int it = 0; it < 64 && m < m1; ++it, m += rpi) f.accum(base + m, c4, a0, a1);
+      // 64-row fp32 runs; rows are loaded 4 at a time before any is consumed so every lane keeps
+      // four 16-B loads (eight for two-operand functors) in flight
+      int it = 0;
+      for (; it + 4 <= 64 && m + 3 * rpi < m1; it += 4, m += 4 * rpi) {
+        typename F::Raw v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = f.load(base + m + u * rpi, c4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) f.add(v[u], a0, a1);
+      }
+      for (; it < 64 && m < m1; ++it, m += rpi) f.add(f.load(base + m, c4), a0, a1);
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         d0[j] += a0[j];
@@ -153,8 +163,9 @@ struct StatsAcc {
     float4 r = *reinterpret_cast<const float4*>(y + base * C + c4 * 4);
     ref[0] = r.x; ref[1] = r.y; ref[2] = r.z; ref[3] = r.w;
   }
-  __device__ void accum(long m, int c4, float* a0, float* a1) const {
-    float4 v = *reinterpret_cast<const float4*>(y + m * C + c4 * 4);
+  using Raw = float4;
+  __device__ Raw load(long m, int c4) const { return *reinterpret_cast<const float4*>(y + m * C + c4 * 4); }
+  __device__ void add(const Raw& v, float* a0, float* a1) const {
     float d[4] = {v.x - ref[0], v.y - ref[1], v.z - ref[2], v.w - ref[3]};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -326,11 +337,16 @@ struct BwdAcc {
       be[j] = beta[c4 * 4 + j];
     }
   }
-  __device__ void accum(long m, int c4, float* a0, float* a1) const {
-    float4 yv = *reinterpret_cast<const float4*>(y + m * C + c4 * 4);
-    float4 gv = *reinterpret_cast<const float4*>(da + m * C + c4 * 4);
-    float ys[4] = {yv.x, yv.y, yv.z, yv.w};
-    float gs[4] = {gv.x, gv.y, gv.z, gv.w};
+  struct Raw {
+    float4 y, g;
+  };
+  __device__ Raw load(long m, int c4) const {
+    return Raw{*reinterpret_cast<const float4*>(y + m * C + c4 * 4),
+               *reinterpret_cast<const float4*>(da + m * C + c4 * 4)};
+  }
+  __device__ void add(const Raw& r, float* a0, float* a1) const {
+    float ys[4] = {r.y.x, r.y.y, r.y.z, r.y.w};
+    float gs[4] = {r.g.x, r.g.y, r.g.z, r.g.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float xh = (ys[j] - mu[j]) * rs[j];
@@ -448,12 +464,20 @@ struct SumAcc {
   __device__ void init(int, int c4, long) {
     if (x.mu) ck = inx_chan4(x, c4 * 4);
   }
-  __device__ void accum(long m, int c4, float* a0, float* a1) const {
-    float4 v = *reinterpret_cast<const float4*>(x.p + m * C + c4 * 4);
+  struct Raw {
+    float4 v, w;
+  };
+  __device__ Raw load(long m, int c4) const {
+    Raw r;
+    r.v = *reinterpret_cast<const float4*>(x.p + m * C + c4 * 4);
+    if (g) r.w = *reinterpret_cast<const float4*>(g + m * C + c4 * 4);
+    return r;
+  }
+  __device__ void add(const Raw& r, float* a0, float* a1) const {
+    float4 v = r.v;
     if (x.mu) v = inx_apply4(x, ck, v);
     if (g) {
-      float4 w = *reinterpret_cast<const float4*>(g + m * C + c4 * 4);
-      v.x *= w.x; v.y *= w.y; v.z *= w.z; v.w *= w.w;
+      v.x *= r.w.x; v.y *= r.w.y; v.z *= r.w.z; v.w *= r.w.w;
     }
     a0[0] += v.x; a0[1] += v.y; a0[2] += v.z; a0[3] += v.w;
     (void)a1;
@@ -682,8 +706,11 @@ void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_
   PHX_LAUNCH_CHECK();
 }
 
-// max pool, TF SAME with -inf padding (efficientdet_keras.py:260-276)
-__global__ void k_maxpool_fwd(InX x, float* __restrict__ y, int B, int H,
+// max pool, TF SAME with -inf padding (efficientdet_keras.py:260-276).  The forward records, per
+// output element, which window tap held the maximum (first in row-major scan order, the element
+// TF's MaxPoolGrad routes the gradient to), so the backward is a gather of at most
+// ceil(k/s)^2 dy values per input element with no window re-scan.
+__global__ void k_maxpool_fwd(InX x, float* __restrict__ y, uint8_t* __restrict__ amax, int B, int H,
                               int W, int C, int Ho, int Wo, int k, int st, int pt, int pl) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long total = (long)B * Ho * Wo * C;
@@ -695,20 +722,25 @@ __global__ void k_maxpool_fwd(InX x, float* __restrict__ y, int B, int H,
   int oy = (int)(t % Ho);
   int b = (int)(t / Ho);
   float m = -INFINITY;
+  int am = 0;
   for (int i = 0; i < k; ++i) {
     int iy = oy * st - pt + i;
     if (iy < 0 || iy >= H) continue;
     for (int j = 0; j < k; ++j) {
       int ix = ox * st - pl + j;
       if (ix < 0 || ix >= W) continue;
-      m = fmaxf(m, inx_load1(x, (((long)b * H + iy) * W + ix) * C + c, c));
+      const float v = inx_load1(x, (((long)b * H + iy) * W + ix) * C + c, c);
+      if (v > m || am == 0 && m == -INFINITY) {
+        if (v > m) m = v;
+        am = i * k + j + 1;
+      }
     }
   }
   y[idx] = m;
+  amax[idx] = (uint8_t)(am - 1);
 }
 
-// gradient goes to the first maximum of each window in row-major scan order
-__global__ void k_maxpool_bwd(InX x, const float* __restrict__ dy,
+__global__ void k_maxpool_bwd(const uint8_t* __restrict__ amax, const float* __restrict__ dy,
                               float* __restrict__ dx, int B, int H, int W, int C, int Ho, int Wo,
                               int k, int st, int pt, int pl, int acc_flag) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -725,44 +757,32 @@ __global__ void k_maxpool_bwd(InX x, const float* __restrict__ dy,
   const int oyl = max(0, (iy + pt - k + st) / st), oyh = min(Ho - 1, (iy + pt) / st);
   const int oxl = max(0, (ix + pl - k + st) / st), oxh = min(Wo - 1, (ix + pl) / st);
   for (int oy = oyl; oy <= oyh; ++oy) {
-    int y0 = oy * st - pt;
-    if (iy < y0 || iy >= y0 + k) continue;
+    const int i = iy - (oy * st - pt);
+    if (i < 0 || i >= k) continue;
     for (int ox = oxl; ox <= oxh; ++ox) {
-      int x0 = ox * st - pl;
-      if (ix < x0 || ix >= x0 + k) continue;
-      // argmax of window (oy, ox)
-      float m = -INFINITY;
-      int ay = -1, ax = -1;
-      for (int i = 0; i < k; ++i) {
-        int yy = y0 + i;
-        if (yy < 0 || yy >= H) continue;
-        for (int j = 0; j < k; ++j) {
-          int xx = x0 + j;
-          if (xx < 0 || xx >= W) continue;
-          float v = inx_load1(x, (((long)b * H + yy) * W + xx) * C + c, c);
-          if (v > m) { m = v; ay = yy; ax = xx; }
-        }
-      }
-      if (ay == iy && ax == ix) g += dy[(((long)b * Ho + oy) * Wo + ox) * C + c];
+      const int j = ix - (ox * st - pl);
+      if (j < 0 || j >= k) continue;
+      const long o = (((long)b * Ho + oy) * Wo + ox) * C + c;
+      if (amax[o] == i * k + j) g += dy[o];
     }
   }
   if (acc_flag) g += dx[idx];
   dx[idx] = g;
 }
 
-void launch_maxpool_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
+void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int C, int Ho, int Wo,
                         int k, int stride, int pt, int pl, hipStream_t s) {
   long total = (long)B * Ho * Wo * C;
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho,
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, amax, B, H, W, C, Ho,
                      Wo, k, stride, pt, pl);
   PHX_LAUNCH_CHECK();
 }
 
-void launch_maxpool_bwd(InX x, const float* dy, float* dx, int B, int H, int W, int C,
+void launch_maxpool_bwd(const uint8_t* amax, const float* dy, float* dx, int B, int H, int W, int C,
                         int Ho, int Wo, int k, int stride, int pt, int pl, bool acc,
                         hipStream_t s) {
   long total = (long)B * H * W * C;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, dy, dx, B, H, W, C,
+  hipLaunchKernelGGL(k_maxpool_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, amax, dy, dx, B, H, W, C,
                      Ho, Wo, k, stride, pt, pl, acc ? 1 : 0);
   PHX_LAUNCH_CHECK();
 }

@@ -268,20 +268,29 @@ void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* kee
 // ------------------------------------------------------------------------------------------
 // per-image max over kept anchors (attacker.py:190): raw max (lowest() if empty) + ties
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_image_max(const float* __restrict__ scores,
-                                                   const uint8_t* __restrict__ keep, int A,
-                                                   float* __restrict__ m, int* __restrict__ argm,
-                                                   int* __restrict__ nties) {
-  const int b = blockIdx.x, t = threadIdx.x;
+// per-image max over kept anchors in two launches: grid (kImaxChunks, B) workgroups each reduce
+// a contiguous anchor chunk to (max, first index, #elements equal to the chunk max); one lane
+// per image then merges its chunks (ties across chunks: counts of chunks whose max equals the
+// image max add up; the first index is the smallest among them).
+constexpr int kImaxChunks = 48;
+
+__global__ __launch_bounds__(256) void k_image_max_part(const float* __restrict__ scores,
+                                                        const uint8_t* __restrict__ keep, int A,
+                                                        float* __restrict__ pm,
+                                                        int* __restrict__ pi,
+                                                        int* __restrict__ pc) {
+  const int b = blockIdx.y, ch = blockIdx.x, t = threadIdx.x;
+  const int per = (A + gridDim.x - 1) / gridDim.x;
+  const int a0 = ch * per, a1 = min(A, a0 + per);
   __shared__ float rs[256];
   __shared__ int ri[256];
   __shared__ int rc[256];
   float best = -FLT_MAX;
   int bi = 0x7fffffff;
-  for (int a = t; a < A; a += 256) {
-    long e = (long)b * A + a;
+  for (int a = a0 + t; a < a1; a += 256) {
+    const long e = (long)b * A + a;
     if (keep[e] & 1) {
-      float v = scores[e];
+      const float v = scores[e];
       if (v > best || (v == best && a < bi)) { best = v; bi = a; }
     }
   }
@@ -290,22 +299,21 @@ __global__ __launch_bounds__(256) void k_image_max(const float* __restrict__ sco
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
     if (t < off) {
-      float v = rs[t + off];
-      int j = ri[t + off];
+      const float v = rs[t + off];
+      const int j = ri[t + off];
       if (v > rs[t] || (v == rs[t] && j < ri[t])) { rs[t] = v; ri[t] = j; }
     }
     __syncthreads();
   }
   const float mx = rs[0];
   const int mi = ri[0];
-  __syncthreads();
   int cnt = 0;
-  if (mi != 0x7fffffff) {
-    for (int a = t; a < A; a += 256) {
-      long e = (long)b * A + a;
+  if (mi != 0x7fffffff)
+    for (int a = a0 + t; a < a1; a += 256) {
+      const long e = (long)b * A + a;
       if ((keep[e] & 1) && scores[e] == mx) ++cnt;
     }
-  }
+  __syncthreads();
   rc[t] = cnt;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
@@ -313,15 +321,48 @@ __global__ __launch_bounds__(256) void k_image_max(const float* __restrict__ sco
     __syncthreads();
   }
   if (t == 0) {
-    m[b] = mi == 0x7fffffff ? -FLT_MAX : mx;
-    argm[b] = mi == 0x7fffffff ? -1 : mi;
-    nties[b] = rc[0];
+    const int o = b * gridDim.x + ch;
+    pm[o] = mx;
+    pi[o] = mi;
+    pc[o] = rc[0];
   }
 }
 
+__global__ void k_image_max_merge(const float* __restrict__ pm, const int* __restrict__ pi,
+                                  const int* __restrict__ pc, int S, int B, float* __restrict__ m,
+                                  int* __restrict__ argm, int* __restrict__ nties) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  float mx = -FLT_MAX;
+  int mi = 0x7fffffff, cnt = 0;
+  for (int k = 0; k < S; ++k) {
+    const int o = b * S + k;
+    const int j = pi[o];
+    if (j == 0x7fffffff) continue;
+    const float v = pm[o];
+    if (mi == 0x7fffffff || v > mx) {
+      mx = v; mi = j; cnt = pc[o];
+    } else if (v == mx) {
+      mi = min(mi, j);
+      cnt += pc[o];
+    }
+  }
+  m[b] = mi == 0x7fffffff ? -FLT_MAX : mx;
+  argm[b] = mi == 0x7fffffff ? -1 : mi;
+  nties[b] = mi == 0x7fffffff ? 0 : cnt;
+}
+
+size_t image_max_scratch_ints(int B) { return (size_t)B * kImaxChunks * 3; }
+
 void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m, int* argmax,
-                      int* nties, hipStream_t s) {
-  hipLaunchKernelGGL(k_image_max, dim3(B), dim3(256), 0, s, scores, keep, A, m, argmax, nties);
+                      int* nties, int* scratch, hipStream_t s) {
+  float* pm = reinterpret_cast<float*>(scratch);
+  int* pi = scratch + (size_t)B * kImaxChunks;
+  int* pc = pi + (size_t)B * kImaxChunks;
+  hipLaunchKernelGGL(k_image_max_part, dim3(kImaxChunks, B), dim3(256), 0, s, scores, keep, A, pm, pi, pc);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_image_max_merge, dim3(cdiv(B, 64)), dim3(64), 0, s, pm, pi, pc, kImaxChunks, B, m,
+                     argmax, nties);
   PHX_LAUNCH_CHECK();
 }
 

@@ -25,3 +25,14 @@ for r in step:
     print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}us gap {gap / 1e3:6.1f} {grid:>14} vgpr {r['VGPR_Count']:>3} {name}")
 span = int(step[-1]["End_Timestamp"]) - t0
 print(f"step span {span / 1e6:.3f} ms, busy {busy / 1e6:.3f} ms, gaps {gap_total / 1e6:.3f} ms, {len(step)} dispatches")
+
+# per kernel family (template arguments kept) for the chosen step
+agg = {}
+for r in step:
+    name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("phx::", "")
+    a = agg.setdefault(name, [0, 0])
+    a[0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    a[1] += 1
+print("--- per kernel ---")
+for name, (ns, n) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+    print(f"{ns / 1e6:8.3f} ms {n:5d} x {ns / n / 1e3:8.1f} us  {name}")
