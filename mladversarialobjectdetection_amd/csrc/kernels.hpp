@@ -30,6 +30,23 @@ int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int 
                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
                 float* partial, StatSink sink = StatSink{});
 int gemm_stat_partials(int M, int N, int K);
+// the two GEMM implementations behind launch_gemm (gemm_impl(): PHX_GEMM env, default 2)
+struct Gemm2Plan {
+  int wm, tm, tn, mtiles, gx, gy, splits, kslice;
+};
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs);
+int gemm_impl();
+int gemm_impl_for(int N);
+int gemm2_target_wgs();
+int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
+              int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+              float* partial, StatSink sink);
+int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
+              int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+              float* partial, StatSink sink, int target_wgs);
+int gemm_splitk_stats_partials(int M, int N);
+int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
+                       bool acc, StatSink sink, hipStream_t s);
 // dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
 void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                        hipStream_t s, float* partial);

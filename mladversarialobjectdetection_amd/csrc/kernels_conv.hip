@@ -12,6 +12,7 @@
 #include "kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace phx {
 
@@ -603,7 +604,35 @@ GemmPlan plan_gemm(int M, int N, int K) {
 
 size_t gemm_partial_floats(int M, int N, int K) {
   GemmPlan p = plan_gemm(M, N, K);
-  return p.splits > 1 ? (size_t)p.splits * M * N : 0;
+  Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs());
+  const size_t a = p.splits > 1 ? (size_t)p.splits * M * N : 0;
+  const size_t b = q.splits > 1 ? (size_t)q.splits * M * N : 0;
+  return std::max(a, b);
+}
+
+// which GEMM implementation launch_gemm / launch_gemm_dgrad use: PHX_GEMM=1 (16x16x4 register
+// kernel) or 2 (LDS-tiled persistent 32x32x2 kernel, default); PHX_GEMM_WGS: persistent width
+static int gemm_impl_env() {
+  static int v = [] {
+    const char* e = getenv("PHX_GEMM");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+// default (0): the 32x32 LDS-tiled kernel except for 16-wide outputs, where its 32-column tile
+// would idle half the matrix core and the 16x16 register kernel streams faster (tools/gemm_bench)
+int gemm_impl_for(int N) {
+  const int e = gemm_impl_env();
+  if (e) return e;
+  return N <= 16 ? 1 : 2;
+}
+int gemm_impl() { return gemm_impl_env() ? gemm_impl_env() : 2; }
+int gemm2_target_wgs() {
+  static int v = [] {
+    const char* e = getenv("PHX_GEMM_WGS");
+    return e ? atoi(e) : 1024;
+  }();
+  return v;
 }
 
 // rows per block of the split-K reduce-with-statistics kernel
@@ -612,14 +641,40 @@ static int splitk_stats_rb(int M, int N) {
   return rpi * std::max(1, cdiv(M, (long)rpi * 256));
 }
 
+int gemm_splitk_stats_partials(int M, int N) { return cdiv(M, splitk_stats_rb(M, N)); }
+
 // 0: the statistics cannot be fused into this GEMM (split-K with N > 1024)
 int gemm_stat_partials(int M, int N, int K) {
+  if (gemm_impl_for(N) == 2) {
+    Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs());
+    if (q.splits > 1) return N <= 1024 ? gemm_splitk_stats_partials(M, N) : 0;
+    return q.gx;
+  }
   GemmPlan p = plan_gemm(M, N, K);
-  if (p.splits > 1) return N <= 1024 ? cdiv(M, splitk_stats_rb(M, N)) : 0;
+  if (p.splits > 1) return N <= 1024 ? gemm_splitk_stats_partials(M, N) : 0;
   return p.gx;
 }
 
-static int gemm_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M,
+// reduce the split-K partial slabs into C (+ bias, + C when acc); with a StatSink the BN column
+// statistics of the result come out of the same pass.  Returns the StatSink partial rows.
+int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
+                       bool acc, StatSink sink, hipStream_t s) {
+  if (sink.part) {
+    const int rb = splitk_stats_rb(M, N);
+    sink.P = cdiv(M, rb);
+    hipLaunchKernelGGL(k_gemm_splitk_reduce_stats, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
+                       M, N, rb, bias, C, sink);
+    PHX_LAUNCH_CHECK();
+    return sink.P;
+  }
+  long mn = (long)M * N;
+  hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
+                     bias, C, acc ? 1 : 0);
+  PHX_LAUNCH_CHECK();
+  return 0;
+}
+
+int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M,
                     int N, int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
                     float* partial, StatSink sink) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
@@ -662,13 +717,20 @@ int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int 
                 float* partial, StatSink sink) {
   if (rowscale && !A.mu) throw std::runtime_error("gemm: rowscale requires a BN view");
   const int mode = rowscale ? 2 : (A.mu ? 1 : 0);
-  return gemm_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink);
+  if (gemm_impl_for(N) == 2)
+    return gemm2_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink,
+                     gemm2_target_wgs());
+  return gemm1_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink);
 }
 
 void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                        hipStream_t s, float* partial) {
   InX raw{A.da, nullptr, nullptr, nullptr, 0};
-  gemm_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{});
+  if (gemm_impl_for(N) == 2)
+    gemm2_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{},
+              gemm2_target_wgs());
+  else
+    gemm1_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{});
 }
 
 __global__ void k_transpose(const float* __restrict__ in, float* __restrict__ out, int rows,

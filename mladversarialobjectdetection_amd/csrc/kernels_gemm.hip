@@ -1,0 +1,382 @@
+// kernels_gemm.hip — the 1x1-convolution GEMM of the victim forward and data-gradient on the
+// fp32 matrix cores (v_mfma_f32_32x32x2_f32, exact f32).
+//
+//   C[M,N] (+)= A'[M,K] * Bt[N,K]^T (+ bias)      A' = A through an InX view (BN + activation on
+//                                                 load), optionally x SE rowscale, or a GradX view
+//
+// Design (MI355X):
+//  * 256-thread workgroup = WM x WN waves, each wave owns TM x TN tiles of 32x32; block tile
+//    BM x BN = (32*WM*TM) x (32*WN*TN), K advanced in BK = 16 chunks through a double-buffered
+//    LDS image (row pitch BK+4 floats).  Operand fragments are ds_read_b128: lane l feeds
+//    k = 4*(l>>5) + s of its row/column at MFMA step s, so one 16-B read serves 4 MFMAs (the k
+//    order is permuted identically for A and B, so the products are unchanged).
+//  * Workgroups are persistent along M: the (m-tile, k-chunk) steps of all the tiles a workgroup
+//    owns form one software pipeline — the global loads of step s+1 are in flight while step s
+//    runs its MFMAs and (on a tile's last chunk) its epilogue, so streaming shapes (K <= 64,
+//    one chunk per tile) still overlap load, compute and store.
+//  * The A view (BN, activation, SE scale, BN backward) is applied once per element when the
+//    prefetched registers are written to LDS; a thread's channel quad is fixed within a chunk, so
+//    its per-channel parameters are three (six) float4 loads per chunk.
+//  * Epilogue straight from the accumulators: in the 32x32 C/D layout the 32 lanes of a half-wave
+//    hold 32 consecutive columns of one row, so every store instruction writes two 128-B row
+//    segments.  STATS: the consumer BN's batch statistics (StatSink) are reduced per tile in
+//    registers (two passes, xor-32 shuffle), merged across the WM waves in LDS and folded across
+//    the workgroup's tiles (Chan), one partial row per workgroup.
+//  * Split-K (blockIdx.z) writes fp32 partial slabs reduced by k_gemm_splitk_reduce(_stats).
+#include <algorithm>
+
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace phx {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct Gemm2Args {
+  InX A;
+  GradX G;
+  const float* Bt;
+  const float* bias;
+  float* C;
+  int M, N, K, acc;
+  const float* rowscale;
+  int rpi;
+  int kslice;
+  float* partial;
+  StatSink sink;
+  int mtiles;
+};
+
+template <int WM, int TM, int TN, int MODE>
+struct G2 {
+  static constexpr int WN = 4 / WM;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 16, LD = BK + 4;
+  static constexpr int NA = BM / 64;                  // A float4 per thread per chunk
+  static constexpr int NB = (BN * 4 + 255) / 256;     // B float4 per thread per chunk
+  static constexpr int LDS_FLOATS = 2 * (BM + BN) * LD;
+};
+
+template <int WM, int TM, int TN, int MODE>
+struct G2Regs {
+  using P = G2<WM, TM, TN, MODE>;
+  float4 a[P::NA];
+  float4 y[MODE == 3 ? P::NA : 1];
+  float4 rs[MODE == 2 ? P::NA : 1];
+  float4 b[P::NB];
+  Chan4 ck;
+  GChan4 gk;
+};
+
+template <int WM, int TM, int TN, int MODE>
+__device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE>& r, const Gemm2Args& a, int m0, int n0,
+                                        int k0, int kend) {
+  using P = G2<WM, TM, TN, MODE>;
+  const int t = threadIdx.x;
+  const int c4 = t & 3;
+  const int kk = k0 + 4 * c4;
+  const bool kok = kk < kend;
+  if (MODE == 1 || MODE == 2) {
+    if (kok) r.ck = inx_chan4(a.A, kk);
+  }
+  if (MODE == 3) {
+    if (kok) r.gk = gx_chan4(a.G, kk);
+  }
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) {
+    const int row = m0 + ((t + 256 * u) >> 2);
+    const bool ok = kok && row < a.M;
+    const long e = (long)row * a.K + kk;
+    if (MODE == 3) {
+      r.a[u] = ok ? *reinterpret_cast<const float4*>(a.G.da + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.y[u] = ok ? *reinterpret_cast<const float4*>(a.G.y + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {
+      r.a[u] = ok ? *reinterpret_cast<const float4*>(a.A.p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (MODE == 2)
+        r.rs[u] = ok ? *reinterpret_cast<const float4*>(a.rowscale + (long)(row / a.rpi) * a.K + kk)
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) {
+    const int idx = t + 256 * u;
+    const int col = n0 + (idx >> 2);
+    const int kb = k0 + 4 * (idx & 3);
+    const bool ok = idx < P::BN * 4 && col < a.N && kb < kend;
+    r.b[u] = ok ? *reinterpret_cast<const float4*>(a.Bt + (long)col * a.K + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int WM, int TM, int TN, int MODE>
+__device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE>& r, const Gemm2Args& a, float* sm,
+                                         int buf, int m0, int k0, int kend) {
+  using P = G2<WM, TM, TN, MODE>;
+  const int t = threadIdx.x;
+  const int c4 = t & 3;
+  const bool kok = k0 + 4 * c4 < kend;
+  float* As = sm + buf * (P::BM + P::BN) * P::LD;
+  float* Bs = As + P::BM * P::LD;
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) {
+    const int rl = (t + 256 * u) >> 2;
+    float4 v = r.a[u];
+    if (kok && m0 + rl < a.M) {
+      if (MODE == 1 || MODE == 2) v = inx_apply4(a.A, r.ck, v);
+      if (MODE == 2) {
+        v.x *= r.rs[u].x; v.y *= r.rs[u].y; v.z *= r.rs[u].z; v.w *= r.rs[u].w;
+      }
+      if (MODE == 3) v = gx_apply4(a.G, r.gk, v, r.y[u]);
+    } else {
+      v = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    *reinterpret_cast<float4*>(As + rl * P::LD + 4 * c4) = v;
+  }
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) {
+    const int idx = t + 256 * u;
+    if (idx < P::BN * 4) *reinterpret_cast<float4*>(Bs + (idx >> 2) * P::LD + 4 * (idx & 3)) = r.b[u];
+  }
+}
+
+template <int WM, int TM, int TN, int MODE, bool STATS>
+__global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
+  using P = G2<WM, TM, TN, MODE>;
+  constexpr int WN = P::WN, BM = P::BM, BN = P::BN, BK = P::BK, LD = P::LD;
+  __shared__ float sm[P::LDS_FLOATS];
+  __shared__ float2 wst[STATS ? 4 : 1][STATS ? TN * 32 : 1];
+  __shared__ float wcn[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int n0 = blockIdx.y * BN;
+  const int kbeg = blockIdx.z * a.kslice;
+  const int kend = min(a.K, kbeg + a.kslice);
+  const int ksteps = (kend - kbeg + BK - 1) / BK;
+  const bool split = a.partial != nullptr;
+  float* out = split ? a.partial + (long)blockIdx.z * a.M * a.N : a.C;
+
+  // running statistics of this workgroup's columns (wave wm == 0, lanes < 32)
+  float sn = 0.f, smean[TN], sm2[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) smean[j] = sm2[j] = 0.f;
+
+  int tile = blockIdx.x;
+  if (tile < a.mtiles && ksteps > 0) {
+    G2Regs<WM, TM, TN, MODE> rg;
+    g2_load<WM, TM, TN, MODE>(rg, a, tile * BM, n0, kbeg, kend);
+    g2_store<WM, TM, TN, MODE>(rg, a, sm, 0, tile * BM, kbeg, kend);
+    __syncthreads();
+    int buf = 0, kc = 0;
+    floatx16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    while (true) {
+      // next step of the pipeline: the following chunk of this tile, or the first of the next
+      int ntile = tile, nkc = kc + 1;
+      if (nkc == ksteps) {
+        ntile = tile + gridDim.x;
+        nkc = 0;
+      }
+      const bool have_next = ntile < a.mtiles;
+      if (have_next) g2_load<WM, TM, TN, MODE>(rg, a, ntile * BM, n0, kbeg + nkc * BK, kend);
+      // MFMAs on the staged chunk
+      {
+        const float* As = sm + buf * (BM + BN) * LD;
+        const float* Bs = As + BM * LD;
+#pragma unroll
+        for (int s8 = 0; s8 < BK / 8; ++s8) {
+          float4 fa[TM], fb[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            fa[i] = *reinterpret_cast<const float4*>(As + (wm * TM * 32 + i * 32 + r32) * LD + 8 * s8 + 4 * h);
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fb[j] = *reinterpret_cast<const float4*>(Bs + (wn * TN * 32 + j * 32 + r32) * LD + 8 * s8 + 4 * h);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
+            }
+        }
+      }
+      if (kc == ksteps - 1) {
+        // ---- epilogue of `tile` ----
+        const int mrow0 = tile * BM + wm * TM * 32;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = n0 + wn * TN * 32 + j * 32 + r32;
+          const bool cok = col < a.N;
+          const float bv = (!split && a.bias && cok) ? a.bias[col] : 0.f;
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+              const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+              float v = acc[i][j][e] + bv;
+              acc[i][j][e] = v;
+              if (cok && row < a.M) {
+                float* cp = out + (long)row * a.N + col;
+                if (!split && a.acc) v += *cp;
+                *cp = v;
+              }
+            }
+        }
+        if constexpr (STATS) {
+          // per-wave column statistics over its TM*32 rows, then merged across the WM waves
+          const float nw = (float)max(0, min(TM * 32, a.M - mrow0));
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) s += acc[i][j][e];
+            s += __shfl_xor(s, 32);
+            const float mean = nw > 0.f ? s / nw : 0.f;
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) {
+                  const float d = acc[i][j][e] - mean;
+                  q = fmaf(d, d, q);
+                }
+            q += __shfl_xor(q, 32);
+            if (h == 0) wst[wave][j * 32 + r32] = make_float2(mean, q);
+          }
+          if (lane == 0) wcn[wave] = nw;
+          __syncthreads();
+          if (wm == 0 && h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              float tn = 0.f, tm = 0.f, t2 = 0.f;
+#pragma unroll
+              for (int w = 0; w < WM; ++w) {
+                const int wv = wn * WM + w;
+                const float2 v = wst[wv][j * 32 + r32];
+                chan_merge(tn, tm, t2, wcn[wv], v.x, v.y);
+              }
+              float n_ = sn;
+              chan_merge(n_, smean[j], sm2[j], tn, tm, t2);
+            }
+            float tn = 0.f;
+#pragma unroll
+            for (int w = 0; w < WM; ++w) tn += wcn[wn * WM + w];
+            sn += tn;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      }
+      if (!have_next) break;
+      g2_store<WM, TM, TN, MODE>(rg, a, sm, buf ^ 1, ntile * BM, kbeg + nkc * BK, kend);
+      __syncthreads();
+      buf ^= 1;
+      tile = ntile;
+      kc = nkc;
+    }
+  }
+  if constexpr (STATS) {
+    if (wm == 0 && h == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 32 + j * 32 + r32;
+        if (col < a.N) sink_put(a.sink, blockIdx.x, col, sn, smean[j], sm2[j]);
+      }
+      if (blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[blockIdx.x] = sn;
+    }
+  }
+}
+
+// ---- host --------------------------------------------------------------------------------
+struct G2Cfg {
+  int wm, tm, tn;
+  int bm() const { return wm * tm * 32; }
+  int bn() const { return (4 / wm) * tn * 32; }
+};
+
+static G2Cfg g2_pick(int N) {
+  if (N <= 32) return {4, 1, 1};
+  if (N <= 64) return {4, 1, 2};
+  if (N <= 96) return {4, 1, 3};
+  if (N <= 128) return {2, 2, 2};
+  if (N <= 160) return {4, 1, 5};
+  return {2, 2, 2};
+}
+
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
+  Gemm2Plan p;
+  const G2Cfg c = g2_pick(N);
+  p.wm = c.wm; p.tm = c.tm; p.tn = c.tn;
+  p.mtiles = cdiv(M, c.bm());
+  p.gy = cdiv(N, c.bn());
+  const long tiles = (long)p.mtiles * p.gy;
+  p.splits = 1;
+  if (tiles < 256 && K >= 256) p.splits = std::max(1, std::min<int>((int)((512 + tiles - 1) / tiles), K / 128));
+  p.kslice = ((K + p.splits - 1) / p.splits + 15) / 16 * 16;
+  p.splits = (K + p.kslice - 1) / p.kslice;
+  const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
+  p.gx = (int)std::min<long>(p.mtiles, want);
+  return p;
+}
+
+template <int WM, int TM, int TN, int MODE>
+static void g2_launch_mode(bool stats, dim3 g, hipStream_t s, const Gemm2Args& a) {
+  if (stats)
+    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, true>), g, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, false>), g, dim3(256), 0, s, a);
+}
+
+template <int WM, int TM, int TN>
+static void g2_launch_cfg(int mode, bool stats, dim3 g, hipStream_t s, const Gemm2Args& a) {
+  switch (mode) {
+    case 0: g2_launch_mode<WM, TM, TN, 0>(stats, g, s, a); break;
+    case 1: g2_launch_mode<WM, TM, TN, 1>(stats, g, s, a); break;
+    case 2: g2_launch_mode<WM, TM, TN, 2>(stats, g, s, a); break;
+    default: g2_launch_mode<WM, TM, TN, 3>(false, g, s, a); break;
+  }
+}
+
+int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
+              int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
+              float* partial, StatSink sink, int target_wgs) {
+  if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
+  const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs);
+  const bool stats = sink.part != nullptr;
+  if (stats && (acc || mode == 3 || (N & 3) || (p.splits > 1 && N > 1024)))
+    throw std::runtime_error("gemm: unsupported statistics epilogue");
+  if (p.splits > 1 && !partial) throw std::runtime_error("gemm: split-K needs a partial buffer");
+  const bool kstats = stats && p.splits == 1;
+  if (stats) sink.P = p.splits > 1 ? gemm_splitk_stats_partials(M, N) : p.gx;
+  Gemm2Args a{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
+              p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles};
+  dim3 g(p.gx, p.gy, p.splits);
+  const int key = p.wm * 100 + p.tm * 10 + p.tn;
+  switch (key) {
+    case 411: g2_launch_cfg<4, 1, 1>(mode, kstats, g, s, a); break;
+    case 412: g2_launch_cfg<4, 1, 2>(mode, kstats, g, s, a); break;
+    case 413: g2_launch_cfg<4, 1, 3>(mode, kstats, g, s, a); break;
+    case 415: g2_launch_cfg<4, 1, 5>(mode, kstats, g, s, a); break;
+    case 222: g2_launch_cfg<2, 2, 2>(mode, kstats, g, s, a); break;
+    default: throw std::runtime_error("gemm2: no kernel for this configuration");
+  }
+  PHX_LAUNCH_CHECK();
+  if (p.splits > 1) return gemm_splitk_finish(partial, p.splits, M, N, bias, C, acc, sink, s);
+  return p.gx;
+}
+
+}  // namespace phx
