@@ -62,6 +62,10 @@ struct Exec {
   std::vector<char> fused_bn;
   std::vector<int> stat_P;                     // tensor id -> partial rows written by its producer
   std::vector<uint8_t*> pool_amax;             // op id -> max-pool argmax taps (MAXPOOL ops)
+  // BN backward sums fused into the dgrad of the BN output's first consumer (op i+1), which is the
+  // last writer of the BN output's gradient in the reverse sweep (GradSink)
+  std::vector<char> gfused_bn;
+  std::vector<int> gstat_P;                    // op id of the BN -> partial rows
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -324,6 +328,31 @@ Exec& phx_ctx::exec_for(int B) {
       E.fused_bn[i] = 1;
       sp_need = std::max(sp_need, (size_t)np * to.c);
       sc_need = std::max(sc_need, (size_t)np);
+    }
+  }
+  E.gfused_bn.assign(P.ops.size(), 0);
+  E.gstat_P.assign(P.ops.size(), 0);
+  if (bn_mode == PHX_BN_LOCAL) {
+    for (size_t i = 0; i + 1 < P.ops.size(); ++i) {
+      const Op& bn = P.ops[i];
+      const Op& L = P.ops[i + 1];
+      if (bn.t != OP_BN || !bn.bwd || !L.bwd) continue;
+      const Tensor& tz = P.tensors[bn.out];
+      int np = 0;
+      const Tensor& li = P.tensors[L.in[0]];
+      const Tensor& lo = P.tensors[L.out];
+      if (L.t == OP_DW && L.in[0] == bn.out)
+        np = dw_bwd_partials(li.n, li.h, li.w, li.c, lo.h, lo.w, L.k, L.stride, L.pad_t, L.pad_l);
+      else if (L.t == OP_SE && L.in[0] == bn.out)
+        np = ew_gstats_partials((long)li.h * li.w, li.c, li.n);
+      else if (L.t == OP_PW && L.in[0] == bn.out && std::find(P.cls_out.begin(), P.cls_out.end(), L.out) == P.cls_out.end())
+        np = gemm_dgrad_gsink_partials((int)li.rows(), li.c, lo.c);
+      else if (L.t == OP_ADD && (L.in[0] == bn.out || L.in[1] == bn.out) && L.in[0] != L.in[1])
+        np = ew_gstats_partials((long)tz.rows(), tz.c, 1);
+      if (np <= 0 || tz.c % 4) continue;
+      E.gfused_bn[i] = 1;
+      E.gstat_P[i] = np;
+      sp_need = std::max(sp_need, (size_t)np * tz.c);
     }
   }
   E.spart = E.alloc<float2>(sp_need);
@@ -593,7 +622,18 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       if (bi >= 0 && P.ops[bi].bwd) by += 4.0 * (double)to.numel();
       if (op.acc[0]) by += 4.0 * (double)ti.numel();
     }
+    // the BN right before this op takes its backward sums from this op's dgrad (GradSink)
+    GradSink gsk{};
+    int gsk_in = -1;  // which input's gradient carries them
+    if (i > 0 && E.gfused_bn[i - 1]) {
+      const Op& bn = P.ops[i - 1];
+      gsk = GradSink{E.spart, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input), E.slot_a[bn.slot],
+                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act};
+      gsk_in = op.in[0] == bn.out ? 0 : 1;
+    }
+    if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
     Scope scope(ctx, kind, fl, by, s);
+    int np = -1;
     switch (op.t) {
       case OP_STEM: {
         // the stem dgrad reads each dy element up to 4x: materialise the BN-backward output once
@@ -606,31 +646,38 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       }
       case OP_PW:
         // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
-        launch_gemm_dgrad(gview(ctx, E, op.out, input), W + op.w, dx, (int)ti.rows(), ti.c, to.c,
-                          op.acc[0], s, E.gpart);
+        np = launch_gemm_dgrad(gview(ctx, E, op.out, input), W + op.w, dx, (int)ti.rows(), ti.c, to.c,
+                               op.acc[0], s, E.gpart, gsk);
         break;
       case OP_DW:
-        launch_dw_bwd(gview(ctx, E, op.out, input), W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride,
-                      op.pad_t, op.pad_l, op.acc[0], s);
+        np = launch_dw_bwd(gview(ctx, E, op.out, input), W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k,
+                           op.stride, op.pad_t, op.pad_l, op.acc[0], s, gsk);
         break;
       case OP_BN:
         // reduction only; the apply half runs in the producer's dgrad (gview)
         if (op.acc[0]) throw std::runtime_error("BN input with several consumers");
-        if (!frozen)
+        if (!frozen && E.gfused_bn[i])
+          launch_bn_bwd_finalize(E.spart, E.gstat_P[i], (long)ti.rows(), ti.c, E.slot_d[op.slot],
+                                 E.slot_e[op.slot], s);
+        else if (!frozen)
           launch_bn_bwd_reduce(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
                                W + op.gamma, W + op.beta, (long)ti.rows(), ti.c, op.act, E.red,
                                E.slot_d[op.slot], E.slot_e[op.slot], s);
         (void)dx;
         break;
       case OP_SE:
-        launch_se_bwd(dy, view(ctx, E, op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
-                      W + op.b1, ctx->wt_of(op.w2), W + op.b2, op.act, E.slot_a[op.slot],
-                      E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s, E.red);
+        np = launch_se_bwd(dy, view(ctx, E, op.in[0], input), dx, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1,
+                           W + op.b1, ctx->wt_of(op.w2), W + op.b2, op.act, E.slot_a[op.slot],
+                           E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s, E.red, gsk);
         break;
-      case OP_ADD:
-        launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s);
-        launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s);
+      case OP_ADD: {
+        const int n0 = launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s, to.c,
+                                        gsk_in == 0 ? gsk : GradSink{});
+        const int n1 = launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s, to.c,
+                                        gsk_in == 1 ? gsk : GradSink{});
+        np = gsk_in == 0 ? n0 : n1;
         break;
+      }
       case OP_MAXPOOL:
         launch_maxpool_bwd(E.pool_amax[i], dy, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w,
                            op.k, op.stride, op.pad_t, op.pad_l, op.acc[0], s);
@@ -654,6 +701,8 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       }
     }
+    if (gsk.part && np != E.gstat_P[i - 1])
+      throw std::logic_error("BN backward sums: planned and launched partial counts differ");
   }
 }
 

@@ -182,6 +182,58 @@ __device__ __forceinline__ void sink_put(const StatSink& k, long p, int c, float
   k.part[(long)c * k.P + p] = make_float2(n * mean, m2);
 }
 
+// ------------------------------------------------------------------------------------------
+// GradSink: the reduction half of a training-mode BN backward, computed by the kernel that
+// finishes the gradient da of the BN OUTPUT (the last consumer's dgrad in the reverse sweep):
+//   dz = da * act'(z), z = (y - mu) * sc + be, xhat = (y - mu) * rstd;  sums of dz and dz*xhat.
+// Each workgroup stores its per-channel (sum dz, sum dz*xhat) as partial p at part[c*P + p];
+// k_bn_finalize<true> adds them in fp64 and writes mean(dz), mean(dz*xhat) (GradX's mdz, mdzx).
+// ------------------------------------------------------------------------------------------
+struct GradSink {
+  float2* part;  // [C][P]; nullptr = off
+  int C, P;
+  const float* y;     // BN input
+  const float* mu;
+  const float* rstd;
+  const float* sc;
+  const float* be;
+  int act;
+};
+
+struct GSChan4 {
+  float4 mu, rs, sc, be;
+};
+
+__device__ __forceinline__ GSChan4 gs_chan4(const GradSink& g, int c) {
+  GSChan4 k;
+  k.mu = *reinterpret_cast<const float4*>(g.mu + c);
+  k.rs = *reinterpret_cast<const float4*>(g.rstd + c);
+  k.sc = *reinterpret_cast<const float4*>(g.sc + c);
+  k.be = *reinterpret_cast<const float4*>(g.be + c);
+  return k;
+}
+
+__device__ __forceinline__ void gs_one(float da, float y, float mu, float rs, float sc, float be,
+                                       int act, float& s1, float& s2) {
+  const float yc = y - mu;
+  float dz = da;
+  if (act) dz *= act_grad(yc * sc + be, act);
+  s1 += dz;
+  s2 = fmaf(dz, yc * rs, s2);
+}
+
+__device__ __forceinline__ void gs_acc4(const GradSink& g, const GSChan4& k, float4 da, float4 y,
+                                        float4& s1, float4& s2) {
+  gs_one(da.x, y.x, k.mu.x, k.rs.x, k.sc.x, k.be.x, g.act, s1.x, s2.x);
+  gs_one(da.y, y.y, k.mu.y, k.rs.y, k.sc.y, k.be.y, g.act, s1.y, s2.y);
+  gs_one(da.z, y.z, k.mu.z, k.rs.z, k.sc.z, k.be.z, g.act, s1.z, s2.z);
+  gs_one(da.w, y.w, k.mu.w, k.rs.w, k.sc.w, k.be.w, g.act, s1.w, s2.w);
+}
+
+__device__ __forceinline__ void gsink_put(const GradSink& g, long p, int c, float s1, float s2) {
+  g.part[(long)c * g.P + p] = make_float2(s1, s2);
+}
+
 // (n, mean, M2) += (nb, mb, m2b)
 __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float mb,
                                            float m2b) {

@@ -40,23 +40,27 @@ int gemm_impl_for(int N);
 int gemm2_target_wgs();
 int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-              float* partial, StatSink sink);
+              float* partial, StatSink sink, GradSink gsk = GradSink{});
 int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-              float* partial, StatSink sink, int target_wgs);
+              float* partial, StatSink sink, int target_wgs, GradSink gsk = GradSink{});
 int gemm_splitk_stats_partials(int M, int N);
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
                        bool acc, StatSink sink, hipStream_t s);
 // dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
-void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
-                       hipStream_t s, float* partial);
+// with a GradSink, the BN-backward sums of the dgrad's result (returns the partial rows)
+int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
+                      hipStream_t s, float* partial, GradSink gs = GradSink{});
+int gemm_dgrad_gsink_partials(int M, int N, int K);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
 int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
                   int Wo, int k, int stride, int pt, int pl, hipStream_t s,
                   StatSink sink = StatSink{});
 int dw_stat_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl);
-void launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
-                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s);
+int launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
+                  int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s,
+                  GradSink gs = GradSink{});
+int dw_bwd_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl);
 void launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);
 
 // ---- normalisation / elementwise (kernels_norm.hip) ---------------------------------------
@@ -93,16 +97,22 @@ void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* 
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
                    float* hidden, float* scale, hipStream_t s, double* scratch);
 // w2t: the expand kernel transposed to [C][Cse]
-void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
-                   const float* w1, const float* b1, const float* w2t, const float* b2, int act,
-                   const float* pool, const float* hidden, const float* scale, float* gsum,
-                   bool acc, hipStream_t s, double* scratch);
+// returns the GradSink partial rows written (gs.part == nullptr: no BN-backward sums)
+int launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
+                  const float* w1, const float* b1, const float* w2t, const float* b2, int act,
+                  const float* pool, const float* hidden, const float* scale, float* gsum,
+                  bool acc, hipStream_t s, double* scratch, GradSink gs = GradSink{});
+int ew_gstats_partials(long seg_rows, int C, int nseg);
+// mdz = mean(dz), mdzx = mean(dz*xhat) from the P GradSink partials
+void launch_bn_bwd_finalize(const float2* part, int P, long M, int C, float* mdz, float* mdzx,
+                            hipStream_t s);
 size_t colred_scratch_doubles(long seg_rows, int C, int nseg);
 // squeeze partials of the SE MLP (they reuse the colred scratch)
 size_t se_scratch_doubles(int B, int C, int Cse);
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s);
-// dst (+)= src
-void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s);
+// dst (+)= src; with a GradSink (C channels) the BN-backward sums of the result come along
+int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s, int C = 4,
+                     GradSink gs = GradSink{});
 // amax: per output element, the window tap (row-major) holding the maximum; the backward
 // routes each dy there (TF MaxPoolGrad)
 void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int C, int Ho, int Wo,

@@ -348,15 +348,68 @@ __device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const fl
   }
 }
 
+// BN-backward sums (GradSink) of a dgrad block's output tile: value v (+ the accumulated C when
+// acc_flag) at rows 4q+j of column r per accumulator tile, the BN input y loaded at the same
+// element; xor-shuffles over q, then the WM waves sharing the columns meet in LDS.
+template <int NT, int WM>
+__device__ __forceinline__ void gemm_gsums(const floatx4 (&acc)[2][NT], const float* __restrict__ C,
+                                           int acc_flag, int M, int N, int m_base, int n_base, int wave,
+                                           int wm, int wn, int lane, const GradSink& g) {
+  __shared__ float2 wsum[4][16 * NT];
+  const int q = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt) {
+    const int col = n_base + nt * 16 + r;
+    float s1 = 0.f, s2 = 0.f;
+    if (col < N) {
+      const float mu = g.mu[col], rs = g.rstd[col], sc = g.sc[col], be = g.be[col];
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = m_base + mt * 16 + 4 * q + j;
+          if (row < M) {
+            const long e = (long)row * N + col;
+            float v = acc[mt][nt][j];
+            if (acc_flag) v += C[e];
+            gs_one(v, g.y[e], mu, rs, sc, be, g.act, s1, s2);
+          }
+        }
+    }
+    s1 += __shfl_xor(s1, 16);
+    s1 += __shfl_xor(s1, 32);
+    s2 += __shfl_xor(s2, 16);
+    s2 += __shfl_xor(s2, 32);
+    if (q == 0) wsum[wave][nt * 16 + r] = make_float2(s1, s2);
+  }
+  __syncthreads();
+  if (wm == 0) {
+    for (int cl = lane; cl < 16 * NT; cl += 64) {
+      const int col = n_base + cl;
+      if (col >= N) continue;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) {
+        const float2 v = wsum[wn * WM + w][cl];
+        t1 += v.x;
+        t2 += v.y;
+      }
+      gsink_put(g, blockIdx.x, col, t1, t2);
+    }
+  }
+}
+
 // STATS: the BN batch statistics of C (bias included) are reduced in the epilogue into partial
 // row blockIdx.x of the StatSink (one (sum, M2) per column over the block's 32*WM rows).
-template <int NT, int WM, int MODE, bool STATS>
+// SK: 0 plain, 1 StatSink (forward BN statistics), 2 GradSink (BN-backward sums of a dgrad)
+template <int NT, int WM, int MODE, int SK>
 __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __restrict__ Bt,
                                               const float* __restrict__ bias,
                                               float* __restrict__ C, int M, int N, int K,
                                               int acc_flag, const float* __restrict__ rowscale,
                                               int rows_per_img, int kslice,
-                                              float* __restrict__ partial, StatSink sink) {
+                                              float* __restrict__ partial, StatSink sink,
+                                              GradSink gsk) {
   constexpr int WN = 4 / WM;
   constexpr int LDW = 16 * NT + 4;  // LDS row pitch (floats) of a wave's staging tile
   __shared__ float stage[4][16 * LDW];
@@ -412,7 +465,8 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
     if (more) cur = nxt;
   }
 
-  if constexpr (STATS) gemm_stats<NT, WM>(acc, bias, M, N, m_base, n_base, wave, wm, wn, lane, sink);
+  if constexpr (SK == 1) gemm_stats<NT, WM>(acc, bias, M, N, m_base, n_base, wave, wm, wn, lane, sink);
+  if constexpr (SK == 2) gemm_gsums<NT, WM>(acc, C, acc_flag, M, N, m_base, n_base, wave, wm, wn, lane, gsk);
 
   // epilogue: accumulator element j of tile (mt,nt) is row 4q+j, col r.  Stage 16 rows at a
   // time through LDS and store row segments with 16-B lanes.
@@ -551,14 +605,15 @@ struct GemmCall {
   int rpi, kslice;
   float* part;
   StatSink sink;
+  GradSink gsk;
 };
 
-template <int WM, int MODE, bool STATS>
+template <int WM, int MODE, int SK>
 static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, const GemmCall& a) {
 #define PHX_G(NT_)                                                                                 \
   case NT_:                                                                                        \
-    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE, STATS>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias, \
-                       a.C, a.M, a.N, a.K, a.accf, a.rs, a.rpi, a.kslice, a.part, a.sink);         \
+    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE, SK>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias,    \
+                       a.C, a.M, a.N, a.K, a.accf, a.rs, a.rpi, a.kslice, a.part, a.sink, a.gsk);  \
     break;
   switch (nt) {
     PHX_G(1) PHX_G(2) PHX_G(3) PHX_G(4) PHX_G(5) PHX_G(6) PHX_G(7) PHX_G(8)
@@ -567,11 +622,11 @@ static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, const GemmCall& a) {
 #undef PHX_G
 }
 
-template <int MODE, bool STATS>
+template <int MODE, int SK>
 static void gemm_dispatch(int wm, int nt, dim3 g, hipStream_t s, const GemmCall& a) {
-  if (wm == 4) gemm_dispatch_nt<4, MODE, STATS>(nt, g, s, a);
-  else if (wm == 2) gemm_dispatch_nt<2, MODE, STATS>(nt, g, s, a);
-  else gemm_dispatch_nt<1, MODE, STATS>(nt, g, s, a);
+  if (wm == 4) gemm_dispatch_nt<4, MODE, SK>(nt, g, s, a);
+  else if (wm == 2) gemm_dispatch_nt<2, MODE, SK>(nt, g, s, a);
+  else gemm_dispatch_nt<1, MODE, SK>(nt, g, s, a);
 }
 
 GemmPlan plan_gemm(int M, int N, int K) {
@@ -674,9 +729,9 @@ int gemm_splitk_finish(const float* partial, int splits, int M, int N, const flo
   return 0;
 }
 
-int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M,
-                    int N, int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-                    float* partial, StatSink sink) {
+int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
+              int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s, float* partial,
+              StatSink sink, GradSink gsk) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
   GemmPlan p = plan_gemm(M, N, K);
   float* part = p.splits > 1 ? partial : nullptr;
@@ -686,14 +741,25 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
     throw std::runtime_error("gemm: unsupported statistics epilogue");
   const bool kstats = stats && p.splits == 1;
   if (stats) sink.P = p.splits > 1 ? cdiv(M, splitk_stats_rb(M, N)) : p.gx;
+  const bool gs = gsk.part != nullptr;
+  if (gs && p.splits > 1) throw std::runtime_error("gemm: GradSink with split-K");
+  gsk.P = p.gx;
   dim3 g(p.gx, p.gy, p.splits);
   GemmCall a{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
-             p.kslice, part, sink};
+             p.kslice, part, sink, gsk};
   switch (mode) {
-    case 0: kstats ? gemm_dispatch<0, true>(p.wm, p.nt, g, s, a) : gemm_dispatch<0, false>(p.wm, p.nt, g, s, a); break;
-    case 1: kstats ? gemm_dispatch<1, true>(p.wm, p.nt, g, s, a) : gemm_dispatch<1, false>(p.wm, p.nt, g, s, a); break;
-    case 2: kstats ? gemm_dispatch<2, true>(p.wm, p.nt, g, s, a) : gemm_dispatch<2, false>(p.wm, p.nt, g, s, a); break;
-    default: gemm_dispatch<3, false>(p.wm, p.nt, g, s, a); break;
+    case 0:
+      if (kstats) gemm_dispatch<0, 1>(p.wm, p.nt, g, s, a);
+      else if (gs) gemm_dispatch<0, 2>(p.wm, p.nt, g, s, a);
+      else gemm_dispatch<0, 0>(p.wm, p.nt, g, s, a);
+      break;
+    case 1: kstats ? gemm_dispatch<1, 1>(p.wm, p.nt, g, s, a) : gemm_dispatch<1, 0>(p.wm, p.nt, g, s, a); break;
+    case 2: kstats ? gemm_dispatch<2, 1>(p.wm, p.nt, g, s, a) : gemm_dispatch<2, 0>(p.wm, p.nt, g, s, a); break;
+    default: gs ? gemm_dispatch<3, 2>(p.wm, p.nt, g, s, a) : gemm_dispatch<3, 0>(p.wm, p.nt, g, s, a); break;
+  }
+  if (gs) {
+    PHX_LAUNCH_CHECK();
+    return p.gx;
   }
   PHX_LAUNCH_CHECK();
   if (p.splits > 1) {
@@ -719,18 +785,28 @@ int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int 
   const int mode = rowscale ? 2 : (A.mu ? 1 : 0);
   if (gemm_impl_for(N) == 2)
     return gemm2_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink,
-                     gemm2_target_wgs());
-  return gemm1_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink);
+                     gemm2_target_wgs(), GradSink{});
+  return gemm1_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink,
+                   GradSink{});
 }
 
-void launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
-                       hipStream_t s, float* partial) {
+// GradSink partial rows a dgrad GEMM of this shape writes (0: the sums cannot be fused: split-K)
+int gemm_dgrad_gsink_partials(int M, int N, int K) {
+  if (gemm_impl_for(N) == 2) {
+    Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs());
+    return q.splits > 1 ? 0 : q.gx;
+  }
+  GemmPlan p = plan_gemm(M, N, K);
+  return p.splits > 1 ? 0 : p.gx;
+}
+
+int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
+                      hipStream_t s, float* partial, GradSink gs) {
   InX raw{A.da, nullptr, nullptr, nullptr, 0};
   if (gemm_impl_for(N) == 2)
-    gemm2_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{},
-              gemm2_target_wgs());
-  else
-    gemm1_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{});
+    return gemm2_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{},
+                     gemm2_target_wgs(), gs);
+  return gemm1_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{}, gs);
 }
 
 __global__ void k_transpose(const float* __restrict__ in, float* __restrict__ out, int rows,

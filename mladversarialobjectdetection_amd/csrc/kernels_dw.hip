@@ -285,9 +285,38 @@ __global__ __launch_bounds__(256) void k_dw_fwd(InX xv, const float* __restrict_
 
 // ---- data gradient: dx[iy][ix] = sum over (i,j) with (iy+pt-i) and (ix+pl-j) divisible by S of
 //      dy[(iy+pt-i)/S][(ix+pl-j)/S] * w[i][j]  (the adjoint of the forward above) ---------------
-template <int K, int S, int RPT>
+// BN-backward sums (GradSink) of the RPT x 4 gradient values a lane wrote: plain sums, reduced
+// over the lanes of the channel group and the 4 waves like dw_stats.
+__device__ __forceinline__ void dw_gsums(float4 s1, float4 s2, int lcg, int c, long p, const GradSink& g) {
+  __shared__ float4 a_[4][8], b_[4][8];
+  const int CG = 1 << lcg, cg = threadIdx.x & (CG - 1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  s1 = dw_xor_sum(s1, lcg);
+  s2 = dw_xor_sum(s2, lcg);
+  if (lane < CG) {
+    a_[wave][cg] = s1;
+    b_[wave][cg] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < CG) {
+    float4 t1 = a_[0][cg], t2 = b_[0][cg];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const float4 u = a_[w][cg], v = b_[w][cg];
+      t1.x += u.x; t1.y += u.y; t1.z += u.z; t1.w += u.w;
+      t2.x += v.x; t2.y += v.y; t2.z += v.z; t2.w += v.w;
+    }
+    gsink_put(g, p, c + 0, t1.x, t2.x);
+    gsink_put(g, p, c + 1, t1.y, t2.y);
+    gsink_put(g, p, c + 2, t1.z, t2.z);
+    gsink_put(g, p, c + 3, t1.w, t2.w);
+  }
+}
+
+template <int K, int S, int RPT, bool GS>
 __global__ __launch_bounds__(256) void k_dw_bwd(GradX gv, const float* __restrict__ w,
-                                                float* __restrict__ dx, DwGeom g, int acc_flag) {
+                                                float* __restrict__ dx, DwGeom g, int acc_flag,
+                                                GradSink gsk) {
   extern __shared__ float4 tile[];
   const int b = blockIdx.z;
   int tl, cgi;
@@ -313,60 +342,69 @@ __global__ __launch_bounds__(256) void k_dw_bwd(GradX gv, const float* __restric
 
   const int ix = ix0 + col;
   const int row0 = rg * RPT;
-  if (rg >= g.nrg || ix >= g.W || iy0 + row0 >= g.H) return;
-  wr.init(wt, w, g.C, c, cg, g.lcg);
+  const bool active = rg < g.nrg && ix < g.W && iy0 + row0 < g.H;
+  if (!GS && !active) return;
   float4 acc[RPT];
 #pragma unroll
   for (int r = 0; r < RPT; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if constexpr (S == 1) {
-    // local dy row of (output row r, tap i) = row0 + r + (K-1-i): a sliding window as forward
-    constexpr int NR = RPT + K - 1;
-    const float4* base = tile + (row0 * g.cin + col) * CG + cg;
+  if (active) {
+    wr.init(wt, w, g.C, c, cg, g.lcg);
+    if constexpr (S == 1) {
+      // local dy row of (output row r, tap i) = row0 + r + (K-1-i): a sliding window as forward
+      constexpr int NR = RPT + K - 1;
+      const float4* base = tile + (row0 * g.cin + col) * CG + cg;
 #pragma unroll
-    for (int ir = 0; ir < NR; ++ir) {
+      for (int ir = 0; ir < NR; ++ir) {
 #pragma unroll
-      for (int jj = 0; jj < K; ++jj) {
-        const float4 v = base[(ir * g.cin + jj) * CG];
+        for (int jj = 0; jj < K; ++jj) {
+          const float4 v = base[(ir * g.cin + jj) * CG];
 #pragma unroll
-        for (int r = 0; r < RPT; ++r) {
-          const int ii = ir - r;  // = K-1-i
-          if (ii >= 0 && ii < K) fma4(acc[r], v, wr((K - 1 - ii) * K + (K - 1 - jj)));
+          for (int r = 0; r < RPT; ++r) {
+            const int ii = ir - r;  // = K-1-i
+            if (ii >= 0 && ii < K) fma4(acc[r], v, wr((K - 1 - ii) * K + (K - 1 - jj)));
+          }
         }
+        if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    const int u0 = ix + g.pl;  // column parity decides which taps land on a dy sample
+    } else {
+      const int u0 = ix + g.pl;  // column parity decides which taps land on a dy sample
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const int t0 = iy0 + row0 + r + g.pt;
+      for (int r = 0; r < RPT; ++r) {
+        const int t0 = iy0 + row0 + r + g.pt;
 #pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const int t = t0 - i;
-        if (t & 1) continue;
-        const int lr = (t >> 1) - oy_lo;
+        for (int i = 0; i < K; ++i) {
+          const int t = t0 - i;
+          if (t & 1) continue;
+          const int lr = (t >> 1) - oy_lo;
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const int u = u0 - j;
-          if (u & 1) continue;
-          const int lc = (u >> 1) - ox_lo;
-          fma4(acc[r], tile[(lr * g.cin + lc) * CG + cg], wr(i * K + j));
+          for (int j = 0; j < K; ++j) {
+            const int u = u0 - j;
+            if (u & 1) continue;
+            const int lc = (u >> 1) - ox_lo;
+            fma4(acc[r], tile[(lr * g.cin + lc) * CG + cg], wr(i * K + j));
+          }
         }
       }
     }
   }
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  GSChan4 kk;
+  if (GS && active) kk = gs_chan4(gsk, c);
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int iy = iy0 + row0 + r;
-    if (iy >= g.H) continue;
-    float4* o = reinterpret_cast<float4*>(dx + (((long)b * g.H + iy) * g.W + ix) * g.C + c);
+    if (!active || iy >= g.H) continue;
+    const long e = (((long)b * g.H + iy) * g.W + ix) * g.C + c;
+    float4* o = reinterpret_cast<float4*>(dx + e);
     float4 a = acc[r];
     if (acc_flag) {
       const float4 p = *o;
       a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
     }
     *o = a;
+    if constexpr (GS) gs_acc4(gsk, kk, a, *reinterpret_cast<const float4*>(gsk.y + e), s1, s2);
   }
+  if constexpr (GS) dw_gsums(s1, s2, g.lcg, c, (long)b * g.ntiles + tl, gsk);
 }
 
 // ---- host planning -------------------------------------------------------------------------
@@ -445,22 +483,32 @@ int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, i
 
 template <int K, int S>
 static void dw_bwd_go(GradX dy, const float* w, float* dx, int B, const DwGeom& g, bool acc,
-                      hipStream_t s) {
+                      GradSink gs, hipStream_t s) {
   dim3 grid(8 * g.per, 1, B);
-  hipLaunchKernelGGL((k_dw_bwd<K, S, 4>), grid, dim3(256), dw_lds(g, K), s, dy, w, dx, g, acc ? 1 : 0);
+  gs.P = B * g.ntiles;
+  if (gs.part)
+    hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true>), grid, dim3(256), dw_lds(g, K), s, dy, w, dx, g, acc ? 1 : 0, gs);
+  else
+    hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false>), grid, dim3(256), dw_lds(g, K), s, dy, w, dx, g, acc ? 1 : 0, gs);
 }
 
-void launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
-                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s) {
+int dw_bwd_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl) {
+  DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, true);
+  return B * g.ntiles;
+}
+
+int launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
+                  int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s, GradSink gs) {
   if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
   DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, true);
   if (dw_lds(g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  if (k == 3 && stride == 1) dw_bwd_go<3, 1>(dy, w, dx, B, g, acc, s);
-  else if (k == 3 && stride == 2) dw_bwd_go<3, 2>(dy, w, dx, B, g, acc, s);
-  else if (k == 5 && stride == 1) dw_bwd_go<5, 1>(dy, w, dx, B, g, acc, s);
-  else if (k == 5 && stride == 2) dw_bwd_go<5, 2>(dy, w, dx, B, g, acc, s);
+  if (k == 3 && stride == 1) dw_bwd_go<3, 1>(dy, w, dx, B, g, acc, gs, s);
+  else if (k == 3 && stride == 2) dw_bwd_go<3, 2>(dy, w, dx, B, g, acc, gs, s);
+  else if (k == 5 && stride == 1) dw_bwd_go<5, 1>(dy, w, dx, B, g, acc, gs, s);
+  else if (k == 5 && stride == 2) dw_bwd_go<5, 2>(dy, w, dx, B, g, acc, gs, s);
   else throw std::invalid_argument("dw: unsupported kernel/stride");
   PHX_LAUNCH_CHECK();
+  return B * g.ntiles;
 }
 
 }  // namespace phx

@@ -45,6 +45,7 @@ struct Gemm2Args {
   float* partial;
   StatSink sink;
   int mtiles;
+  GradSink gsk;
 };
 
 template <int WM, int TM, int TN, int MODE>
@@ -137,12 +138,14 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE>& r, cons
   }
 }
 
-template <int WM, int TM, int TN, int MODE, bool STATS>
+// SK: 0 plain, 1 StatSink (BN statistics of C), 2 GradSink (BN-backward sums of a dgrad's C)
+template <int WM, int TM, int TN, int MODE, int SK>
 __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
+  constexpr bool STATS = SK == 1;
   using P = G2<WM, TM, TN, MODE>;
   constexpr int WN = P::WN, BM = P::BM, BN = P::BN, BK = P::BK, LD = P::LD;
   __shared__ float sm[P::LDS_FLOATS];
-  __shared__ float2 wst[STATS ? 4 : 1][STATS ? TN * 32 : 1];
+  __shared__ float2 wst[SK ? 4 : 1][SK ? TN * 32 : 1];
   __shared__ float wcn[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -155,6 +158,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
   float* out = split ? a.partial + (long)blockIdx.z * a.M * a.N : a.C;
 
   // running statistics of this workgroup's columns (wave wm == 0, lanes < 32)
+  // (GradSink: smean = running sum dz, sm2 = running sum dz*xhat)
   float sn = 0.f, smean[TN], sm2[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) smean[j] = sm2[j] = 0.f;
@@ -225,6 +229,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
                 float* cp = out + (long)row * a.N + col;
                 if (!split && a.acc) v += *cp;
                 *cp = v;
+                if (SK == 2) acc[i][j][e] = v;
               }
             }
         }
@@ -274,6 +279,39 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
             sn += tn;
           }
         }
+        if constexpr (SK == 2) {
+          // BN-backward sums of the finished gradient tile (BN input y at the same elements)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * TN * 32 + j * 32 + r32;
+            float s1 = 0.f, s2 = 0.f;
+            if (col < a.N) {
+              const float mu = a.gsk.mu[col], rs = a.gsk.rstd[col], sc = a.gsk.sc[col], be = a.gsk.be[col];
+#pragma unroll
+              for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                  const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                  if (row < a.M)
+                    gs_one(acc[i][j][e], a.gsk.y[(long)row * a.N + col], mu, rs, sc, be, a.gsk.act, s1, s2);
+                }
+            }
+            s1 += __shfl_xor(s1, 32);
+            s2 += __shfl_xor(s2, 32);
+            if (h == 0) wst[wave][j * 32 + r32] = make_float2(s1, s2);
+          }
+          __syncthreads();
+          if (wm == 0 && h == 0) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+              for (int w = 0; w < WM; ++w) {
+                const float2 v = wst[wn * WM + w][j * 32 + r32];
+                smean[j] += v.x;
+                sm2[j] += v.y;
+              }
+          }
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -297,6 +335,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
         if (col < a.N) sink_put(a.sink, blockIdx.x, col, sn, smean[j], sm2[j]);
       }
       if (blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[blockIdx.x] = sn;
+    }
+  }
+  if constexpr (SK == 2) {
+    if (wm == 0 && h == 0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 32 + j * 32 + r32;
+        if (col < a.N) gsink_put(a.gsk, blockIdx.x, col, smean[j], sm2[j]);
+      }
     }
   }
 }
@@ -333,27 +380,29 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
   return p;
 }
 
-template <int WM, int TM, int TN, int MODE>
-static void g2_launch_mode(bool stats, dim3 g, hipStream_t s, const Gemm2Args& a) {
-  if (stats)
-    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, true>), g, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, false>), g, dim3(256), 0, s, a);
+template <int WM, int TM, int TN, int MODE, int SK>
+static void g2_go(dim3 g, hipStream_t s, const Gemm2Args& a) {
+  hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK>), g, dim3(256), 0, s, a);
 }
 
+// sk: 1 forward statistics (modes 0-2), 2 BN-backward sums (dgrad modes 0, 3)
 template <int WM, int TM, int TN>
-static void g2_launch_cfg(int mode, bool stats, dim3 g, hipStream_t s, const Gemm2Args& a) {
+static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a) {
   switch (mode) {
-    case 0: g2_launch_mode<WM, TM, TN, 0>(stats, g, s, a); break;
-    case 1: g2_launch_mode<WM, TM, TN, 1>(stats, g, s, a); break;
-    case 2: g2_launch_mode<WM, TM, TN, 2>(stats, g, s, a); break;
-    default: g2_launch_mode<WM, TM, TN, 3>(false, g, s, a); break;
+    case 0:
+      if (sk == 1) g2_go<WM, TM, TN, 0, 1>(g, s, a);
+      else if (sk == 2) g2_go<WM, TM, TN, 0, 2>(g, s, a);
+      else g2_go<WM, TM, TN, 0, 0>(g, s, a);
+      break;
+    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1>(g, s, a) : g2_go<WM, TM, TN, 1, 0>(g, s, a); break;
+    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1>(g, s, a) : g2_go<WM, TM, TN, 2, 0>(g, s, a); break;
+    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2>(g, s, a) : g2_go<WM, TM, TN, 3, 0>(g, s, a); break;
   }
 }
 
 int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-              float* partial, StatSink sink, int target_wgs) {
+              float* partial, StatSink sink, int target_wgs, GradSink gsk) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
   const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs);
   const bool stats = sink.part != nullptr;
@@ -362,16 +411,20 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   if (p.splits > 1 && !partial) throw std::runtime_error("gemm: split-K needs a partial buffer");
   const bool kstats = stats && p.splits == 1;
   if (stats) sink.P = p.splits > 1 ? gemm_splitk_stats_partials(M, N) : p.gx;
+  const bool gs = gsk.part != nullptr;
+  if (gs && (p.splits > 1 || mode == 1 || mode == 2)) throw std::runtime_error("gemm: unsupported GradSink");
+  gsk.P = p.gx;
+  const int sk = kstats ? 1 : gs ? 2 : 0;
   Gemm2Args a{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
-              p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles};
+              p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles, gsk};
   dim3 g(p.gx, p.gy, p.splits);
   const int key = p.wm * 100 + p.tm * 10 + p.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1>(mode, kstats, g, s, a); break;
-    case 412: g2_launch_cfg<4, 1, 2>(mode, kstats, g, s, a); break;
-    case 413: g2_launch_cfg<4, 1, 3>(mode, kstats, g, s, a); break;
-    case 415: g2_launch_cfg<4, 1, 5>(mode, kstats, g, s, a); break;
-    case 222: g2_launch_cfg<2, 2, 2>(mode, kstats, g, s, a); break;
+    case 411: g2_launch_cfg<4, 1, 1>(mode, sk, g, s, a); break;
+    case 412: g2_launch_cfg<4, 1, 2>(mode, sk, g, s, a); break;
+    case 413: g2_launch_cfg<4, 1, 3>(mode, sk, g, s, a); break;
+    case 415: g2_launch_cfg<4, 1, 5>(mode, sk, g, s, a); break;
+    case 222: g2_launch_cfg<2, 2, 2>(mode, sk, g, s, a); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();

@@ -154,6 +154,83 @@ static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hi
   PHX_LAUNCH_CHECK();
 }
 
+// ---- 2-D elementwise producers of a BN-output gradient, with the GradSink reduction ---------
+// Same [nseg][seg_rows][C] lane layout as the column reduction: a lane owns 4 channels of every
+// rpi-th row of its chunk, computes and stores the float4 result (functor F::out), and folds it
+// into the BN-backward sums of its channels; the rpi lanes of a channel quad meet in LDS and the
+// block writes partial (seg * chunks + chunk) of the GradSink.
+template <class F>
+__global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, long rpc,
+                                                   GradSink g) {
+  const int tpr_total = C >> 2;
+  const int g0 = blockIdx.y * 256;
+  const int tpr = min(tpr_total - g0, 256);
+  const int rpi = 256 / tpr;
+  const int t = threadIdx.x;
+  const int rr = t / tpr, cc = t % tpr;
+  const bool active = rr < rpi;
+  const int c4 = g0 + cc;
+  const int seg = blockIdx.z;
+  const long m0 = (long)blockIdx.x * rpc;
+  const long m1 = min(seg_rows, m0 + rpc);
+  const long base = (long)seg * seg_rows;
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  if (active) {
+    f.init(seg, c4);
+    GSChan4 k;
+    if (g.part) k = gs_chan4(g, c4 * 4);
+    long m = m0 + rr;
+    for (; m + 3 * rpi < m1; m += 4 * rpi) {
+      typename F::Raw v[4];
+      float4 yv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        v[u] = f.load(base + m + u * rpi, c4);
+        if (g.part) yv[u] = *reinterpret_cast<const float4*>(g.y + (base + m + u * rpi) * C + c4 * 4);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 o = f.out(v[u], base + m + u * rpi, c4);
+        if (g.part) gs_acc4(g, k, o, yv[u], s1, s2);
+      }
+    }
+    for (; m < m1; m += rpi) {
+      const float4 o = f.out(f.load(base + m, c4), base + m, c4);
+      if (g.part) gs_acc4(g, k, o, *reinterpret_cast<const float4*>(g.y + (base + m) * C + c4 * 4), s1, s2);
+    }
+  }
+  if (!g.part) return;
+  __shared__ float4 sh1[256], sh2[256];
+  sh1[t] = s1;
+  sh2[t] = s2;
+  __syncthreads();
+  if (rr == 0) {
+    for (int r = 1; r < rpi; ++r) {
+      const float4 a = sh1[r * tpr + cc], b = sh2[r * tpr + cc];
+      s1.x += a.x; s1.y += a.y; s1.z += a.z; s1.w += a.w;
+      s2.x += b.x; s2.y += b.y; s2.z += b.z; s2.w += b.w;
+    }
+    const long p = (long)seg * gridDim.x + blockIdx.x;
+    gsink_put(g, p, c4 * 4 + 0, s1.x, s2.x);
+    gsink_put(g, p, c4 * 4 + 1, s1.y, s2.y);
+    gsink_put(g, p, c4 * 4 + 2, s1.z, s2.z);
+    gsink_put(g, p, c4 * 4 + 3, s1.w, s2.w);
+  }
+}
+
+template <class F>
+static int ew_gstats(F f, long seg_rows, int C, int nseg, GradSink g, hipStream_t s) {
+  if (C % 4) throw std::runtime_error("ew_gstats: C % 4 != 0");
+  RedPlan p = red_plan(seg_rows, C, nseg);
+  g.P = nseg * p.chunks;
+  hipLaunchKernelGGL((k_ew_gstats<F>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows, C,
+                     p.rpc, g);
+  PHX_LAUNCH_CHECK();
+  return g.P;
+}
+
+int ew_gstats_partials(long seg_rows, int C, int nseg) { return nseg * red_plan(seg_rows, C, nseg).chunks; }
+
 // ---- BN forward statistics ------------------------------------------------------------------
 struct StatsAcc {
   const float* y;
@@ -213,18 +290,28 @@ void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, f
   colred(f, e, M, C, 1, part, s);
 }
 
-// ---- BN statistics from producer partials (StatSink) ----------------------------------------
+// ---- BN statistics from producer partials (StatSink / GradSink) ---------------------------
 // One workgroup per channel: its P partials are contiguous (channel-major), each lane folds a
-// strided subset into fp64 (S1 = sum x, S2 = sum x^2 rebuilt per partial as M2 + sum^2/n), the
-// 256 lane pairs meet in an LDS tree, and the StatsEpi epilogue (shift 0) finishes the channel.
-// Fixed summation order: the statistics are bit-reproducible run to run.
+// strided subset into fp64, the 256 lane pairs meet in an LDS tree and the epilogue finishes the
+// channel.  Forward (StatSink): partial = (sum, M2) of cnt[p] rows, folded as S1 = sum x and
+// S2 = sum x^2 = M2 + sum^2/n.  Backward (GradSink): partial = (sum dz, sum dz*xhat), plain sums.
+// Fixed summation order: bit-reproducible run to run.
+template <bool BWD, class E>
 __global__ __launch_bounds__(256) void k_bn_finalize(const float2* __restrict__ part,
-                                                     const float* __restrict__ cnt, int P,
-                                                     StatsEpi e) {
+                                                     const float* __restrict__ cnt, int P, E e) {
   __shared__ double r1[256], r2[256];
   const int c = blockIdx.x, t = threadIdx.x;
   const float2* pc = part + (long)c * P;
   double s1 = 0.0, s2 = 0.0;
+  auto fold = [&](float2 v, float n) {
+    if (BWD) {
+      s1 += (double)v.x;
+      s2 += (double)v.y;
+    } else if (n > 0.f) {
+      s1 += (double)v.x;
+      s2 += (double)v.y + (double)v.x * (double)v.x / (double)n;
+    }
+  };
   int p = t;
   for (; p + 768 < P; p += 1024) {
     float2 v[4];
@@ -232,23 +319,12 @@ __global__ __launch_bounds__(256) void k_bn_finalize(const float2* __restrict__ 
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       v[u] = pc[p + 256 * u];
-      n[u] = cnt[p + 256 * u];
+      n[u] = BWD ? 1.f : cnt[p + 256 * u];
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (n[u] > 0.f) {
-        s1 += (double)v[u].x;
-        s2 += (double)v[u].y + (double)v[u].x * (double)v[u].x / (double)n[u];
-      }
+    for (int u = 0; u < 4; ++u) fold(v[u], n[u]);
   }
-  for (; p < P; p += 256) {
-    const float2 v = pc[p];
-    const float n = cnt[p];
-    if (n > 0.f) {
-      s1 += (double)v.x;
-      s2 += (double)v.y + (double)v.x * (double)v.x / (double)n;
-    }
-  }
+  for (; p < P; p += 256) fold(pc[p], BWD ? 1.f : cnt[p]);
   r1[t] = s1;
   r2[t] = s2;
   __syncthreads();
@@ -267,7 +343,7 @@ void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int
                         float eps, hipStream_t s) {
   // StatsEpi's shift is 0 here: S1, S2 are plain sums of x and x^2 in fp64
   StatsEpi e{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps};
-  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(256), 0, s, part, cnt, P, e);
+  hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi>), dim3(C), dim3(256), 0, s, part, cnt, P, e);
   PHX_LAUNCH_CHECK();
 }
 
@@ -416,6 +492,13 @@ struct BwdEpi2 {
     mdzx[c] = (float)(s1 / (double)M);
   }
 };
+
+void launch_bn_bwd_finalize(const float2* part, int P, long M, int C, float* mdz, float* mdzx,
+                            hipStream_t s) {
+  hipLaunchKernelGGL((k_bn_finalize<true, BwdEpi2>), dim3(C), dim3(256), 0, s, part, nullptr, P,
+                     BwdEpi2{M, mdz, mdzx});
+  PHX_LAUNCH_CHECK();
+}
 
 __global__ __launch_bounds__(256) void k_gx_materialize(GradX g, float4* __restrict__ out, long n4,
                                                         int C) {
@@ -625,34 +708,38 @@ void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* 
   (void)y;  // the excitation is folded into the consuming GEMM's A load (rowscale)
 }
 
-__global__ __launch_bounds__(256) void k_se_bwd_apply(const float* __restrict__ dy,
-                                                      const float* __restrict__ scale,
-                                                      const float* __restrict__ dpool,
-                                                      float* __restrict__ dx, long n4, int HW,
-                                                      int C, int acc_flag) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n4) return;
-  long e = i * 4;
-  int c = (int)(e % C);
-  long b = e / ((long)HW * C);
-  float4 g = reinterpret_cast<const float4*>(dy)[i];
-  const float* sv = scale + b * C + c;
-  const float* dp = dpool + b * C + c;
-  const float inv = 1.0f / (float)HW;
-  float4 o = make_float4(g.x * sv[0] + dp[0] * inv, g.y * sv[1] + dp[1] * inv,
-                         g.z * sv[2] + dp[2] * inv, g.w * sv[3] + dp[3] * inv);
-  float4* op = reinterpret_cast<float4*>(dx) + i;
-  if (acc_flag) {
-    float4 p = *op;
-    o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+// dx = dy * scale[b,c] + dpool[b,c] / HW (+ dx)
+struct SeBwdApply {
+  const float* dy;
+  const float* scale;
+  const float* dpool;
+  float* dx;
+  int C, acc;
+  float inv;
+  float4 sc, dp;
+  using Raw = float4;
+  __device__ void init(int seg, int c4) {
+    sc = *reinterpret_cast<const float4*>(scale + (long)seg * C + c4 * 4);
+    const float4 d = *reinterpret_cast<const float4*>(dpool + (long)seg * C + c4 * 4);
+    dp = make_float4(d.x * inv, d.y * inv, d.z * inv, d.w * inv);
   }
-  *op = o;
-}
+  __device__ Raw load(long m, int c4) const { return *reinterpret_cast<const float4*>(dy + m * C + c4 * 4); }
+  __device__ float4 out(const Raw& g, long m, int c4) const {
+    float4 o = make_float4(fmaf(g.x, sc.x, dp.x), fmaf(g.y, sc.y, dp.y), fmaf(g.z, sc.z, dp.z), fmaf(g.w, sc.w, dp.w));
+    float4* op = reinterpret_cast<float4*>(dx + m * C + c4 * 4);
+    if (acc) {
+      const float4 p = *op;
+      o.x += p.x; o.y += p.y; o.z += p.z; o.w += p.w;
+    }
+    *op = o;
+    return o;
+  }
+};
 
-void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
-                   const float* w1, const float* b1, const float* w2t, const float* b2, int act,
-                   const float* pool, const float* hidden, const float* scale, float* gsum,
-                   bool acc, hipStream_t s, double* scratch) {
+int launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int Cse,
+                  const float* w1, const float* b1, const float* w2t, const float* b2, int act,
+                  const float* pool, const float* hidden, const float* scale, float* gsum,
+                  bool acc, hipStream_t s, double* scratch, GradSink gs) {
   (void)b1; (void)b2; (void)pool;
   float* sums = gsum + (long)B * C;  // gsum: [B*C dpool | B*C sum_hw dy*x]
   colred(SumAcc{x, dy, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
@@ -664,10 +751,7 @@ void launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int 
   hipLaunchKernelGGL(k_se_excite_bwd, dim3(cdiv(C, 256), B), dim3(256), Cse * sizeof(float), s, part, G,
                      C, Cse, w1, act, hidden, gsum);
   PHX_LAUNCH_CHECK();
-  long n4 = (long)B * HW * C / 4;
-  hipLaunchKernelGGL(k_se_bwd_apply, dim3(cdiv(n4, 256)), dim3(256), 0, s, dy, scale, gsum, dx, n4,
-                     HW, C, acc ? 1 : 0);
-  PHX_LAUNCH_CHECK();
+  return ew_gstats(SeBwdApply{dy, scale, gsum, dx, C, acc ? 1 : 0, 1.0f / (float)HW, {}, {}}, HW, C, B, gs, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -699,11 +783,33 @@ __global__ void k_copy_grad(const float4* __restrict__ src, float4* __restrict__
   dst[i] = v;
 }
 
-void launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s) {
+struct CopyGrad {
+  const float* src;
+  float* dst;
+  int C, acc;
+  using Raw = float4;
+  __device__ void init(int, int) {}
+  __device__ Raw load(long m, int c4) const { return *reinterpret_cast<const float4*>(src + m * C + c4 * 4); }
+  __device__ float4 out(const Raw& v0, long m, int c4) const {
+    float4 v = v0;
+    float4* op = reinterpret_cast<float4*>(dst + m * C + c4 * 4);
+    if (acc) {
+      const float4 p = *op;
+      v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+    }
+    *op = v;
+    return v;
+  }
+};
+
+int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s, int C,
+                     GradSink gs) {
+  if (gs.part) return ew_gstats(CopyGrad{src, dst, C, acc ? 1 : 0}, n / C, C, 1, gs, s);
   long n4 = n / 4;
   hipLaunchKernelGGL(k_copy_grad, dim3(cdiv(n4, 256)), dim3(256), 0, s, (const float4*)src,
                      (float4*)dst, n4, acc ? 1 : 0);
   PHX_LAUNCH_CHECK();
+  return 0;
 }
 
 // max pool, TF SAME with -inf padding (efficientdet_keras.py:260-276).  The forward records, per
