@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -99,6 +100,9 @@ struct Exec {
   int* err = nullptr;
   float* patched = nullptr;
   int16_t* owner = nullptr;
+  // caller-injected placement boxes ([B,100,4] slot layout + counts)
+  float* inj_boxes = nullptr;
+  int* inj_count = nullptr;
 
   size_t bytes = 0;  // device bytes owned by this executor
   template <typename T>
@@ -304,7 +308,6 @@ Exec& phx_ctx::exec_for(int B) {
       E.slot_c[op.slot] = E.alloc<float>((size_t)B * ti.c);
       seg_need = std::max(seg_need, (size_t)B * ti.c * 2);
       red_need = std::max(red_need, colred_scratch_doubles((long)ti.h * ti.w, ti.c, B));
-      red_need = std::max(red_need, se_scratch_doubles(B, ti.c, op.cse));
       E.se_of_tensor[op.out] = (int)i;
     }
   }
@@ -433,13 +436,15 @@ Exec& phx_ctx::exec_for(int B) {
   const long nslot = (long)B * PHX_MAX_OUT;
   E.img = E.alloc<ImgParams>(B);
   {
-    size_t bytes = nslot * sizeof(BoxPlace) + (4 + 2 * B + 2 * nslot + 1) * sizeof(int);
+    size_t bytes = nslot * sizeof(BoxPlace) + (4 + 2 * B + 3 * nslot + 2) * sizeof(int);
     E.place = reinterpret_cast<BoxPlace*>(E.alloc<char>(bytes));
   }
   E.spans = E.alloc<SpanEntry>(nslot * S);
   E.ysum = E.alloc<double>((size_t)B * 2 * 64);
   E.ymean = E.alloc<float>((size_t)B * 2);
-  E.rstore = E.alloc<float>(E.ed.rcap);
+  // the resized patches; reused by the resize adjoint's row buffer once the rotation backward
+  // has consumed them
+  E.rstore = E.alloc<float>(std::max(E.ed.rcap, eot_resize_scratch_floats(E.ed)));
   E.dstore = E.alloc<float>(E.ed.rcap);
   const size_t np = (size_t)PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3;
   E.matched = E.alloc<float>(np * B);
@@ -449,6 +454,8 @@ Exec& phx_ctx::exec_for(int B) {
   E.err = E.alloc<int>(1);
   E.patched = E.alloc<float>((size_t)B * S * S * 3);
   E.owner = E.alloc<int16_t>((size_t)B * S * S * 3);
+  E.inj_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
+  E.inj_count = E.alloc<int>(B);
   execs.push_back(std::move(ex));
   return *execs.back();
 }
@@ -724,6 +731,8 @@ void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc
                   0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s);
 }
 
+// run `fn(side)` on the executor's side stream after the work enqueued on `s` so far; join_side
+// makes `s` wait for it
 void check_ready(phx_ctx* ctx, int B) {
   if (!ctx->weights_loaded) throw std::logic_error("weights not loaded");
   if (B <= 0 || B > ctx->max_batch) throw std::out_of_range("batch exceeds max_batch");
@@ -941,15 +950,16 @@ void eot_forward(phx_ctx* ctx, Exec& E, const float* images, int B, const float*
   launch_eot_composite(d, images, E.place, E.rstore, E.patched, E.owner, s);
 }
 
-// copy caller boxes [B,maxb,4] into the [B,100,4] slot layout
+// copy caller boxes [B,maxb,4] into the [B,100,4] slot layout of the injected-box buffers
 void stage_boxes(Exec& E, const float* boxes, const int32_t* count, int B, int maxb,
                  hipStream_t s) {
   if (maxb > PHX_MAX_OUT) throw std::out_of_range("maxb > 100");
-  PHX_HIP(hipMemsetAsync(E.nms1_boxes, 0, (size_t)B * PHX_MAX_OUT * 16, s));
-  PHX_HIP(hipMemcpy2DAsync(E.nms1_boxes, PHX_MAX_OUT * 16, boxes, (size_t)maxb * 16,
+  if (maxb < PHX_MAX_OUT) PHX_HIP(hipMemsetAsync(E.inj_boxes, 0, (size_t)B * PHX_MAX_OUT * 16, s));
+  PHX_HIP(hipMemcpy2DAsync(E.inj_boxes, PHX_MAX_OUT * 16, boxes, (size_t)maxb * 16,
                            (size_t)maxb * 16, B, hipMemcpyDeviceToDevice, s));
-  PHX_HIP(hipMemcpyAsync(E.nms1_count, count, B * sizeof(int), hipMemcpyDeviceToDevice, s));
+  PHX_HIP(hipMemcpyAsync(E.inj_count, count, B * sizeof(int), hipMemcpyDeviceToDevice, s));
 }
+
 }  // namespace
 
 int phx_patch_images(phx_ctx* ctx, const float* images, int B, const float* boxes,
@@ -962,7 +972,7 @@ int phx_patch_images(phx_ctx* ctx, const float* images, int B, const float* boxe
   Exec& E = ctx->exec_for(B);
   ctx->last = &E;
   stage_boxes(E, boxes, count, B, maxb, s);
-  eot_forward(ctx, E, images, B, E.nms1_boxes, E.nms1_count, params, step, gimg0, s);
+  eot_forward(ctx, E, images, B, E.inj_boxes, E.inj_count, params, step, gimg0, s);
   const int S = ctx->mc.image_size;
   PHX_HIP(hipMemcpyAsync(out_images, E.patched, (size_t)B * S * S * 12, hipMemcpyDeviceToDevice, s));
   if (placements) {
@@ -996,14 +1006,18 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
   run_forward(ctx, E, images, s);
   run_pre_nms(ctx, E, s);
+  // (a second HIP stream for the NMS passes that only feed the ASR metric was measured: any
+  // multi-stream use slows the whole step by ~0.8 ms on this runtime, so everything stays on `s`)
   run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
   launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
-  if (boxes) {
+  const bool inject = boxes != nullptr;
+  if (inject) {
     if (!count) throw std::invalid_argument("boxes without count");
     stage_boxes(E, boxes, count, B, maxb, s);  // injected placement boxes
   }
   // 2. EOT paste
-  eot_forward(ctx, E, images, B, E.nms1_boxes, E.nms1_count, params, step, gimg0, s);
+  eot_forward(ctx, E, images, B, inject ? E.inj_boxes : E.nms1_boxes,
+              inject ? E.inj_count : E.nms1_count, params, step, gimg0, s);
   launch_eot_count(E.ed, E.place, metrics, s);
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s);
@@ -1021,7 +1035,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   const float* dimg = E.gptr(E.prog.input);
   Scope scope(ctx, "eot_bwd", 0.0, (double)B * (3.0 * PHX_NPATCH + 2.0 * d.H * d.W * 3) * 4.0, s);
   launch_eot_rot_bwd(d, dimg, E.owner, E.place, E.rstore, E.dstore, s);
-  launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.dmatched, s);
+  launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.rstore, E.dmatched, s);
   launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
   return PHX_OK;

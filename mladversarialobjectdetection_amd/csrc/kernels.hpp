@@ -107,8 +107,6 @@ int ew_gstats_partials(long seg_rows, int C, int nseg);
 void launch_bn_bwd_finalize(const float2* part, int P, long M, int C, float* mdz, float* mdzx,
                             hipStream_t s);
 size_t colred_scratch_doubles(long seg_rows, int C, int nseg);
-// squeeze partials of the SE MLP (they reuse the colred scratch)
-size_t se_scratch_doubles(int B, int C, int Cse);
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s);
 // dst (+)= src; with a GradSink (C channels) the BN-backward sums of the result come along
 int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s, int C = 4,

@@ -50,6 +50,9 @@ struct EotLists {
   int total_chunks;
 };
 
+// output rows per separable-resize work item (k_eot_resize, k_eot_resize_bwd_rows)
+constexpr int kResizeRT = 4;
+
 __global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __restrict__ boxes,
                                                    const int* __restrict__ count,
                                                    const float* __restrict__ params,
@@ -132,51 +135,59 @@ __global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __res
   int* img_first = img_n + d.B;        // [B]  index into vlist of the image's first box
   int* vlist = img_first + d.B;        // [B*maxb] slot ids
   int* cprefix = vlist + nslot;        // [B*maxb+1] chunk prefix over vlist
+  int* tprefix = cprefix + nslot + 1;  // [B*maxb+1] resize row-tile prefix over vlist
   __shared__ long s_need[256];
-  __shared__ int s_ch[256], s_v[256];
+  __shared__ int s_ch[256], s_v[256], s_tl[256];
   __shared__ long run_off;
-  __shared__ int run_ch, run_v;
-  if (t == 0) { run_off = 0; run_ch = 0; run_v = 0; }
+  __shared__ int run_ch, run_v, run_tl;
+  if (t == 0) { run_off = 0; run_ch = 0; run_v = 0; run_tl = 0; }
   __syncthreads();
   for (int base = 0; base < nslot; base += 256) {
     const int sl = base + t;
     long need = 0;
-    int ch = 0, v = 0;
+    int ch = 0, v = 0, tl = 0;
     if (sl < nslot && place[sl].valid) {
       const int ps = place[sl].ps;
       need = (long)ps * ps * 3;
       ch = (ps * ps + 255) / 256;
+      tl = (ps + kResizeRT - 1) / kResizeRT;
       v = 1;
     }
-    s_need[t] = need; s_ch[t] = ch; s_v[t] = v;
+    s_need[t] = need; s_ch[t] = ch; s_v[t] = v; s_tl[t] = tl;
     __syncthreads();
     for (int off = 1; off < 256; off <<= 1) {
       long a1 = t >= off ? s_need[t - off] : 0;
       int a2 = t >= off ? s_ch[t - off] : 0;
       int a3 = t >= off ? s_v[t - off] : 0;
+      int a4 = t >= off ? s_tl[t - off] : 0;
       __syncthreads();
-      s_need[t] += a1; s_ch[t] += a2; s_v[t] += a3;
+      s_need[t] += a1; s_ch[t] += a2; s_v[t] += a3; s_tl[t] += a4;
       __syncthreads();
     }
     if (sl < nslot) {
       const long ex_off = run_off + s_need[t] - need;
       const int ex_ch = run_ch + s_ch[t] - ch;
       const int ex_v = run_v + s_v[t] - v;
+      const int ex_tl = run_tl + s_tl[t] - tl;
       if (sl % d.maxb == 0) img_first[sl / d.maxb] = ex_v;
       if (v) {
         place[sl].roff = ex_off;
         vlist[ex_v] = sl;
         cprefix[ex_v] = ex_ch;
+        tprefix[ex_v] = ex_tl;
       }
     }
     __syncthreads();
-    if (t == 255) { run_off += s_need[255]; run_ch += s_ch[255]; run_v += s_v[255]; }
+    if (t == 255) {
+      run_off += s_need[255]; run_ch += s_ch[255]; run_v += s_v[255]; run_tl += s_tl[255];
+    }
     __syncthreads();
   }
   if (t == 0) {
     *nvalid = run_v;
     *total_chunks = run_ch;
     cprefix[run_v] = run_ch;
+    tprefix[run_v] = run_tl;
     if (err) *err = 0;
   }
   __syncthreads();
@@ -363,6 +374,7 @@ struct ListView {
   const int* img_first;
   const int* vlist;
   const int* cprefix;
+  const int* tprefix;  // resize row tiles (kResizeRT rows) per valid box, prefix over vlist
 };
 
 __device__ __forceinline__ ListView lists_of(const EotDims& d, const BoxPlace* place) {
@@ -374,6 +386,7 @@ __device__ __forceinline__ ListView lists_of(const EotDims& d, const BoxPlace* p
   v.img_first = v.img_n + d.B;
   v.vlist = v.img_first + d.B;
   v.cprefix = v.vlist + d.B * d.maxb;
+  v.tprefix = v.cprefix + d.B * d.maxb + 1;
   return v;
 }
 
@@ -389,56 +402,77 @@ __device__ __forceinline__ int find_box(const int* cprefix, int nv, int item) {
 
 constexpr int kBoxGrid = 2048;
 
-// resize (+noise +brightness): R_pre[i,j,c] = sum_y Wr[i,y] sum_x Wc[j,x] m[y,x,c] + n + delta
+// resize (+noise +brightness): R_pre[i,j,c] = sum_x Wc[j,x] sum_y Wr[i,y] m[y,x,c] + n + delta.
+// Separable, vertical pass first: a work item is (valid box, kResizeRT output rows).  Its lanes
+// run along x, so the vertical taps read whole NHWC rows of `matched` (coalesced); the
+// kResizeRT x nx x 3 intermediate stays in LDS for the horizontal pass.
+constexpr int kResizeGrid = 1280;  // 5 workgroups per CU (30 KB of LDS each)
+
 __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __restrict__ matched,
                                                     const BoxPlace* __restrict__ place,
                                                     const SpanEntry* __restrict__ spans,
                                                     uint64_t seed, int64_t step, int gimg0,
                                                     float* __restrict__ rstore) {
+  extern __shared__ float V[];  // [kResizeRT][nx][3]
   const ListView L = lists_of(d, place);
-  const int nv = *L.nvalid, total = *L.total_chunks;
+  const int nv = *L.nvalid, total = L.tprefix[nv];
   for (int item = blockIdx.x; item < total; item += gridDim.x) {
-    const int v = find_box(L.cprefix, nv, item);
+    const int v = find_box(L.tprefix, nv, item);
     const int sl = L.vlist[v];
     const BoxPlace P = place[sl];
     const int b = sl / d.maxb, k = sl % d.maxb;
-    const int px = (item - L.cprefix[v]) * 256 + threadIdx.x;
-    if (px >= P.ps * P.ps) continue;
-    const int i = px / P.ps, j = px % P.ps;
-    const SpanEntry si = spans[(long)sl * d.span_stride + i];
-    const SpanEntry sj = spans[(long)sl * d.span_stride + j];
+    const int i0 = (item - L.tprefix[v]) * kResizeRT;
+    const int ni = min(kResizeRT, P.ps - i0);
+    const SpanEntry* sp = spans + (long)sl * d.span_stride;
     const float scale = (float)P.ps / (float)d.P;
     const float inv_scale = (float)(1.0 / (double)scale);
     const float one_over_k = 1.0f / fmaxf(inv_scale, 1.0f);
+    const int xlo = sp[0].start, nx = sp[P.ps - 1].end - xlo;
     const float* m = matched + (long)b * d.P * d.P * 3;
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-    for (int y = si.start; y < si.end; ++y) {
-      const float wy = span_weight(si, y, one_over_k);
-      float c0 = 0.f, c1 = 0.f, c2 = 0.f;
-      const float* row = m + (long)y * d.P * 3;
+    for (int e = threadIdx.x; e < ni * nx; e += blockDim.x) {
+      const int ii = e / nx, xo = e - ii * nx;
+      const SpanEntry si = sp[i0 + ii];
+      const float* col = m + (long)(xlo + xo) * 3;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      for (int y = si.start; y < si.end; ++y) {
+        const float wy = span_weight(si, y, one_over_k);
+        const float* q = col + (long)y * d.P * 3;
+        a0 += wy * q[0];
+        a1 += wy * q[1];
+        a2 += wy * q[2];
+      }
+      float* o = V + e * 3;
+      o[0] = a0; o[1] = a1; o[2] = a2;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < ni * P.ps; e += blockDim.x) {
+      const int ii = e / P.ps, j = e - ii * P.ps;
+      const SpanEntry sj = sp[j];
+      const float* row = V + (ii * nx - xlo) * 3;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
       for (int x = sj.start; x < sj.end; ++x) {
         const float wx = span_weight(sj, x, one_over_k);
-        c0 += wx * row[x * 3 + 0];
-        c1 += wx * row[x * 3 + 1];
-        c2 += wx * row[x * 3 + 2];
+        a0 += wx * row[x * 3 + 0];
+        a1 += wx * row[x * 3 + 1];
+        a2 += wx * row[x * 3 + 2];
       }
-      a0 += wy * c0;
-      a1 += wy * c1;
-      a2 += wy * c2;
+      const int px = (i0 + ii) * P.ps + j;
+      u32x4 r = rng(seed, (uint32_t)px, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_NOISE);
+      float* o = rstore + P.roff + (long)px * 3;
+      o[0] = (a0 + runif(r.x, -0.01f, 0.01f)) + P.delta;
+      o[1] = (a1 + runif(r.y, -0.01f, 0.01f)) + P.delta;
+      o[2] = (a2 + runif(r.z, -0.01f, 0.01f)) + P.delta;
     }
-    u32x4 r = rng(seed, (uint32_t)px, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_NOISE);
-    float* o = rstore + P.roff + (long)px * 3;
-    o[0] = (a0 + runif(r.x, -0.01f, 0.01f)) + P.delta;
-    o[1] = (a1 + runif(r.y, -0.01f, 0.01f)) + P.delta;
-    o[2] = (a2 + runif(r.z, -0.01f, 0.01f)) + P.delta;
+    __syncthreads();
   }
 }
 
 void launch_eot_resize(const EotDims& d, const float* matched, const BoxPlace* place,
                        const SpanEntry* spans, uint64_t seed, int64_t step, int gimg0,
                        float* rstore, hipStream_t s) {
-  hipLaunchKernelGGL(k_eot_resize, dim3(kBoxGrid), dim3(256), 0, s, d, matched, place, spans, seed,
-                     step, gimg0, rstore);
+  const size_t shm = (size_t)kResizeRT * d.P * 3 * sizeof(float);
+  hipLaunchKernelGGL(k_eot_resize, dim3(kResizeGrid), dim3(256), shm, s, d, matched, place, spans,
+                     seed, step, gimg0, rstore);
   PHX_LAUNCH_CHECK();
 }
 
@@ -563,11 +597,60 @@ void launch_eot_rot_bwd(const EotDims& d, const float* dimg, const int16_t* owne
   PHX_LAUNCH_CHECK();
 }
 
-// exact adjoint of the antialiased resize, gathered per source pixel over the image's boxes
-__global__ __launch_bounds__(256) void k_eot_resize_bwd(EotDims d, const BoxPlace* __restrict__ place,
-                                                        const SpanEntry* __restrict__ spans,
-                                                        const float* __restrict__ dstore,
-                                                        float* __restrict__ dmatched) {
+// Exact adjoint of the antialiased resize, separable: per box U[i][x] = sum_j Wc[j,x] dR[i,j]
+// (rows kernel, work items of kResizeRT rows, U rows of valid box v at tprefix[v]*kResizeRT*P*3 of
+// the row buffer), then per source pixel dmatched[y,x] = sum over the image's boxes of
+// sum_i Wr[i,y] U[i][x] (cols kernel, lanes along x: coalesced U rows).
+// output indices whose span may contain source index `src` (conservative, clamped to [0, ps))
+__device__ __forceinline__ void adj_range(int src, float inv_scale, float ks, int ps, int* lo, int* hi) {
+  *lo = max((int)floorf(((float)src - ks - 0.5f) / inv_scale - 0.5f) - 1, 0);
+  *hi = min((int)ceilf(((float)src + ks + 1.5f) / inv_scale - 0.5f) + 1, ps - 1);
+}
+
+__global__ __launch_bounds__(256) void k_eot_resize_bwd_rows(EotDims d, const BoxPlace* __restrict__ place,
+                                                             const SpanEntry* __restrict__ spans,
+                                                             const float* __restrict__ dstore,
+                                                             float* __restrict__ tstore) {
+  const ListView L = lists_of(d, place);
+  const int nv = *L.nvalid, total = L.tprefix[nv];
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int v = find_box(L.tprefix, nv, item);
+    const int sl = L.vlist[v];
+    const BoxPlace P = place[sl];
+    const int i0 = (item - L.tprefix[v]) * kResizeRT;
+    const int ni = min(kResizeRT, P.ps - i0);
+    const SpanEntry* sp = spans + (long)sl * d.span_stride;
+    const float scale = (float)P.ps / (float)d.P;
+    const float inv_scale = (float)(1.0 / (double)scale);
+    const float ks = fmaxf(inv_scale, 1.0f);
+    const float one_over_k = 1.0f / ks;
+    const float* D = dstore + P.roff;
+    float* U = tstore + (long)L.tprefix[v] * kResizeRT * d.P * 3;
+    for (int e = threadIdx.x; e < ni * d.P; e += blockDim.x) {
+      const int ii = e / d.P, x = e - ii * d.P;
+      const int i = i0 + ii;
+      int jlo, jhi;
+      adj_range(x, inv_scale, ks, P.ps, &jlo, &jhi);
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      for (int j = jlo; j <= jhi; ++j) {
+        const SpanEntry sj = sp[j];
+        if (x < sj.start || x >= sj.end) continue;
+        const float w = span_weight(sj, x, one_over_k);
+        const float* g = D + ((long)i * P.ps + j) * 3;
+        a0 += w * g[0];
+        a1 += w * g[1];
+        a2 += w * g[2];
+      }
+      float* o = U + ((long)i * d.P + x) * 3;
+      o[0] = a0; o[1] = a1; o[2] = a2;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_eot_resize_bwd_cols(EotDims d, const BoxPlace* __restrict__ place,
+                                                             const SpanEntry* __restrict__ spans,
+                                                             const float* __restrict__ tstore,
+                                                             float* __restrict__ dmatched) {
   const int b = blockIdx.y;
   const long npx = (long)d.P * d.P;
   long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -577,34 +660,25 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd(EotDims d, const BoxPlac
   const int n = L.img_n[b], f = L.img_first[b];
   float a0 = 0.f, a1 = 0.f, a2 = 0.f;
   for (int q = 0; q < n; ++q) {
-    const int sl = L.vlist[f + q];
+    const int v = f + q;
+    const int sl = L.vlist[v];
     const BoxPlace& P = place[sl];
     const float scale = (float)P.ps / (float)d.P;
     const float inv_scale = (float)(1.0 / (double)scale);
     const float ks = fmaxf(inv_scale, 1.0f);
     const float one_over_k = 1.0f / ks;
     const SpanEntry* sp = spans + (long)sl * d.span_stride;
-    int ilo = (int)floorf(((float)y - ks - 0.5f) / inv_scale - 0.5f) - 1;
-    int ihi = (int)ceilf(((float)y + ks + 1.5f) / inv_scale - 0.5f) + 1;
-    int jlo = (int)floorf(((float)x - ks - 0.5f) / inv_scale - 0.5f) - 1;
-    int jhi = (int)ceilf(((float)x + ks + 1.5f) / inv_scale - 0.5f) + 1;
-    ilo = max(ilo, 0); jlo = max(jlo, 0);
-    ihi = min(ihi, P.ps - 1); jhi = min(jhi, P.ps - 1);
-    const float* D = dstore + P.roff;
+    int ilo, ihi;
+    adj_range(y, inv_scale, ks, P.ps, &ilo, &ihi);
+    const float* U = tstore + (long)L.tprefix[v] * kResizeRT * d.P * 3 + (long)x * 3;
     for (int i = ilo; i <= ihi; ++i) {
       const SpanEntry si = sp[i];
       if (y < si.start || y >= si.end) continue;
       const float wy = span_weight(si, y, one_over_k);
-      if (wy == 0.0f) continue;
-      for (int j = jlo; j <= jhi; ++j) {
-        const SpanEntry sj = sp[j];
-        if (x < sj.start || x >= sj.end) continue;
-        const float w = wy * span_weight(sj, x, one_over_k);
-        const float* g = D + ((long)i * P.ps + j) * 3;
-        a0 += w * g[0];
-        a1 += w * g[1];
-        a2 += w * g[2];
-      }
+      const float* g = U + (long)i * d.P * 3;
+      a0 += wy * g[0];
+      a1 += wy * g[1];
+      a2 += wy * g[2];
     }
   }
   float* o = dmatched + ((long)b * npx + p) * 3;
@@ -612,10 +686,18 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd(EotDims d, const BoxPlac
 }
 
 void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEntry* spans,
-                           const float* dstore, float* dmatched, hipStream_t s) {
-  hipLaunchKernelGGL(k_eot_resize_bwd, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d,
-                     place, spans, dstore, dmatched);
+                           const float* dstore, float* tstore, float* dmatched, hipStream_t s) {
+  hipLaunchKernelGGL(k_eot_resize_bwd_rows, dim3(kBoxGrid), dim3(256), 0, s, d, place, spans, dstore,
+                     tstore);
   PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_resize_bwd_cols, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d,
+                     place, spans, tstore, dmatched);
+  PHX_LAUNCH_CHECK();
+}
+
+long eot_resize_scratch_floats(const EotDims& d) {
+  const long tiles = (d.span_stride + kResizeRT - 1) / kResizeRT;
+  return (long)d.B * d.maxb * tiles * kResizeRT * d.P * 3;
 }
 
 // brightness-matcher backward per pixel: returns d(print output) for the 3 channels given
@@ -684,14 +766,19 @@ __global__ __launch_bounds__(256) void k_eot_patch_grad(EotDims d, const float* 
                                                         const float* __restrict__ dmatched,
                                                         const double* __restrict__ dsum, int chunks,
                                                         int add_tv, float* __restrict__ grad) {
+  extern __shared__ float s_mdyc[];  // [B] mean dYc per image, folded once per workgroup
   const long npx = (long)d.P * d.P;
+  for (int b = threadIdx.x; b < d.B; b += blockDim.x) {
+    double s = 0.0;
+    for (int k = 0; k < chunks; ++k) s += dsum[(long)b * chunks + k];
+    s_mdyc[b] = (float)(s / (double)npx);
+  }
+  __syncthreads();
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= npx) return;
   float g[3] = {0.f, 0.f, 0.f};
   for (int b = 0; b < d.B; ++b) {
-    double s = 0.0;
-    for (int k = 0; k < chunks; ++k) s += dsum[(long)b * chunks + k];
-    const float mean_dyc = (float)(s / (double)npx);
+    const float mean_dyc = s_mdyc[b];
     const ImgParams ip = img[b];
     float p[3], pre[3];
     for (int c = 0; c < 3; ++c) {
@@ -727,7 +814,8 @@ void launch_eot_patch_bwd(const EotDims& d, const float* patch, const ImgParams*
   hipLaunchKernelGGL(k_eot_dyc_sum, dim3(kYChunks, d.B), dim3(256), 0, s, d, patch, img, ymean,
                      dmatched, dsum);
   PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_eot_patch_grad, dim3(cdiv((long)d.P * d.P, 256)), dim3(256), 0, s, d, patch,
+  hipLaunchKernelGGL(k_eot_patch_grad, dim3(cdiv((long)d.P * d.P, 256)), dim3(256),
+                     (size_t)d.B * sizeof(float), s, d, patch,
                      img, ymean, dmatched, dsum, kYChunks, add_tv ? 1 : 0, grad);
   PHX_LAUNCH_CHECK();
 }
@@ -759,9 +847,14 @@ __global__ __launch_bounds__(256) void k_tv_part(const float* __restrict__ p, in
 
 __global__ void k_tv_final(const double* __restrict__ part, int n, float* __restrict__ metrics,
                            int add) {
+  __shared__ double sh[64];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < n; i += 64) a += part[i];
+  sh[threadIdx.x] = a;
+  __syncthreads();
   if (threadIdx.x) return;
   double s = 0.0;
-  for (int i = 0; i < n; ++i) s += part[i];
+  for (int i = 0; i < 64; ++i) s += sh[i];
   metrics[PHX_M_TV] = (float)s;
   if (add) metrics[PHX_M_LOSS] += 1e-5f * (float)s;
 }

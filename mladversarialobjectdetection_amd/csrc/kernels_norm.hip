@@ -142,15 +142,22 @@ __global__ __launch_bounds__(256) void k_colred_final(E e, const double* __restr
   }
 }
 
-template <class F, class E>
-static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hipStream_t s) {
+// first half only: chunk partials [nseg][chunks][C][2] in scratch; returns chunks
+template <class F>
+static int colred_parts(F f, long seg_rows, int C, int nseg, double* scratch, hipStream_t s) {
   if (C % 4) throw std::runtime_error("colred: C % 4 != 0");
   RedPlan p = red_plan(seg_rows, C, nseg);
   hipLaunchKernelGGL((k_colred_part<F>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
                      C, p.rpc, scratch);
   PHX_LAUNCH_CHECK();
+  return p.chunks;
+}
+
+template <class F, class E>
+static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hipStream_t s) {
+  const int chunks = colred_parts(f, seg_rows, C, nseg, scratch, s);
   hipLaunchKernelGGL((k_colred_final<E>), dim3(cdiv(C, 16), nseg), dim3(256), 0, s, e, scratch,
-                     p.chunks, C);
+                     chunks, C);
   PHX_LAUNCH_CHECK();
 }
 
@@ -566,144 +573,164 @@ struct SumAcc {
     (void)a1;
   }
 };
-struct SumEpi {
-  float* out;  // [seg][C]
-  int C;
-  __device__ void operator()(int seg, int c, double s0, double) const {
-    out[(long)seg * C + c] = (float)s0;
-  }
-};
 
-// The SE MLP ([B,C] -> [B,Cse] -> [B,C], efficientnet_model.py:184-196) is tiny but latency-
-// bound, so it is spread over many workgroups in two launches:
-//   squeeze  grid (G = ceil(C/64), B): part[b][g][j] = sum over the g-th 64-channel slice of
-//            v[b][c] * m[c][j]; lanes run over j (coalesced rows of m), the 4 waves take 16
-//            channels each with all 16 loads in flight, and meet in LDS;
-//   excite   grid (ceil(C/256), B): every block re-sums the G partials of its image (Cse values),
-//            then one lane per channel runs the expand row.
-constexpr int kSeSlice = 64;
+// The SE MLP ([B,C] -> [B,Cse] -> [B,C], efficientnet_model.py:184-196) runs as ONE launch per
+// SE op after the per-image channel sums' chunk partials: a 1024-lane workgroup per image folds
+// its partials in fp64 (fixed order), then both matrix-vector products run from LDS —
+//   squeeze  lanes (j, channel group): rows of the [C][Cse] matrix are read along j (coalesced),
+//            the channel groups meet in LDS;
+//   excite   one lane per channel, rows of the [Cse][C] matrix read along c.
+// (Three small launches — partial fold, squeeze, excite — cost more than the whole MLP.)
+constexpr int kSeThreads = 1024;
 
-static int se_groups(int C) { return (C + kSeSlice - 1) / kSeSlice; }
-
-size_t se_scratch_doubles(int B, int C, int Cse) {
-  return ((size_t)B * se_groups(C) * Cse + 1) / 2 + 1;
-}
-
-// MODE 0: v = sums * inv (pool, also written out); MODE 1: v = gsum * s * (1 - s)
-template <int MODE>
-__global__ __launch_bounds__(256) void k_se_squeeze(const float* __restrict__ a,
-                                                    const float* __restrict__ sv, float inv, int C,
-                                                    int N, const float* __restrict__ m,
-                                                    float* __restrict__ part,
-                                                    float* __restrict__ pool) {
-  __shared__ float v[kSeSlice];
-  __shared__ float red[256];
-  const int g = blockIdx.x, b = blockIdx.y, G = gridDim.x;
-  const int c0 = g * kSeSlice, n = min(kSeSlice, C - c0);
-  if (threadIdx.x < kSeSlice) {
-    float x = 0.f;
-    if ((int)threadIdx.x < n) {
-      const long i = (long)b * C + c0 + threadIdx.x;
-      if (MODE == 0) {
-        x = a[i] * inv;
-        pool[i] = x;
-      } else {
-        const float sg = sv[i];
-        x = a[i] * sg * (1.f - sg);
-      }
+// v[c] = (float) sum of image b's colred chunk partials (fp64, fixed order)
+__device__ __forceinline__ void se_fold(const double* __restrict__ part, int chunks, int C, int b,
+                                        double* red, float* v) {
+  const int t = threadIdx.x;
+  if (2 * C <= kSeThreads) {
+    const int ng = min(chunks, kSeThreads / C);
+    const int c = t % C, grp = t / C;
+    if (grp < ng) {
+      double s = 0.0;
+#pragma unroll 4
+      for (int k = grp; k < chunks; k += ng) s += part[(((long)b * chunks + k) * C + c) * 2];
+      red[grp * C + c] = s;
     }
-    v[threadIdx.x] = x;
+    __syncthreads();
+    if (t < C) {
+      double s = 0.0;
+      for (int g = 0; g < ng; ++g) s += red[g * C + t];
+      v[t] = (float)s;
+    }
+  } else {
+    for (int c = t; c < C; c += kSeThreads) {
+      double s = 0.0;
+#pragma unroll 4
+      for (int k = 0; k < chunks; ++k) s += part[(((long)b * chunks + k) * C + c) * 2];
+      v[c] = (float)s;
+    }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const float* mr = m + (long)(c0 + wv * 16) * N;
-  for (int j0 = 0; j0 < N; j0 += 64) {
-    const int j = j0 + lane;
-    float acc = 0.f;
-    if (j < N) {
-      float t[16];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) t[r] = (wv * 16 + r < n) ? mr[(long)r * N + j] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc = fmaf(v[wv * 16 + r], t[r], acc);
-    }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    if (wv == 0 && j < N)
-      part[((long)b * G + g) * N + j] = red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane];
-    __syncthreads();
-  }
 }
 
-// forward excite: hidden = b1 + sum_g part; h = act(hidden); scale = sigmoid(b2 + h . w2[:, c])
-__global__ __launch_bounds__(256) void k_se_excite(const float* __restrict__ part, int G, int C,
-                                                   int N, const float* __restrict__ b1,
-                                                   const float* __restrict__ w2,
-                                                   const float* __restrict__ b2, int act,
-                                                   float* __restrict__ hidden,
-                                                   float* __restrict__ scale) {
-  extern __shared__ float sh[];  // [N]
-  const int b = blockIdx.y;
-  for (int j = threadIdx.x; j < N; j += blockDim.x) {
-    float h = b1[j];
-    for (int g = 0; g < G; ++g) h += part[((long)b * G + g) * N + j];
-    if (blockIdx.x == 0) hidden[(long)b * N + j] = h;  // pre-activation, kept for backward
-    sh[j] = act_fwd(h, act);
+// out[j] = sum_c v[c] * m[c][j] (+ through redf), lanes (j, channel group); ends synchronised
+__device__ __forceinline__ void se_squeeze(const float* v, int C, int N, const float* __restrict__ m,
+                                           float* redf) {
+  const int t = threadIdx.x;
+  const int ng = kSeThreads / N;
+  const int j = t % N, g = t / N;
+  // 8 independent rows in flight per lane (a dependent chain of loads would be latency-bound)
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (g < ng) {
+    int c = g;
+    for (; c + 7 * ng < C; c += 8 * ng) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = m[(long)(c + u * ng) * N + j];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = fmaf(v[c + u * ng], w[u], a[u]);
+    }
+    for (; c < C; c += ng) a[0] = fmaf(v[c], m[(long)c * N + j], a[0]);
+  }
+  redf[t] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kSeThreads) void k_se_mlp(const double* __restrict__ part, int chunks,
+                                                       int C, int N, float inv,
+                                                       const float* __restrict__ w1,
+                                                       const float* __restrict__ b1,
+                                                       const float* __restrict__ w2,
+                                                       const float* __restrict__ b2, int act,
+                                                       float* __restrict__ pool,
+                                                       float* __restrict__ hidden,
+                                                       float* __restrict__ scale) {
+  extern __shared__ float se_sm[];  // v [C] | activated hidden [N]
+  __shared__ double red[kSeThreads];
+  __shared__ float redf[kSeThreads];
+  float* v = se_sm;
+  float* hs = se_sm + C;
+  const int b = blockIdx.x, t = threadIdx.x;
+  se_fold(part, chunks, C, b, red, v);
+  for (int c = t; c < C; c += kSeThreads) {
+    const float x = v[c] * inv;  // mean over HW
+    v[c] = x;
+    pool[(long)b * C + c] = x;
   }
   __syncthreads();
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float e[4] = {b2[c], 0.f, 0.f, 0.f};
-  int j = 0;
-  for (; j + 3 < N; j += 4) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = fmaf(sh[j + u], w2[(long)(j + u) * C + c], e[u]);
+  se_squeeze(v, C, N, w1, redf);
+  if (t < N) {
+    float h = b1[t];
+    for (int g = 0; g < kSeThreads / N; ++g) h += redf[g * N + t];
+    hidden[(long)b * N + t] = h;  // pre-activation, kept for backward
+    hs[t] = act_fwd(h, act);
   }
-  for (; j < N; ++j) e[0] = fmaf(sh[j], w2[(long)j * C + c], e[0]);
-  scale[(long)b * C + c] = sigmoidf_((e[0] + e[1]) + (e[2] + e[3]));
+  __syncthreads();
+  for (int c = t; c < C; c += kSeThreads) {
+    float e[8] = {b2[c], 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int j = 0;
+    for (; j + 7 < N; j += 8) {
+      float w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) w[u] = w2[(long)(j + u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) e[u] = fmaf(hs[j + u], w[u], e[u]);
+    }
+    for (; j < N; ++j) e[0] = fmaf(hs[j], w2[(long)j * C + c], e[0]);
+    scale[(long)b * C + c] = sigmoidf_(((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7])));
+  }
 }
 
-// backward excite: dh = (sum_g part) * act'(hidden); dpool[c] = dh . w1[c, :]
-__global__ __launch_bounds__(256) void k_se_excite_bwd(const float* __restrict__ part, int G,
-                                                       int C, int N,
-                                                       const float* __restrict__ w1, int act,
-                                                       const float* __restrict__ hidden,
-                                                       float* __restrict__ dpool) {
-  extern __shared__ float dh[];  // [N]
-  const int b = blockIdx.y;
-  for (int j = threadIdx.x; j < N; j += blockDim.x) {
+// backward: dlogit = (sum_hw dy*x) * s(1-s); dh = (dlogit . w2t) * act'(hidden); dpool = dh . w1[c,:]
+__global__ __launch_bounds__(kSeThreads) void k_se_mlp_bwd(const double* __restrict__ part, int chunks,
+                                                           int C, int N,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ w1,
+                                                           const float* __restrict__ w2t, int act,
+                                                           const float* __restrict__ hidden,
+                                                           float* __restrict__ dpool) {
+  extern __shared__ float se_sm[];  // v [C] | dh [N]
+  __shared__ double red[kSeThreads];
+  __shared__ float redf[kSeThreads];
+  float* v = se_sm;
+  float* dh = se_sm + C;
+  const int b = blockIdx.x, t = threadIdx.x;
+  se_fold(part, chunks, C, b, red, v);
+  for (int c = t; c < C; c += kSeThreads) {
+    const float sg = scale[(long)b * C + c];
+    v[c] = v[c] * sg * (1.f - sg);
+  }
+  __syncthreads();
+  se_squeeze(v, C, N, w2t, redf);
+  if (t < N) {
     float d = 0.f;
-    for (int g = 0; g < G; ++g) d += part[((long)b * G + g) * N + j];
-    dh[j] = d * act_grad(hidden[(long)b * N + j], act);
+    for (int g = 0; g < kSeThreads / N; ++g) d += redf[g * N + t];
+    dh[t] = d * act_grad(hidden[(long)b * N + t], act);
   }
   __syncthreads();
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float* wr = w1 + (long)c * N;
-  float e[4] = {0.f, 0.f, 0.f, 0.f};
-  int j = 0;
-  for (; j + 3 < N; j += 4) {
+  for (int c = t; c < C; c += kSeThreads) {
+    const float* wr = w1 + (long)c * N;
+    float e[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int j = 0;
+    for (; j + 7 < N; j += 8) {
+      float w[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) e[u] = fmaf(dh[j + u], wr[j + u], e[u]);
+      for (int u = 0; u < 8; ++u) w[u] = wr[j + u];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) e[u] = fmaf(dh[j + u], w[u], e[u]);
+    }
+    for (; j < N; ++j) e[0] = fmaf(dh[j], wr[j], e[0]);
+    dpool[(long)b * C + c] = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
   }
-  for (; j < N; ++j) e[0] = fmaf(dh[j], wr[j], e[0]);
-  dpool[(long)b * C + c] = (e[0] + e[1]) + (e[2] + e[3]);
 }
 
 void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
                    float* hidden, float* scale, hipStream_t s, double* scratch) {
-  // per-image channel sums land after the pool vector: pool buffer = [B*C pool | B*C sums]
-  float* sums = pool + (long)B * C;
-  colred(SumAcc{x, nullptr, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
-  // the colred scratch is free again once the sums are out: it holds the squeeze partials
-  float* part = reinterpret_cast<float*>(scratch);
-  const int G = se_groups(C);
-  hipLaunchKernelGGL(k_se_squeeze<0>, dim3(G, B), dim3(256), 0, s, sums, nullptr, 1.0f / (float)HW, C,
-                     Cse, w1, part, pool);
-  PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_se_excite, dim3(cdiv(C, 256), B), dim3(256), Cse * sizeof(float), s, part, G, C,
-                     Cse, b1, w2, b2, act, hidden, scale);
+  if (Cse > kSeThreads) throw std::runtime_error("se: squeeze width > 1024");
+  const int chunks = colred_parts(SumAcc{x, nullptr, C, {}}, HW, C, B, scratch, s);
+  hipLaunchKernelGGL(k_se_mlp, dim3(B), dim3(kSeThreads), (size_t)(C + Cse) * sizeof(float), s, scratch,
+                     chunks, C, Cse, 1.0f / (float)HW, w1, b1, w2, b2, act, pool, hidden, scale);
   PHX_LAUNCH_CHECK();
   (void)y;  // the excitation is folded into the consuming GEMM's A load (rowscale)
 }
@@ -741,15 +768,11 @@ int launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int C
                   const float* pool, const float* hidden, const float* scale, float* gsum,
                   bool acc, hipStream_t s, double* scratch, GradSink gs) {
   (void)b1; (void)b2; (void)pool;
-  float* sums = gsum + (long)B * C;  // gsum: [B*C dpool | B*C sum_hw dy*x]
-  colred(SumAcc{x, dy, C, {}}, SumEpi{sums, C}, HW, C, B, scratch, s);
-  float* part = reinterpret_cast<float*>(scratch);
-  const int G = se_groups(C);
-  hipLaunchKernelGGL(k_se_squeeze<1>, dim3(G, B), dim3(256), 0, s, sums, scale, 1.0f, C, Cse, w2t, part,
-                     nullptr);
-  PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_se_excite_bwd, dim3(cdiv(C, 256), B), dim3(256), Cse * sizeof(float), s, part, G,
-                     C, Cse, w1, act, hidden, gsum);
+  if (Cse > kSeThreads) throw std::runtime_error("se: squeeze width > 1024");
+  // gsum[0 .. B*C): dpool
+  const int chunks = colred_parts(SumAcc{x, dy, C, {}}, HW, C, B, scratch, s);
+  hipLaunchKernelGGL(k_se_mlp_bwd, dim3(B), dim3(kSeThreads), (size_t)(C + Cse) * sizeof(float), s,
+                     scratch, chunks, C, Cse, scale, w1, w2t, act, hidden, gsum);
   PHX_LAUNCH_CHECK();
   return ew_gstats(SeBwdApply{dy, scale, gsum, dx, C, acc ? 1 : 0, 1.0f / (float)HW, {}, {}}, HW, C, B, gs, s);
 }

@@ -72,9 +72,10 @@ void launch_eot_composite(const EotDims& d, const float* img_in, const BoxPlace*
 void launch_eot_rot_bwd(const EotDims& d, const float* dimg, const int16_t* owner,
                         const BoxPlace* place, const float* rstore, float* dstore,
                         hipStream_t s);
-// backward: dmatched[b] = sum_k resize^T(dR_k)
+// backward: dmatched[b] = sum_k resize^T(dR_k); tstore: eot_resize_scratch_floats(d) floats
 void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEntry* spans,
-                           const float* dstore, float* dmatched, hipStream_t s);
+                           const float* dstore, float* tstore, float* dmatched, hipStream_t s);
+long eot_resize_scratch_floats(const EotDims& d);
 // backward through brightness matcher + print variation, summed over images, + 1e-5 TV grad.
 void launch_eot_patch_bwd(const EotDims& d, const float* patch, const ImgParams* img,
                           const float* ymean, const float* dmatched, double* dsum, float* grad,
