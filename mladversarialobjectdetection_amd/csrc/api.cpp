@@ -100,6 +100,13 @@ struct Exec {
   int* err = nullptr;
   float* patched = nullptr;
   int16_t* owner = nullptr;
+  // drop connect (non-b0 backbones, training): per drop op its block id and survival, and the
+  // per-image keep flags of the current pass [ndrop][B]
+  int ndrop = 0;
+  int* drop_block = nullptr;
+  float* drop_p = nullptr;
+  float* drop_keep = nullptr;
+  std::vector<int> drop_slot;                  // op id -> row of drop_keep (-1)
   // caller-injected placement boxes ([B,100,4] slot layout + counts)
   float* inj_boxes = nullptr;
   int* inj_count = nullptr;
@@ -454,6 +461,25 @@ Exec& phx_ctx::exec_for(int B) {
   E.err = E.alloc<int>(1);
   E.patched = E.alloc<float>((size_t)B * S * S * 3);
   E.owner = E.alloc<int16_t>((size_t)B * S * S * 3);
+  {
+    std::vector<int> blk;
+    std::vector<float> pr;
+    E.drop_slot.assign(P.ops.size(), -1);
+    for (size_t i = 0; i < P.ops.size(); ++i)
+      if (P.ops[i].t == OP_ADD && P.ops[i].survival > 0.f) {
+        E.drop_slot[i] = (int)blk.size();
+        blk.push_back(P.ops[i].drop_block);
+        pr.push_back(P.ops[i].survival);
+      }
+    E.ndrop = (int)blk.size();
+    if (E.ndrop) {
+      E.drop_block = E.alloc<int>(E.ndrop);
+      E.drop_p = E.alloc<float>(E.ndrop);
+      E.drop_keep = E.alloc<float>((size_t)E.ndrop * B);
+      PHX_HIP(hipMemcpy(E.drop_block, blk.data(), blk.size() * sizeof(int), hipMemcpyHostToDevice));
+      PHX_HIP(hipMemcpy(E.drop_p, pr.data(), pr.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
+  }
   E.inj_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
   E.inj_count = E.alloc<int>(B);
   execs.push_back(std::move(ex));
@@ -483,10 +509,22 @@ GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
 }
 
 // victim forward over the program (EfficientDetNet.call, efficientdet_keras.py:884-906)
-void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
+// pass: 0 first (clean) pass, 1 second (patched) pass, 2 standalone detect — with `step` and the
+// global index of the first image it keys the drop-connect draws
+DropView drop_view(const Exec& E, int op) {
+  const int d = E.drop_slot.empty() ? -1 : E.drop_slot[op];
+  if (d < 0) return DropView{};
+  const Tensor& t = E.prog.tensors[E.prog.ops[op].out];
+  return DropView{E.drop_keep + (long)d * E.B, E.prog.ops[op].survival, (long)t.h * t.w};
+}
+
+void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int pass, int64_t step,
+                 int gimg0) {
   const Program& P = E.prog;
   float* W = ctx->w();
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN;
+  if (E.ndrop)
+    launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   for (size_t i = 0; i < P.ops.size(); ++i) {
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
@@ -555,7 +593,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       case OP_ADD:
         launch_add(view(ctx, E, op.in[0], input), view(ctx, E, op.in[1], input), y,
-                   (long)to.numel(), to.c, s);
+                   (long)to.numel(), to.c, s, drop_view(E, (int)i));
         break;
       case OP_MAXPOOL:
         launch_maxpool_fwd(view(ctx, E, op.in[0], input), y, E.pool_amax[i], ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
@@ -679,7 +717,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       case OP_ADD: {
         const int n0 = launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s, to.c,
-                                        gsk_in == 0 ? gsk : GradSink{});
+                                        gsk_in == 0 ? gsk : GradSink{}, drop_view(E, i));
         const int n1 = launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s, to.c,
                                         gsk_in == 1 ? gsk : GradSink{});
         np = gsk_in == 0 ? n0 : n1;
@@ -877,7 +915,7 @@ int phx_detect(phx_ctx* ctx, const float* images, int B, float* scores, int32_t*
   check_ready(ctx, B);
   hipStream_t s = (hipStream_t)stream;
   Exec& E = ctx->exec_for(B);
-  run_forward(ctx, E, images, s);
+  run_forward(ctx, E, images, s, 2, 0, 0);
   run_pre_nms(ctx, E, s);
   const long BA = (long)B * ctx->A;
   if (scores) PHX_HIP(hipMemcpyAsync(scores, E.scores, BA * 4, hipMemcpyDeviceToDevice, s));
@@ -894,7 +932,7 @@ int phx_first_pass(phx_ctx* ctx, const float* images, int B, float* ob, float* o
   check_ready(ctx, B);
   hipStream_t s = (hipStream_t)stream;
   Exec& E = ctx->exec_for(B);
-  run_forward(ctx, E, images, s);
+  run_forward(ctx, E, images, s, 0, 0, 0);
   run_pre_nms(ctx, E, s);
   run_nms(ctx, E, 2, ob, os, oc, s);
   return PHX_OK;
@@ -1004,7 +1042,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   ctx->last = &E;
   PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
   // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
-  run_forward(ctx, E, images, s);
+  run_forward(ctx, E, images, s, 0, step, gimg0);
   run_pre_nms(ctx, E, s);
   // (a second HIP stream for the NMS passes that only feed the ASR metric was measured: any
   // multi-stream use slows the whole step by ~0.8 ms on this runtime, so everything stays on `s`)
@@ -1020,7 +1058,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
               inject ? E.inj_count : E.nms1_count, params, step, gimg0, s);
   launch_eot_count(E.ed, E.place, metrics, s);
   // 3. second pass + loss
-  run_forward(ctx, E, E.patched, s);
+  run_forward(ctx, E, E.patched, s, 1, step, gimg0);
   run_pre_nms(ctx, E, s);
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, grad, metrics, s);

@@ -282,6 +282,7 @@ enum RngStream : uint32_t {
   RNG_PLACE = 2,      // per box: centre jitter (attacker.py:474-475)
   RNG_BOX = 3,        // per box: brightness delta, angle (attacker.py:427, 436)
   RNG_NOISE = 4,      // per box element: U(-.01,.01) noise (attacker.py:426)
+  RNG_DROP = 5,       // per (MBConv block, pass, image): drop-connect uniform (utils.py:336-339)
 };
 
 }  // namespace phx

@@ -107,10 +107,21 @@ int ew_gstats_partials(long seg_rows, int C, int nseg);
 void launch_bn_bwd_finalize(const float2* part, int P, long M, int C, float* mdz, float* mdzx,
                             hipStream_t s);
 size_t colred_scratch_doubles(long seg_rows, int C, int nseg);
-void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s);
-// dst (+)= src; with a GradSink (C channels) the BN-backward sums of the result come along
+// drop connect (utils.py:329-344) on one operand: v' = (v / p) * keep[image], forward, and
+// (g * keep[image]) / p for its gradient
+struct DropView {
+  const float* keep = nullptr;  // [B] 0 / 1 per image (launch_drop_keep); nullptr = off
+  float p = 1.f;                // survival probability of the block
+  long rows = 1;                // rows (pixels) per image
+};
+// keep[d*B + b] = floor(p[d] + U), U = u01(Philox(seed; block[d], pass, gimg0 + b, step<<8|RNG_DROP))
+void launch_drop_keep(const int* block, const float* p, int nd, int B, uint64_t seed, int64_t step,
+                      int gimg0, int pass, float* keep, hipStream_t s);
+// y = drop(a) + b
+void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s, DropView dv = DropView{});
+// dst (+)= drop'(src); with a GradSink (C channels) the BN-backward sums of the result come along
 int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s, int C = 4,
-                     GradSink gs = GradSink{});
+                     GradSink gs = GradSink{}, DropView dv = DropView{});
 // amax: per output element, the window tap (row-major) holding the maximum; the backward
 // routes each dy there (TF MaxPoolGrad)
 void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int C, int Ho, int Wo,

@@ -780,25 +780,57 @@ int launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int C
 // ------------------------------------------------------------------------------------------
 // elementwise
 // ------------------------------------------------------------------------------------------
-__global__ void k_add(InX a, InX b, float4* __restrict__ y, long n4, int C) {
+__device__ __forceinline__ float4 drop_fwd4(const DropView& dv, long row, float4 u) {
+  const float k = dv.keep[row / dv.rows];
+  return make_float4((u.x / dv.p) * k, (u.y / dv.p) * k, (u.z / dv.p) * k, (u.w / dv.p) * k);
+}
+__device__ __forceinline__ float4 drop_bwd4(const DropView& dv, long row, float4 g) {
+  const float k = dv.keep[row / dv.rows];
+  return make_float4((g.x * k) / dv.p, (g.y * k) / dv.p, (g.z * k) / dv.p, (g.w * k) / dv.p);
+}
+
+__global__ void k_add(InX a, InX b, float4* __restrict__ y, long n4, int C, DropView dv) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
   const int c = (int)((i * 4) % C);
   float4 u = inx_load4(a, i * 4, c), v = inx_load4(b, i * 4, c);
+  if (dv.keep) u = drop_fwd4(dv, i * 4 / C, u);
   y[i] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
 }
 
-void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s) {
+void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s, DropView dv) {
   long n4 = n / 4;
-  hipLaunchKernelGGL(k_add, dim3(cdiv(n4, 256)), dim3(256), 0, s, a, b, (float4*)y, n4, C);
+  hipLaunchKernelGGL(k_add, dim3(cdiv(n4, 256)), dim3(256), 0, s, a, b, (float4*)y, n4, C, dv);
+  PHX_LAUNCH_CHECK();
+}
+
+// drop connect keep flags: tf.floor(survival + tf.random.uniform([B,1,1,1])) per block and image
+__global__ void k_drop_keep(const int* __restrict__ block, const float* __restrict__ p, int nd, int B,
+                            uint64_t seed, int64_t step, int gimg0, int pass,
+                            float* __restrict__ keep) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nd * B) return;
+  const int d = i / B, b = i - d * B;
+  const u32x4 r = philox4x32_10(
+      u32x4{(uint32_t)block[d], (uint32_t)pass, (uint32_t)(gimg0 + b),
+            (uint32_t)((uint64_t)step << 8) | (uint32_t)RNG_DROP},
+      (uint32_t)seed, (uint32_t)(seed >> 32));
+  keep[i] = floorf(p[d] + u01(r.x));
+}
+
+void launch_drop_keep(const int* block, const float* p, int nd, int B, uint64_t seed, int64_t step,
+                      int gimg0, int pass, float* keep, hipStream_t s) {
+  hipLaunchKernelGGL(k_drop_keep, dim3(cdiv(nd * B, 256)), dim3(256), 0, s, block, p, nd, B, seed, step,
+                     gimg0, pass, keep);
   PHX_LAUNCH_CHECK();
 }
 
 __global__ void k_copy_grad(const float4* __restrict__ src, float4* __restrict__ dst, long n4,
-                            int acc) {
+                            int acc, int C, DropView dv) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
   float4 v = src[i];
+  if (dv.keep) v = drop_bwd4(dv, i * 4 / C, v);
   if (acc) {
     float4 p = dst[i];
     v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
@@ -810,11 +842,13 @@ struct CopyGrad {
   const float* src;
   float* dst;
   int C, acc;
+  DropView dv;
   using Raw = float4;
   __device__ void init(int, int) {}
   __device__ Raw load(long m, int c4) const { return *reinterpret_cast<const float4*>(src + m * C + c4 * 4); }
   __device__ float4 out(const Raw& v0, long m, int c4) const {
     float4 v = v0;
+    if (dv.keep) v = drop_bwd4(dv, m, v);
     float4* op = reinterpret_cast<float4*>(dst + m * C + c4 * 4);
     if (acc) {
       const float4 p = *op;
@@ -826,11 +860,11 @@ struct CopyGrad {
 };
 
 int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s, int C,
-                     GradSink gs) {
-  if (gs.part) return ew_gstats(CopyGrad{src, dst, C, acc ? 1 : 0}, n / C, C, 1, gs, s);
+                     GradSink gs, DropView dv) {
+  if (gs.part) return ew_gstats(CopyGrad{src, dst, C, acc ? 1 : 0, dv}, n / C, C, 1, gs, s);
   long n4 = n / 4;
   hipLaunchKernelGGL(k_copy_grad, dim3(cdiv(n4, 256)), dim3(256), 0, s, (const float4*)src,
-                     (float4*)dst, n4, acc ? 1 : 0);
+                     (float4*)dst, n4, acc ? 1 : 0, C, dv);
   PHX_LAUNCH_CHECK();
   return 0;
 }

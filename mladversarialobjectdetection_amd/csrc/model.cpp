@@ -84,7 +84,7 @@ bool get_model_config(const std::string& name, ModelConfig* c) {
       if (name == "efficientdet-d7") c->anchor_scale = 5.0f;
       // b0 disables drop connect (efficientdet_keras.py:803-804); others keep 0.8
       // (efficientnet_builder.py:174).
-      c->survival_prob = (std::string(d.bb) == "efficientnet-b0") ? 0.0f : 0.8f;
+      c->survival_prob = (std::string(d.bb) == "efficientnet-b0") ? 0.0 : 0.8;
       return true;
     }
   }
@@ -111,7 +111,7 @@ bool get_model_config(const std::string& name, ModelConfig* c) {
       c->act = ACT_RELU6;
       c->fpn_weight_method = 1;
       for (int i = 0; i < 3; ++i) { c->mean_rgb[i] = 127.0f; c->stddev_rgb[i] = 128.0f; }
-      c->survival_prob = 0.8f;
+      c->survival_prob = 0.8;
       return true;
     }
   }
@@ -353,9 +353,14 @@ void NetBuilder::build_backbone(std::vector<int>* feats) {
     x = op_pw(x, pfx + "/" + conv_name(), b.o, false);
     x = op_bn(x, pfx + "/" + bn_name(), ACT_NONE);
     if (b.s == 1 && b.i == b.o) {  // id_skip: :406-413
-      if (cfg_.survival_prob > 0.0f && batch_ > 0 && training_)
-        throw std::runtime_error("drop-connect backbones (non-b0) are not supported yet");
       x = op_add(x, xin);
+      // drop connect on the block branch before the add (:411-412, utils.py:329-344) with the
+      // survival probability decayed per block (efficientnet_model.py:752-755); training only
+      if (cfg_.survival_prob > 0.0 && batch_ > 0 && training_) {
+        const double drop_rate = 1.0 - cfg_.survival_prob;
+        prog_.ops.back().survival = (float)(1.0 - drop_rate * (double)idx / (double)nb);
+        prog_.ops.back().drop_block = idx;
+      }
     }
     (void)cin;
     // reduction endpoints: :751-762

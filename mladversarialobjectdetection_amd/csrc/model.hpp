@@ -57,6 +57,8 @@ struct Op {
   int fuse_method = 0;                             // 0 fastattn, 1 sum
   bool acc[3] = {false, false, false};             // backward: accumulate into input grad
   bool bwd = false;                                // op participates in the backward pass
+  float survival = 0.f;                            // OP_ADD: drop connect on in[0] (0 = off)
+  int drop_block = -1;                             // its MBConv block index (Philox counter)
   std::string name;
 };
 
@@ -86,7 +88,7 @@ struct ModelConfig {
   // backbone
   double width_coefficient = 1.0, depth_coefficient = 1.0;
   bool lite = false;             // relu6, no SE, fixed stem/head
-  float survival_prob = 0.0f;    // drop connect (0 = off); b0 disables it
+  double survival_prob = 0.0;    // drop connect (0 = off); b0 disables it
   int num_anchors() const { return num_scales * (int)aspect_ratios.size(); }
 };
 

@@ -21,6 +21,8 @@ import numpy as np
 import torch
 import torch.nn.functional as F
 
+from . import philox as ph
+
 # hparams_config.py:301-467
 MODELS = {
     "efficientdet-d0": dict(backbone="efficientnet-b0", image_size=512, fpn=64, cells=3, rep=3, w=1.0, d=1.0),
@@ -110,12 +112,14 @@ class Detector:
     """EfficientDetNet.call(images, training) restated; weights: name -> HWIO array."""
 
     def __init__(self, weights: dict, model="efficientdet-d0", image_size=None, dtype=torch.float64,
-                 training=True):
+                 training=True, drop=None):
         self.W = weights
         self.cfg = MODELS[model]
         self.image_size = image_size or self.cfg["image_size"]
         self.dtype = dtype
         self.training = training
+        # drop-connect draws: dict(seed, step, gimg0, pass) — pass 0 first, 1 second, 2 detect
+        self.drop = drop
         self._cache = {}
         self.bn_stats = {}
 
@@ -171,6 +175,21 @@ class Detector:
         x = self.dwconv(x, pfx + "/depthwise_kernel")
         return self.conv(x, pfx + "/pointwise_kernel", bias=pfx + "/bias")
 
+    def drop_connect(self, x, idx, nb):
+        """utils.py:329-344 with the per-block survival of efficientnet_model.py:752-755 (global
+        survival 0.8, efficientnet_builder.py:174; b0 overrides it to 0, efficientdet_keras.py:803-804).
+        TF draws U[0,1) per image; here U = u01(Philox(seed; block, pass, global image, step, RNG_DROP))
+        so the product's draws are reproduced: keep = floor(p + U) in fp32, x / p * keep."""
+        if self.drop is None:
+            raise ValueError("drop connect is active (non-b0 backbone, training): pass drop=dict(...)")
+        d = self.drop
+        p = np.float32(1.0 - (1.0 - 0.8) * float(idx) / nb)
+        B = x.shape[0]
+        u = ph.u01(ph.draw(d["seed"], idx, d["pass"], np.arange(B) + d["gimg0"], d["step"], ph.RNG_DROP)[0])
+        keep = np.floor((p + u).astype(np.float32))
+        k = torch.as_tensor(keep.astype(np.float64), dtype=x.dtype).view(-1, 1, 1, 1)
+        return x / float(p) * k
+
     # ---- backbone ----------------------------------------------------------------------------
     def backbone(self, x):
         bb = self.cfg["backbone"]
@@ -208,6 +227,8 @@ class Detector:
             x = torch.sigmoid(sq) * x
             x = self.bn(self.conv(x, f"{pfx}/{cname(cid)}/kernel"), f"{pfx}/{bname(bid)}")
             if s == 1 and inf == outf:
+                if self.training and "b0" not in bb:
+                    x = self.drop_connect(x, idx, len(blocks))
                 x = x + inputs
             if idx == len(blocks) - 1 or blocks[idx + 1][1] > 1:
                 reductions.append(x)

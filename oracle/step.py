@@ -43,10 +43,12 @@ def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0
     boxes: None -> first-pass soft-NMS boxes (the reference); else a list per image of [n,4]
     arrays used for placement (the first pass still runs, as in the product)."""
     image_size = image_size or D.MODELS[model]["image_size"]
-    det = D.Detector(weights, model, image_size, dtype=dtype, training=True)
+    det = D.Detector(weights, model, image_size, dtype=dtype, training=True,
+                     drop=dict(seed=seed, step=step, gimg0=gimg0, **{"pass": 0}))
     images_t = torch.as_tensor(np.asarray(images, dtype=np.float64), dtype=dtype)
     B = images_t.shape[0]
     fp = first_pass(det, images_t, image_size, score_thresh)
+    det.drop = dict(det.drop, **{"pass": 1})  # the second pass draws its own drop-connect masks
     place_boxes = [fp[b][0] for b in range(B)] if boxes is None else [np.asarray(bx, np.float32) for bx in boxes]
     patch_t = torch.as_tensor(np.asarray(patch, dtype=np.float64), dtype=dtype).requires_grad_(True)
     scale_t = torch.tensor(float(np.float32(scale)), dtype=dtype, requires_grad=True)

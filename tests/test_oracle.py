@@ -140,3 +140,20 @@ def test_adam_reference_formula():
     # t=1: m = .1 g, v = .001 g^2, alpha = lr*sqrt(.001)/.1 -> step ~ lr * sign(g)
     np.testing.assert_allclose(out[:2], [0.5 - 0.01, -0.98], rtol=1e-5)
     assert out[2] == np.float32(0.2)   # scale slot untouched by a zero gradient, clip [0,1]
+
+
+def test_drop_connect_draws():
+    """Oracle drop connect (utils.py:329-344): per-image keep = floor(p + U) with the per-block
+    survival p = 1 - 0.2*idx/N (efficientnet_model.py:752-755); the branch is x/p or exactly 0, and
+    the two passes of a step draw independently."""
+    import torch
+    from oracle import detector as D
+    det = D.Detector({}, "efficientdet-d1", 128, drop={"seed": 5, "step": 3, "gimg0": 0, "pass": 1})
+    x = torch.ones(2, 4, 3, 3, dtype=torch.float64)
+    y = det.drop_connect(x, 19, 23)  # both images dropped at step 3, pass 1 (see the GPU test)
+    assert torch.equal(y, torch.zeros_like(x))
+    p = float(np.float32(1.0 - 0.2 * 1 / 23))
+    y = det.drop_connect(x, 1, 23)   # block 1 keeps both images
+    assert torch.allclose(y, x / p)
+    det.drop = {"seed": 5, "step": 3, "gimg0": 0, "pass": 0}
+    assert torch.equal(det.drop_connect(x, 19, 23), x / float(np.float32(1.0 - 0.2 * 19 / 23)))
