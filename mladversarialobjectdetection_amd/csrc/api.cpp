@@ -681,8 +681,14 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     int np = -1;
     switch (op.t) {
       case OP_STEM: {
-        // the stem dgrad reads each dy element up to 4x: materialise the BN-backward output once
         GradX g = gview(ctx, E, op.out, input);
+        // the image gradient feeds only the EOT backward, which reads it at owned pixels
+        if (!op.acc[0] && stem_bwd_gx_supported(to.c)) {
+          launch_stem_bwd_gx(g, W + op.w, E.owner, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t,
+                             op.pad_l, s);
+          break;
+        }
+        // the stem dgrad reads each dy element up to 4x: materialise the BN-backward output once
         float* gy = E.gptr(op.out);
         if (g.y) launch_bn_bwd_apply2(g, gy, (long)to.rows(), to.c, s);
         launch_stem_bwd(g.y ? gy : g.da, W + op.w, dx, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l,
@@ -716,10 +722,21 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
                            E.slot_b[op.slot], E.slot_c[op.slot], E.se_g, op.acc[0], s, E.red, gsk);
         break;
       case OP_ADD: {
-        const int n0 = launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s, to.c,
-                                        gsk_in == 0 ? gsk : GradSink{}, drop_view(E, i));
-        const int n1 = launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s, to.c,
-                                        gsk_in == 1 ? gsk : GradSink{});
+        // inputs whose gradient buffer aliases the output's (model.cpp: plan_backward) need no
+        // copy, only the BN-backward sums when they are a BN output
+        int n0 = 0, n1 = 0;
+        if (dx == dy) {
+          if (gsk_in == 0) n0 = launch_grad_sums(dy, (long)to.numel(), to.c, gsk, s);
+        } else {
+          n0 = launch_copy_grad(dy, dx, (long)to.numel(), op.acc[0], s, to.c,
+                                gsk_in == 0 ? gsk : GradSink{}, drop_view(E, i));
+        }
+        if (E.gptr(op.in[1]) == dy) {
+          if (gsk_in == 1) n1 = launch_grad_sums(dy, (long)to.numel(), to.c, gsk, s);
+        } else {
+          n1 = launch_copy_grad(dy, E.gptr(op.in[1]), (long)to.numel(), op.acc[1], s, to.c,
+                                gsk_in == 1 ? gsk : GradSink{});
+        }
         np = gsk_in == 0 ? n0 : n1;
         break;
       }

@@ -18,6 +18,11 @@ int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int 
 // dx [B,H,W,3] (+)= conv_transpose(dy); dy is a materialised gradient [B,Ho,Wo,Co]
 void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
                      int Wo, int Co, int pt, int pl, bool acc, hipStream_t s);
+// dx [B,H,W,3] = conv_transpose(gx(dy)) through the stem BN's gradient view, only at pixels some
+// paste owns (owner [B,H,W,3] >= 0; nullptr = everywhere), zero elsewhere; overwrites dx
+bool stem_bwd_gx_supported(int Co);
+void launch_stem_bwd_gx(GradX g, const float* w, const int16_t* owner, float* dx, int B, int H, int W,
+                        int Ho, int Wo, int Co, int pt, int pl, hipStream_t s);
 // C[M,N] (+)= A[M,K] * B + bias ; B given as Bt[N][K].  rowscale (optional): A[m,k] is
 // multiplied by rowscale[(m / rows_per_img) * K + k] (SE excitation folded into the load).
 struct GemmPlan {
@@ -122,6 +127,8 @@ void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s, DropView d
 // dst (+)= drop'(src); with a GradSink (C channels) the BN-backward sums of the result come along
 int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t s, int C = 4,
                      GradSink gs = GradSink{}, DropView dv = DropView{});
+// GradSink sums of src [n/C, C] without writing anything (src is already the BN output's gradient)
+int launch_grad_sums(const float* src, long n, int C, GradSink gs, hipStream_t s);
 // amax: per output element, the window tap (row-major) holding the maximum; the backward
 // routes each dy there (TF MaxPoolGrad)
 void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int C, int Ho, int Wo,

@@ -173,6 +173,120 @@ __global__ __launch_bounds__(256) void k_stem_bwd(const float* __restrict__ dy,
   }
 }
 
+// Stem dgrad fused with the stem BN's backward (GradX view) and restricted to the pixels that
+// are read: the image gradient's only consumer is the EOT rotation backward, which reads it where
+// a pasted patch owns the pixel (k_eot_rot_bwd), so a 32x32-pixel tile without an owned pixel
+// writes zeros and skips its dy reads.  A live tile stages its 17x17 dy window into LDS with the
+// BN backward applied once per element (neighbouring quads re-read each dy pixel from LDS), then
+// each lane computes one 2x2 input quad as k_stem_bwd does.
+constexpr int kStemTQ = 16;  // quads per tile side
+
+template <int CO>
+__global__ __launch_bounds__(256) void k_stem_bwd_gx(GradX g, const float* __restrict__ w,
+                                                     const int16_t* __restrict__ owner,
+                                                     float* __restrict__ dx, int B, int H, int W,
+                                                     int Ho, int Wo, int tiles_x) {
+  constexpr int WIN = kStemTQ + 1, C4 = CO / 4;
+  __shared__ float4 sdy[WIN * WIN * C4];
+  __shared__ int s_live;
+  const int b = blockIdx.y;
+  const int ty = blockIdx.x / tiles_x, tx = blockIdx.x - ty * tiles_x;
+  const int Y0 = ty * kStemTQ, X0 = tx * kStemTQ;
+  const int qy = threadIdx.x / kStemTQ, qx = threadIdx.x % kStemTQ;
+  const int Y = Y0 + qy, X = X0 + qx;
+  const int Hq = H >> 1, Wq = W >> 1;
+  const bool inq = Y < Hq && X < Wq;
+  bool own = inq;
+  if (inq && owner) {
+    own = false;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int16_t* op = owner + (((long)b * H + 2 * Y + a) * W + 2 * X) * 3;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) own |= op[e] >= 0;
+    }
+  }
+  if (threadIdx.x == 0) s_live = 0;
+  __syncthreads();
+  if (own) s_live = 1;
+  __syncthreads();
+  if (!s_live) {
+    if (inq) {
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        float2* op = reinterpret_cast<float2*>(dx + (((long)b * H + 2 * Y + a) * W + 2 * X) * 3);
+        op[0] = op[1] = op[2] = make_float2(0.f, 0.f);
+      }
+    }
+    return;
+  }
+  // dy window rows Y0-1 .. Y0+15, cols X0-1 .. X0+15 (input row 2Y uses dy rows Y and Y-1)
+  for (int e = threadIdx.x; e < WIN * WIN * C4; e += 256) {
+    const int p = e / C4, c4 = e - p * C4;
+    const int wy = p / WIN, wx = p - wy * WIN;
+    const int oy = Y0 - 1 + wy, ox = X0 - 1 + wx;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) {
+      const long i = (((long)b * Ho + oy) * Wo + ox) * CO + c4 * 4;
+      v = *reinterpret_cast<const float4*>(g.da + i);
+      if (g.y) v = gx_apply4(g, gx_chan4(g, c4 * 4), v, *reinterpret_cast<const float4*>(g.y + i));
+    }
+    sdy[e] = v;
+  }
+  __syncthreads();
+  if (!inq) return;
+  float o[2][2][3];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) o[a][c][ci] = 0.f;
+#pragma unroll
+  for (int dyo = 0; dyo < 2; ++dyo) {
+#pragma unroll
+    for (int dxo = 0; dxo < 2; ++dxo) {
+      const int oy = Y - dyo, ox = X - dxo;
+      if (oy < 0 || ox < 0 || oy >= Ho || ox >= Wo) continue;
+      float gg[CO];
+      const float4* gp = sdy + ((qy - dyo + 1) * WIN + (qx - dxo + 1)) * C4;
+#pragma unroll
+      for (int c = 0; c < C4; ++c) {
+        const float4 v = gp[c];
+        gg[4 * c] = v.x; gg[4 * c + 1] = v.y; gg[4 * c + 2] = v.z; gg[4 * c + 3] = v.w;
+      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int i = dyo ? 2 : a;
+        if (dyo && a) continue;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int j = dxo ? 2 : c;
+          if (dxo && c) continue;
+#pragma unroll
+          for (int ci = 0; ci < 3; ++ci) {
+            const float* wp = w + ((i * 3 + j) * 3 + ci) * CO;
+            float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+            for (int k = 0; k < CO; k += 2) {
+              s0 = fmaf(gg[k], wp[k], s0);
+              s1 = fmaf(gg[k + 1], wp[k + 1], s1);
+            }
+            o[a][c][ci] += s0 + s1;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    float2* op = reinterpret_cast<float2*>(dx + (((long)b * H + 2 * Y + a) * W + 2 * X) * 3);
+    op[0] = make_float2(o[a][0][0], o[a][0][1]);
+    op[1] = make_float2(o[a][0][2], o[a][1][0]);
+    op[2] = make_float2(o[a][1][1], o[a][1][2]);
+  }
+}
+
 template <template <int> class Launch, class... Args>
 static void stem_dispatch(int Co, Args... args) {
   switch (Co) {
@@ -206,6 +320,30 @@ struct StemBwd {
                        Wo, acc);
   }
 };
+
+template <int CO>
+struct StemBwdGx {
+  static void go(GradX g, const float* w, const int16_t* owner, float* dx, int B, int H, int W,
+                 int Ho, int Wo, hipStream_t s) {
+    const int tx = cdiv(W / 2, kStemTQ), ty = cdiv(H / 2, kStemTQ);
+    hipLaunchKernelGGL((k_stem_bwd_gx<CO>), dim3(tx * ty, B), dim3(256), 0, s, g, w, owner, dx, B, H, W,
+                       Ho, Wo, tx);
+  }
+};
+
+bool stem_bwd_gx_supported(int Co) { return Co == 32 || Co == 40 || Co == 48; }
+
+void launch_stem_bwd_gx(GradX g, const float* w, const int16_t* owner, float* dx, int B, int H, int W,
+                        int Ho, int Wo, int Co, int pt, int pl, hipStream_t s) {
+  if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
+  switch (Co) {
+    case 32: StemBwdGx<32>::go(g, w, owner, dx, B, H, W, Ho, Wo, s); break;
+    case 40: StemBwdGx<40>::go(g, w, owner, dx, B, H, W, Ho, Wo, s); break;
+    case 48: StemBwdGx<48>::go(g, w, owner, dx, B, H, W, Ho, Wo, s); break;
+    default: throw std::invalid_argument("stem_bwd_gx: unsupported output channels");
+  }
+  PHX_LAUNCH_CHECK();
+}
 
 int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                     int Co, int pt, int pl, hipStream_t s, StatSink sink) {

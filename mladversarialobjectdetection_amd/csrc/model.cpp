@@ -501,12 +501,30 @@ void NetBuilder::plan_backward() {
       has[t] = 1;
     }
   }
+  // Residual adds: both input gradients equal the output's.  When the add is the last consumer
+  // of both inputs (nothing accumulated into them yet) and has no drop connect, both inputs take
+  // the output's gradient buffer instead of copies of it.  Later accumulations into the skip input
+  // (the block's expand conv) happen after every reader of the branch gradient (project dgrad,
+  // BN sums) in the reverse sweep.  Aliases are resolved last-op-first so chains of blocks share.
+  std::vector<char> alias(T.size(), 0);
+  std::vector<int> alias_ops;
+  for (int i = (int)prog_.ops.size() - 1; i >= 0; --i) {
+    const Op& op = prog_.ops[i];
+    if (op.t != OP_ADD || !op.bwd || op.survival > 0.f || op.in[0] == op.in[1]) continue;
+    if (op.acc[0] || op.acc[1] || alias[op.in[0]] || alias[op.in[1]]) continue;
+    alias[op.in[0]] = alias[op.in[1]] = 1;
+    alias_ops.push_back(i);
+  }
   size_t g = 0;
   for (size_t t = 0; t < T.size(); ++t) {
-    if (has[t]) {
+    if (has[t] && !alias[t]) {
       T[t].goff = (long)g;
       g += (T[t].numel() + 15) / 16 * 16;
     }
+  }
+  for (int i : alias_ops) {  // last op first: an add's output may itself alias a later add's
+    const Op& op = prog_.ops[i];
+    T[op.in[0]].goff = T[op.in[1]].goff = T[op.out].goff;
   }
   prog_.grad_floats = g;
 }
