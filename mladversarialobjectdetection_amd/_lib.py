@@ -25,7 +25,10 @@ NMETRIC = 8
 BN_LOCAL, BN_FROZEN = 0, 1
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libphx.so")
+# PHX_LIB selects another in-tree build (libphx*.so next to this file) for A/B timing runs
+_ALT = os.environ.get("PHX_LIB", "")
+LIB_PATH = os.path.join(_HERE, os.path.basename(_ALT) if _ALT.startswith("libphx") and _ALT.endswith(".so")
+                        else "libphx.so")
 
 
 class PhxError(RuntimeError):

@@ -67,6 +67,16 @@ struct Exec {
   // last writer of the BN output's gradient in the reverse sweep (GradSink)
   std::vector<char> gfused_bn;
   std::vector<int> gstat_P;                    // op id of the BN -> partial rows
+  // Level-batched heads: the per-level members of a class/box-head conv share their weights, so
+  // each (head, position) runs as ONE grouped launch (members = levels), and so do the BNs after
+  // them.  grp_of: op id -> group (-1); a group runs at its first member in the forward sweep and
+  // at its last in the reverse sweep.  Member r of a group keeps its statistics partials in
+  // region r of spart / scnt (region strides sp_region / sc_region).
+  std::vector<int> grp_of;
+  std::vector<std::vector<int>> groups;
+  size_t sp_region = 0, sc_region = 0;
+  std::vector<int> stat_region;                // tensor id -> region of its producer's partials
+  std::vector<int> gstat_region;               // BN op id -> region of its backward partials
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -272,6 +282,11 @@ struct Scope {
 // ------------------------------------------------------------------------------------------
 // executor
 // ------------------------------------------------------------------------------------------
+namespace {
+void plan_groups(Exec& E, bool local_bn);
+bool is_cls_out(const Program& P, int t);
+}  // namespace
+
 Exec& phx_ctx::exec_for(int B) {
   for (auto& e : execs)
     if (e->B == B) return *e;
@@ -365,8 +380,14 @@ Exec& phx_ctx::exec_for(int B) {
       sp_need = std::max(sp_need, (size_t)np * tz.c);
     }
   }
-  E.spart = E.alloc<float2>(sp_need);
-  E.scnt = E.alloc<float>(sc_need);
+  plan_groups(E, bn_mode == PHX_BN_LOCAL);
+  const size_t nreg = E.groups.empty() ? 1 : kMaxSeg;
+  E.sp_region = sp_need;
+  E.sc_region = sc_need;
+  E.spart = E.alloc<float2>(sp_need * nreg);
+  E.scnt = E.alloc<float>(sc_need * nreg);
+  E.stat_region.assign(P.tensors.size(), 0);
+  E.gstat_region.assign(P.ops.size(), 0);
   E.pool_amax.assign(P.ops.size(), nullptr);
   for (size_t i = 0; i < P.ops.size(); ++i)
     if (P.ops[i].t == OP_MAXPOOL) E.pool_amax[i] = E.alloc<uint8_t>(P.tensors[P.ops[i].out].numel());
@@ -508,6 +529,285 @@ GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
   return GradX{E.gptr(t), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 }
 
+// ---- level-batched heads -----------------------------------------------------------------
+bool grouping_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_GROUP");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// Members of a candidate group must be interchangeable launches: same op kind and geometry, same
+// statistics / gradient-sink wiring, no SE row scale; grouped GEMMs must not need split-K.
+bool group_uniform(const Exec& E, const std::vector<int>& v) {
+  const Program& P = E.prog;
+  const Op& a = P.ops[v[0]];
+  const int n = (int)P.ops.size();
+  auto fused_next = [&](int i) { return i + 1 < n && E.fused_bn[i + 1]; };
+  auto gfused_prev = [&](int i) { return i > 0 && E.gfused_bn[i - 1]; };
+  auto has_gx = [&](int i) {
+    const int bi = E.bn_consumer[P.ops[i].out];
+    return bi >= 0 && P.ops[bi].bwd;
+  };
+  std::vector<int> M;
+  for (int i : v) {
+    const Op& b = P.ops[i];
+    const Tensor& ti = P.tensors[b.in[0]];
+    const Tensor& to = P.tensors[b.out];
+    const Tensor& ta = P.tensors[a.in[0]];
+    const Tensor& tb = P.tensors[a.out];
+    if (b.t != a.t || b.k != a.k || b.stride != a.stride || b.nin != 1 || ti.c != ta.c || to.c != tb.c ||
+        ti.n != ta.n)
+      return false;
+    if (b.bwd != a.bwd || b.acc[0] != a.acc[0] || fused_next(i) != fused_next(v[0]) ||
+        gfused_prev(i) != gfused_prev(v[0]) || has_gx(i) != has_gx(v[0]))
+      return false;
+    if ((E.bn_of_tensor[b.in[0]] >= 0) != (E.bn_of_tensor[a.in[0]] >= 0)) return false;
+    if (E.se_of_tensor[b.in[0]] >= 0 || b.in[0] == P.input) return false;
+    if (gfused_prev(i) && P.ops[i - 1].out != b.in[0]) return false;
+    M.push_back((int)ti.rows());
+  }
+  if (a.t == OP_PW) {
+    const Tensor& ta = P.tensors[a.in[0]];
+    const Tensor& tb = P.tensors[a.out];
+    if (!gemm_group_ok(M.data(), (int)M.size(), tb.c, ta.c)) return false;  // forward
+    if (a.bwd && !gemm_group_ok(M.data(), (int)M.size(), ta.c, tb.c)) return false;  // dgrad
+  }
+  return true;
+}
+
+// Groups: convs sharing a weight tensor (the per-level copies of a head conv) and the BNs right
+// after them.  The schedule is then checked; any violation disables grouping for this executor.
+void plan_groups(Exec& E, bool local_bn) {
+  const Program& P = E.prog;
+  const int n = (int)P.ops.size();
+  E.grp_of.assign(n, -1);
+  E.groups.clear();
+  if (!grouping_enabled() || !local_bn) return;
+  std::map<long, std::vector<int>> byw;
+  for (int i = 0; i < n; ++i)
+    if ((P.ops[i].t == OP_DW || P.ops[i].t == OP_PW) && P.ops[i].w >= 0) byw[P.ops[i].w].push_back(i);
+  for (auto& kv : byw) {
+    const std::vector<int>& v = kv.second;
+    if (v.size() < 2 || v.size() > (size_t)kMaxSeg || !group_uniform(E, v)) continue;
+    const int g = (int)E.groups.size();
+    E.groups.push_back(v);
+    for (int i : v) E.grp_of[i] = g;
+    std::vector<int> bn;
+    for (int i : v)
+      if (i + 1 < n && P.ops[i + 1].t == OP_BN && P.ops[i + 1].in[0] == P.ops[i].out && E.fused_bn[i + 1] &&
+          !P.ops[i + 1].acc[0])
+        bn.push_back(i + 1);
+    if (bn.size() != v.size()) continue;
+    bool ok = true;
+    for (int b : bn)
+      ok = ok && P.ops[b].bwd == P.ops[bn[0]].bwd && E.gfused_bn[b] == E.gfused_bn[bn[0]] &&
+           P.ops[b].act == P.ops[bn[0]].act;
+    if (!ok || (P.ops[bn[0]].bwd && !E.gfused_bn[bn[0]])) continue;
+    const int gb = (int)E.groups.size();
+    E.groups.push_back(bn);
+    for (int b : bn) E.grp_of[b] = gb;
+  }
+  if (E.groups.empty()) return;
+  // schedule checks: forward position = first member, reverse position = last member
+  auto fpos = [&](int i) { return E.grp_of[i] >= 0 ? E.groups[E.grp_of[i]].front() : i; };
+  auto bpos = [&](int i) { return E.grp_of[i] >= 0 ? E.groups[E.grp_of[i]].back() : i; };
+  std::vector<int> producer(P.tensors.size(), -1);
+  for (int i = 0; i < n; ++i) producer[P.ops[i].out] = i;
+  bool ok = true;
+  for (int i = 0; i < n && ok; ++i) {
+    const Op& op = P.ops[i];
+    for (int j = 0; j < op.nin; ++j) {
+      const int p = producer[op.in[j]];
+      if (p >= 0 && (fpos(p) >= fpos(i) || (E.grp_of[i] >= 0 && E.grp_of[p] == E.grp_of[i]))) ok = false;
+    }
+    // statistics partials: producer launch immediately before its BN's finalize
+    if (op.t == OP_BN && E.fused_bn[i] && fpos(i) != fpos(i - 1) + 1) ok = false;
+    if (op.t == OP_BN && E.gfused_bn[i] && op.bwd && bpos(i + 1) != bpos(i) + 1) ok = false;
+  }
+  // reverse sweep: every consumer's backward before its producer's; writers of one gradient keep
+  // their program order and never share a launch
+  for (int i = 0; i < n && ok; ++i) {
+    if (!P.ops[i].bwd) continue;
+    for (int c = i + 1; c < n && ok; ++c) {
+      const Op& oc = P.ops[c];
+      if (!oc.bwd || (oc.t == OP_PW && is_cls_out(P, oc.out))) continue;
+      for (int j = 0; j < oc.nin; ++j) {
+        if (oc.in[j] == P.ops[i].out && bpos(c) <= bpos(i)) ok = false;
+        for (int k = 0; k < P.ops[i].nin; ++k)
+          if (oc.in[j] == P.ops[i].in[k] && (bpos(c) <= bpos(i))) ok = false;
+      }
+    }
+  }
+  if (!ok) {
+    E.grp_of.assign(n, -1);
+    E.groups.clear();
+  }
+}
+
+void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream_t s) {
+  const Program& P = E.prog;
+  const std::vector<int>& g = E.groups[gid];
+  const int n = (int)g.size();
+  const Op& o0 = P.ops[g[0]];
+  const Tensor& ti0 = P.tensors[o0.in[0]];
+  const Tensor& to0 = P.tensors[o0.out];
+  float* W = ctx->w();
+  const bool sink_on = g[0] + 1 < (int)P.ops.size() && E.fused_bn[g[0] + 1];
+  auto sink_of = [&](int r) {
+    return sink_on ? StatSink{E.spart + (size_t)r * E.sp_region, E.scnt + (size_t)r * E.sc_region, to0.c, 0}
+                   : StatSink{};
+  };
+  double fl = 0, by = 0;
+  for (int i : g) {
+    const Tensor& ti = P.tensors[P.ops[i].in[0]];
+    const Tensor& to = P.tensors[P.ops[i].out];
+    if (o0.t == OP_PW) fl += 2.0 * ti.rows() * ti.c * to.c;
+    if (o0.t == OP_DW) fl += 2.0 * to.numel() * o0.k * o0.k;
+    by += o0.t == OP_BN ? 8.0 * (double)E.stat_P[P.ops[i].in[0]] * ti.c : 4.0 * (double)(ti.numel() + to.numel());
+  }
+  if (o0.t == OP_PW) by += 4.0 * ti0.c * to0.c;
+  Scope scope(ctx, o0.t == OP_PW ? "gemm" : o0.t == OP_DW ? "dw_fwd" : "bn_stats", fl, by, s);
+  switch (o0.t) {
+    case OP_DW: {
+      DwSeg segs[kMaxSeg];
+      int nps[kMaxSeg];
+      for (int r = 0; r < n; ++r) {
+        const Op& op = P.ops[g[r]];
+        const Tensor& ti = P.tensors[op.in[0]];
+        const Tensor& to = P.tensors[op.out];
+        segs[r] = DwSeg{view(ctx, E, op.in[0], input), GradX{}, E.tptr(op.out, input), ti.h, ti.w, to.h, to.w,
+                        op.pad_t, op.pad_l, false, sink_of(r), GradSink{}};
+      }
+      launch_dw_fwd_group(segs, n, ti0.n, ti0.c, W + o0.w, o0.k, o0.stride, s, nps);
+      if (sink_on)
+        for (int r = 0; r < n; ++r) {
+          E.stat_P[P.ops[g[r]].out] = nps[r];
+          E.stat_region[P.ops[g[r]].out] = r;
+        }
+      break;
+    }
+    case OP_PW: {
+      GemmSeg segs[kMaxSeg];
+      const int mode = view(ctx, E, o0.in[0], input).mu ? 1 : 0;
+      for (int r = 0; r < n; ++r) {
+        const Op& op = P.ops[g[r]];
+        segs[r] = GemmSeg{view(ctx, E, op.in[0], input), GradX{}, op.b >= 0 ? W + op.b : nullptr,
+                          E.tptr(op.out, input), (int)P.tensors[op.in[0]].rows(), false, sink_of(r), GradSink{}};
+      }
+      const int np = gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s);
+      if (sink_on)
+        for (int r = 0; r < n; ++r) {
+          E.stat_P[P.ops[g[r]].out] = np;
+          E.stat_region[P.ops[g[r]].out] = r;
+        }
+      break;
+    }
+    case OP_BN: {
+      BnFinSeg segs[kMaxSeg];
+      for (int r = 0; r < n; ++r) {
+        const Op& op = P.ops[g[r]];
+        const int reg = E.stat_region[op.in[0]];
+        segs[r] = BnFinSeg{E.spart + (size_t)reg * E.sp_region, E.scnt + (size_t)reg * E.sc_region,
+                           E.stat_P[op.in[0]], (long)P.tensors[op.in[0]].rows(), E.slot_a[op.slot],
+                           E.slot_b[op.slot], W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar,
+                           nullptr, nullptr};
+      }
+      launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
+      break;
+    }
+    default:
+      throw std::logic_error("grouped launch of an unsupported op");
+  }
+}
+
+void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream_t s) {
+  const Program& P = E.prog;
+  const std::vector<int>& g = E.groups[gid];
+  const int n = (int)g.size();
+  const Op& o0 = P.ops[g[0]];
+  const Tensor& ti0 = P.tensors[o0.in[0]];
+  const Tensor& to0 = P.tensors[o0.out];
+  float* W = ctx->w();
+  const bool gs_on = g[0] > 0 && E.gfused_bn[g[0] - 1];
+  auto gsk_of = [&](int r) {
+    if (!gs_on) return GradSink{};
+    const Op& bn = P.ops[g[r] - 1];
+    return GradSink{E.spart + (size_t)r * E.sp_region, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input),
+                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act};
+  };
+  double fl = 0, by = 0;
+  for (int i : g) {
+    const Tensor& ti = P.tensors[P.ops[i].in[0]];
+    const Tensor& to = P.tensors[P.ops[i].out];
+    if (o0.t == OP_PW) fl += 2.0 * ti.rows() * ti.c * to.c;
+    if (o0.t == OP_DW) fl += 2.0 * to.numel() * o0.k * o0.k;
+    by += o0.t == OP_BN ? 8.0 * (double)E.gstat_P[i] * ti.c : 4.0 * (double)(ti.numel() + to.numel());
+    if (o0.t != OP_BN) {
+      const int bi = E.bn_consumer[P.ops[i].out];
+      if (bi >= 0 && P.ops[bi].bwd) by += 4.0 * (double)to.numel();
+      if (P.ops[i].acc[0]) by += 4.0 * (double)ti.numel();
+    }
+  }
+  if (o0.t == OP_PW) by += 4.0 * ti0.c * to0.c;
+  Scope scope(ctx, o0.t == OP_PW ? "gemm" : o0.t == OP_DW ? "dw_bwd" : "bn_bwd_reduce", fl, by, s);
+  switch (o0.t) {
+    case OP_DW: {
+      DwSeg segs[kMaxSeg];
+      int nps[kMaxSeg];
+      for (int r = 0; r < n; ++r) {
+        const Op& op = P.ops[g[r]];
+        const Tensor& ti = P.tensors[op.in[0]];
+        const Tensor& to = P.tensors[op.out];
+        segs[r] = DwSeg{InX{}, gview(ctx, E, op.out, input), E.gptr(op.in[0]), ti.h, ti.w, to.h, to.w, op.pad_t,
+                        op.pad_l, op.acc[0], StatSink{}, gsk_of(r)};
+      }
+      launch_dw_bwd_group(segs, n, ti0.n, ti0.c, W + o0.w, o0.k, o0.stride, s, nps);
+      if (gs_on)
+        for (int r = 0; r < n; ++r) {
+          E.gstat_P[g[r] - 1] = nps[r];
+          E.gstat_region[g[r] - 1] = r;
+        }
+      break;
+    }
+    case OP_PW: {
+      GemmSeg segs[kMaxSeg];
+      const GradX gx0 = gview(ctx, E, o0.out, input);
+      const int mode = gx0.y ? 3 : 0;
+      for (int r = 0; r < n; ++r) {
+        const Op& op = P.ops[g[r]];
+        const GradX gv = gview(ctx, E, op.out, input);
+        segs[r] = GemmSeg{InX{gv.da, nullptr, nullptr, nullptr, 0}, gv, nullptr, E.gptr(op.in[0]),
+                          (int)P.tensors[op.in[0]].rows(), op.acc[0], StatSink{}, gsk_of(r)};
+      }
+      // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
+      const int np = gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s);
+      if (gs_on)
+        for (int r = 0; r < n; ++r) {
+          E.gstat_P[g[r] - 1] = np;
+          E.gstat_region[g[r] - 1] = r;
+        }
+      break;
+    }
+    case OP_BN: {
+      if (ctx->bn_mode == PHX_BN_FROZEN) break;
+      BnFinSeg segs[kMaxSeg];
+      for (int r = 0; r < n; ++r) {
+        const int i = g[r];
+        const Op& op = P.ops[i];
+        segs[r] = BnFinSeg{E.spart + (size_t)E.gstat_region[i] * E.sp_region, nullptr, E.gstat_P[i],
+                           (long)P.tensors[op.in[0]].rows(), nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
+      }
+      launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
+      break;
+    }
+    default:
+      throw std::logic_error("grouped launch of an unsupported op");
+  }
+}
+
 // victim forward over the program (EfficientDetNet.call, efficientdet_keras.py:884-906)
 // pass: 0 first (clean) pass, 1 second (patched) pass, 2 standalone detect — with `step` and the
 // global index of the first image it keys the drop-connect draws
@@ -526,6 +826,10 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
   if (E.ndrop)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   for (size_t i = 0; i < P.ops.size(); ++i) {
+    if (E.grp_of[i] >= 0) {
+      if (E.groups[E.grp_of[i]].front() == (int)i) run_group_fwd(ctx, E, E.grp_of[i], input, s);
+      continue;
+    }
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
@@ -578,7 +882,9 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
                                  E.slot_c[op.slot], ti.c, kBnEps, s);
         else if (E.fused_bn[i])
-          launch_bn_finalize(E.spart, E.scnt, E.stat_P[op.in[0]], (long)ti.rows(), ti.c, mean, rstd,
+          launch_bn_finalize(E.spart + E.stat_region[op.in[0]] * E.sp_region,
+                             E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]],
+                             (long)ti.rows(), ti.c, mean, rstd,
                              W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
         else
           launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.gamma,
@@ -612,7 +918,10 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         break;
       }
     }
-    if (sink_on) E.stat_P[op.out] = np;
+    if (sink_on) {
+      E.stat_P[op.out] = np;
+      E.stat_region[op.out] = 0;
+    }
   }
 }
 
@@ -646,6 +955,10 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     const Op& op = P.ops[i];
     if (!op.bwd) continue;
     if (op.t == OP_PW && is_cls_out(P, op.out)) continue;  // handled by the scatter
+    if (E.grp_of[i] >= 0) {
+      if (E.groups[E.grp_of[i]].back() == i) run_group_bwd(ctx, E, E.grp_of[i], input, s);
+      continue;
+    }
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
     const float* dy = E.gptr(op.out);
@@ -708,7 +1021,8 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         // reduction only; the apply half runs in the producer's dgrad (gview)
         if (op.acc[0]) throw std::runtime_error("BN input with several consumers");
         if (!frozen && E.gfused_bn[i])
-          launch_bn_bwd_finalize(E.spart, E.gstat_P[i], (long)ti.rows(), ti.c, E.slot_d[op.slot],
+          launch_bn_bwd_finalize(E.spart + E.gstat_region[i] * E.sp_region, E.gstat_P[i], (long)ti.rows(),
+                                 ti.c, E.slot_d[op.slot],
                                  E.slot_e[op.slot], s);
         else if (!frozen)
           launch_bn_bwd_reduce(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
@@ -765,6 +1079,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     }
     if (gsk.part && np != E.gstat_P[i - 1])
       throw std::logic_error("BN backward sums: planned and launched partial counts differ");
+    if (gsk.part) E.gstat_region[i - 1] = 0;
   }
 }
 

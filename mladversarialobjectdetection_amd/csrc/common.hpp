@@ -170,6 +170,20 @@ __device__ __forceinline__ float4 gx_load4(const GradX& g, long e, int c) {
 // partials contiguously (one workgroup per channel, fp64, fixed order: bit-reproducible), then
 // writes mean / rstd / gamma*rstd and updates the moving statistics.
 // ------------------------------------------------------------------------------------------
+// members of one grouped launch (the per-level convs of a class/box head)
+constexpr int kMaxSeg = 5;
+
+// member i of a grouped launch's by-value argument array, read at constant offsets only (a
+// run-time index into kernel arguments turns every field access into a vector load)
+template <class T, int NS>
+__device__ __forceinline__ T pick_seg(const T (&arr)[NS], int i) {
+  T v = arr[0];
+#pragma unroll
+  for (int k = 1; k < NS; ++k)
+    if (i == k) v = arr[k];
+  return v;
+}
+
 struct StatSink {
   float2* part;  // [C][P] (sum, M2); nullptr = no statistics wanted
   float* cnt;    // [P]

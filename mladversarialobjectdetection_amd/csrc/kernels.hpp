@@ -57,6 +57,21 @@ int gemm_splitk_finish(const float* partial, int splits, int M, int N, const flo
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                       hipStream_t s, float* partial, GradSink gs = GradSink{});
 int gemm_dgrad_gsink_partials(int M, int N, int K);
+// Grouped GEMM: members share Bt [N][K] (weights shared across pyramid levels) and differ in A,
+// C, M and sinks.  mode as gemm2 (0 raw, 1 BN view, 3 gradient view).  No split-K: see
+// gemm_group_ok.  Returns the partial rows P written per member (the same for all).
+struct GemmSeg {
+  InX A;
+  GradX G;
+  const float* bias;
+  float* C;
+  int M;
+  bool acc;
+  StatSink sink;
+  GradSink gsk;
+};
+bool gemm_group_ok(const int* M, int n, int N, int K);
+int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
 int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
                   int Wo, int k, int stride, int pt, int pl, hipStream_t s,
@@ -66,6 +81,21 @@ int launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int 
                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s,
                   GradSink gs = GradSink{});
 int dw_bwd_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl);
+// grouped depthwise convs (same taps w, C, k, stride; per-member tensors and sinks); H, W are the
+// conv input, Ho, Wo its output; out = y (forward) or dx (backward); nps[i] = partial rows
+struct DwSeg {
+  InX x;          // forward input view
+  GradX gv;       // backward: gradient view of the conv output
+  float* out;
+  int H, W, Ho, Wo, pt, pl;
+  bool acc;       // backward: accumulate into dx
+  StatSink sink;  // forward
+  GradSink gs;    // backward
+};
+void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
+                         hipStream_t s, int* nps);
+void launch_dw_bwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
+                         hipStream_t s, int* nps);
 void launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);
 
 // ---- normalisation / elementwise (kernels_norm.hip) ---------------------------------------
@@ -79,6 +109,19 @@ void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, f
 void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
                         float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
                         float eps, hipStream_t s);
+// grouped finalize (one launch for the per-level BNs of a head conv, each its own partials)
+struct BnFinSeg {
+  const float2* part;
+  const float* cnt;  // forward only
+  int P;
+  long M;
+  float *mean, *rstd;
+  const float* gamma;
+  float *sc, *mmean, *mvar;
+  float *mdz, *mdzx;  // backward
+};
+void launch_bn_finalize_group(const BnFinSeg* segs, int n, int C, float eps, hipStream_t s);
+void launch_bn_bwd_finalize_group(const BnFinSeg* segs, int n, int C, hipStream_t s);
 // frozen BN: mean/rstd from moving statistics
 void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd,
                             const float* gamma, float* sc, int C, float eps, hipStream_t s);

@@ -19,6 +19,7 @@
 // Block order is XCD-aware: the NCG channel slices of one spatial tile are dispatched
 // back-to-back on the same XCD, so the NHWC lines they each read a 16*CG-byte piece of are L2 hits
 // for the others.
+#include <algorithm>
 #include <stdexcept>
 
 #include "kernels.hpp"
@@ -35,6 +36,32 @@ struct DwGeom {
   int rin, cin;     // staged window
   int tiles_x, ntiles, ncg;
   int per;          // work items per XCD
+};
+
+// Grouped launch: up to kMaxSeg convolutions with the same taps, kernel size, stride and channel
+// count (the per-level members of a class/box-head conv) run as one grid, blockIdx.y = member.
+struct DwFwdSeg {
+  InX x;
+  float* y;
+  DwGeom g;
+  StatSink sink;
+};
+template <int NS>  // argument slots: 1 (ordinary launch, small kernarg) or kMaxSeg
+struct DwFwdGroup {
+  DwFwdSeg s[NS];
+  const float* w;
+};
+struct DwBwdSeg {
+  GradX gv;
+  float* dx;
+  DwGeom g;
+  int acc;
+  GradSink gs;
+};
+template <int NS>
+struct DwBwdGroup {
+  DwBwdSeg s[NS];
+  const float* w;
 };
 
 // XCD-aware work split: the ntiles*ncg (tile, channel slice) items, tile-major, are cut into
@@ -224,9 +251,14 @@ __device__ __forceinline__ void dw_stats(const float4 (&acc)[RPT], unsigned vmas
 }
 
 // ---- forward: y[oy][ox] = sum_ij a[oy*S - pt + i][ox*S - pl + j] * w[i][j] ----------------
-template <int K, int S, int RPT, bool STATS>
-__global__ __launch_bounds__(256) void k_dw_fwd(InX xv, const float* __restrict__ w,
-                                                float* __restrict__ y, DwGeom g, StatSink sink) {
+template <int K, int S, int RPT, bool STATS, int NS>
+__global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS> grp) {
+  const DwFwdSeg sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
+  const InX& xv = sg.x;
+  const DwGeom& g = sg.g;
+  const StatSink& sink = sg.sink;
+  const float* __restrict__ w = grp.w;
+  float* __restrict__ y = sg.y;
   extern __shared__ float4 tile[];
   const int b = blockIdx.z;
   int tl, cgi;
@@ -313,10 +345,15 @@ __device__ __forceinline__ void dw_gsums(float4 s1, float4 s2, int lcg, int c, l
   }
 }
 
-template <int K, int S, int RPT, bool GS>
-__global__ __launch_bounds__(256) void k_dw_bwd(GradX gv, const float* __restrict__ w,
-                                                float* __restrict__ dx, DwGeom g, int acc_flag,
-                                                GradSink gsk) {
+template <int K, int S, int RPT, bool GS, int NS>
+__global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
+  const DwBwdSeg sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
+  const GradX& gv = sg.gv;
+  const DwGeom& g = sg.g;
+  const GradSink& gsk = sg.gs;
+  const int acc_flag = sg.acc;
+  const float* __restrict__ w = grp.w;
+  float* __restrict__ dx = sg.dx;
   extern __shared__ float4 tile[];
   const int b = blockIdx.z;
   int tl, cgi;
@@ -448,16 +485,33 @@ static size_t dw_lds(const DwGeom& g, int k) {
   return ((size_t)g.rin * g.cin + (k > 3 ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
 }
 
-template <int K, int S>
-static void dw_fwd_go(InX x, const float* w, float* y, int B, const DwGeom& g, StatSink sink,
-                      hipStream_t s) {
+template <int K, int S, int NS>
+static void dw_fwd_go(const DwFwdGroup<NS>& grp, int n, int B, bool stats, hipStream_t s) {
   constexpr int RPT = S == 1 ? 4 : 2;
-  sink.P = B * g.ntiles;
-  dim3 grid(8 * g.per, 1, B);
-  if (sink.part)
-    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true>), grid, dim3(256), dw_lds(g, K), s, x, w, y, g, sink);
+  int gx = 1;
+  size_t lds = 0;
+  for (int i = 0; i < n; ++i) {
+    gx = std::max(gx, 8 * grp.s[i].g.per);
+    lds = std::max(lds, dw_lds(grp.s[i].g, K));
+  }
+  dim3 grid(gx, n, B);
+  if (stats)
+    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS>), grid, dim3(256), lds, s, grp);
   else
-    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false>), grid, dim3(256), dw_lds(g, K), s, x, w, y, g, sink);
+    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS>), grid, dim3(256), lds, s, grp);
+}
+
+template <int NS>
+static void dw_fwd_dispatch(const DwFwdGroup<NS>& grp, int n, int B, bool stats, int k, int stride,
+                            hipStream_t s) {
+  for (int i = 0; i < n; ++i)
+    if (dw_lds(grp.s[i].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
+  if (k == 3 && stride == 1) dw_fwd_go<3, 1, NS>(grp, n, B, stats, s);
+  else if (k == 3 && stride == 2) dw_fwd_go<3, 2, NS>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 1) dw_fwd_go<5, 1, NS>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 2) dw_fwd_go<5, 2, NS>(grp, n, B, stats, s);
+  else throw std::invalid_argument("dw: unsupported kernel/stride");
+  PHX_LAUNCH_CHECK();
 }
 
 int dw_stat_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl) {
@@ -470,26 +524,58 @@ int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, i
                   int k, int stride, int pt, int pl, hipStream_t s, StatSink sink) {
   if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
   const int rpt = stride == 1 ? 4 : 2;
-  DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false);
-  if (dw_lds(g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  if (k == 3 && stride == 1) dw_fwd_go<3, 1>(x, w, y, B, g, sink, s);
-  else if (k == 3 && stride == 2) dw_fwd_go<3, 2>(x, w, y, B, g, sink, s);
-  else if (k == 5 && stride == 1) dw_fwd_go<5, 1>(x, w, y, B, g, sink, s);
-  else if (k == 5 && stride == 2) dw_fwd_go<5, 2>(x, w, y, B, g, sink, s);
-  else throw std::invalid_argument("dw: unsupported kernel/stride");
-  PHX_LAUNCH_CHECK();
-  return B * g.ntiles;
+  DwFwdGroup<1> grp{};
+  grp.w = w;
+  grp.s[0] = DwFwdSeg{x, y, dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false), sink};
+  grp.s[0].sink.P = B * grp.s[0].g.ntiles;
+  dw_fwd_dispatch(grp, 1, B, sink.part != nullptr, k, stride, s);
+  return B * grp.s[0].g.ntiles;
 }
 
-template <int K, int S>
-static void dw_bwd_go(GradX dy, const float* w, float* dx, int B, const DwGeom& g, bool acc,
-                      GradSink gs, hipStream_t s) {
-  dim3 grid(8 * g.per, 1, B);
-  gs.P = B * g.ntiles;
-  if (gs.part)
-    hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true>), grid, dim3(256), dw_lds(g, K), s, dy, w, dx, g, acc ? 1 : 0, gs);
+void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
+                         hipStream_t s, int* nps) {
+  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
+  if (n < 1 || n > kMaxSeg) throw std::runtime_error("dw group: bad member count");
+  const int rpt = stride == 1 ? 4 : 2;
+  DwFwdGroup<kMaxSeg> grp{};
+  grp.w = w;
+  const bool stats = segs[0].sink.part != nullptr;
+  for (int i = 0; i < n; ++i) {
+    const DwSeg& d = segs[i];
+    if ((d.sink.part != nullptr) != stats) throw std::runtime_error("dw group: members differ in sinks");
+    grp.s[i] = DwFwdSeg{d.x, d.out, dw_plan(d.H, d.W, C, d.Ho, d.Wo, d.pt, d.pl, k, stride, rpt, false), d.sink};
+    grp.s[i].sink.P = B * grp.s[i].g.ntiles;
+    nps[i] = grp.s[i].sink.P;
+  }
+  dw_fwd_dispatch(grp, n, B, stats, k, stride, s);
+}
+
+template <int K, int S, int NS>
+static void dw_bwd_go(const DwBwdGroup<NS>& grp, int n, int B, bool gsums, hipStream_t s) {
+  int gx = 1;
+  size_t lds = 0;
+  for (int i = 0; i < n; ++i) {
+    gx = std::max(gx, 8 * grp.s[i].g.per);
+    lds = std::max(lds, dw_lds(grp.s[i].g, K));
+  }
+  dim3 grid(gx, n, B);
+  if (gsums)
+    hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS>), grid, dim3(256), lds, s, grp);
   else
-    hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false>), grid, dim3(256), dw_lds(g, K), s, dy, w, dx, g, acc ? 1 : 0, gs);
+    hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false, NS>), grid, dim3(256), lds, s, grp);
+}
+
+template <int NS>
+static void dw_bwd_dispatch(const DwBwdGroup<NS>& grp, int n, int B, bool gsums, int k, int stride,
+                            hipStream_t s) {
+  for (int i = 0; i < n; ++i)
+    if (dw_lds(grp.s[i].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
+  if (k == 3 && stride == 1) dw_bwd_go<3, 1, NS>(grp, n, B, gsums, s);
+  else if (k == 3 && stride == 2) dw_bwd_go<3, 2, NS>(grp, n, B, gsums, s);
+  else if (k == 5 && stride == 1) dw_bwd_go<5, 1, NS>(grp, n, B, gsums, s);
+  else if (k == 5 && stride == 2) dw_bwd_go<5, 2, NS>(grp, n, B, gsums, s);
+  else throw std::invalid_argument("dw: unsupported kernel/stride");
+  PHX_LAUNCH_CHECK();
 }
 
 int dw_bwd_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl) {
@@ -500,15 +586,30 @@ int dw_bwd_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int strid
 int launch_dw_bwd(GradX dy, const float* w, float* dx, int B, int H, int W, int C, int Ho,
                   int Wo, int k, int stride, int pt, int pl, bool acc, hipStream_t s, GradSink gs) {
   if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
-  DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, true);
-  if (dw_lds(g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  if (k == 3 && stride == 1) dw_bwd_go<3, 1>(dy, w, dx, B, g, acc, gs, s);
-  else if (k == 3 && stride == 2) dw_bwd_go<3, 2>(dy, w, dx, B, g, acc, gs, s);
-  else if (k == 5 && stride == 1) dw_bwd_go<5, 1>(dy, w, dx, B, g, acc, gs, s);
-  else if (k == 5 && stride == 2) dw_bwd_go<5, 2>(dy, w, dx, B, g, acc, gs, s);
-  else throw std::invalid_argument("dw: unsupported kernel/stride");
-  PHX_LAUNCH_CHECK();
-  return B * g.ntiles;
+  DwBwdGroup<1> grp{};
+  grp.w = w;
+  grp.s[0] = DwBwdSeg{dy, dx, dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, true), acc ? 1 : 0, gs};
+  grp.s[0].gs.P = B * grp.s[0].g.ntiles;
+  dw_bwd_dispatch(grp, 1, B, gs.part != nullptr, k, stride, s);
+  return B * grp.s[0].g.ntiles;
+}
+
+void launch_dw_bwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
+                         hipStream_t s, int* nps) {
+  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
+  if (n < 1 || n > kMaxSeg) throw std::runtime_error("dw group: bad member count");
+  DwBwdGroup<kMaxSeg> grp{};
+  grp.w = w;
+  const bool gsums = segs[0].gs.part != nullptr;
+  for (int i = 0; i < n; ++i) {
+    const DwSeg& d = segs[i];
+    if ((d.gs.part != nullptr) != gsums) throw std::runtime_error("dw group: members differ in sinks");
+    grp.s[i] = DwBwdSeg{d.gv, d.out, dw_plan(d.H, d.W, C, d.Ho, d.Wo, d.pt, d.pl, k, stride, 4, true),
+                        d.acc ? 1 : 0, d.gs};
+    grp.s[i].gs.P = B * grp.s[i].g.ntiles;
+    nps[i] = grp.s[i].gs.P;
+  }
+  dw_bwd_dispatch(grp, n, B, gsums, k, stride, s);
 }
 
 }  // namespace phx

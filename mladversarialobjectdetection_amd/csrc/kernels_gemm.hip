@@ -23,7 +23,11 @@
 //    registers (two passes, xor-32 shuffle), merged across the WM waves in LDS and folded across
 //    the workgroup's tiles (Chan), one partial row per workgroup.
 //  * Split-K (blockIdx.z) writes fp32 partial slabs reduced by k_gemm_splitk_reduce(_stats).
+//  * Grouped launch: up to kMaxSeg GEMMs with the same B operand, N and K but their own A, C, M and
+//    statistics sinks (the per-level members of a class/box-head conv, whose weights are shared
+//    across pyramid levels) run as one grid; blockIdx.z = segment * splits + split.
 #include <algorithm>
+#include <vector>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -46,6 +50,14 @@ struct Gemm2Args {
   StatSink sink;
   int mtiles;
   GradSink gsk;
+};
+
+// NS = argument slots: 1 for ordinary launches (small kernarg: ~1 us per launch is at stake),
+// kMaxSeg for grouped ones
+template <int NS>
+struct Gemm2Group {
+  Gemm2Args a[NS];
+  int n;
 };
 
 template <int WM, int TM, int TN, int MODE>
@@ -139,8 +151,12 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE>& r, cons
 }
 
 // SK: 0 plain, 1 StatSink (BN statistics of C), 2 GradSink (BN-backward sums of a dgrad's C)
-template <int WM, int TM, int TN, int MODE, int SK>
-__global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
+template <int WM, int TM, int TN, int MODE, int SK, int NS>
+__global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
+  const int zper = NS == 1 ? (int)gridDim.z : (int)gridDim.z / grp.n;
+  const int seg = NS == 1 ? 0 : (int)blockIdx.z / zper;
+  const int zs = (int)blockIdx.z - seg * zper;
+  const Gemm2Args a = pick_seg(grp.a, seg);
   constexpr bool STATS = SK == 1;
   using P = G2<WM, TM, TN, MODE>;
   constexpr int WN = P::WN, BM = P::BM, BN = P::BN, BK = P::BK, LD = P::LD;
@@ -151,11 +167,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Args a) {
   const int wm = wave % WM, wn = wave / WM;
   const int r32 = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * BN;
-  const int kbeg = blockIdx.z * a.kslice;
+  const int kbeg = zs * a.kslice;
   const int kend = min(a.K, kbeg + a.kslice);
   const int ksteps = (kend - kbeg + BK - 1) / BK;
   const bool split = a.partial != nullptr;
-  float* out = split ? a.partial + (long)blockIdx.z * a.M * a.N : a.C;
+  float* out = split ? a.partial + (long)zs * a.M * a.N : a.C;
 
   // running statistics of this workgroup's columns (wave wm == 0, lanes < 32)
   // (GradSink: smean = running sum dz, sm2 = running sum dz*xhat)
@@ -380,23 +396,23 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
   return p;
 }
 
-template <int WM, int TM, int TN, int MODE, int SK>
-static void g2_go(dim3 g, hipStream_t s, const Gemm2Args& a) {
-  hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK>), g, dim3(256), 0, s, a);
+template <int WM, int TM, int TN, int MODE, int SK, int NS>
+static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a) {
+  hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS>), g, dim3(256), 0, s, a);
 }
 
 // sk: 1 forward statistics (modes 0-2), 2 BN-backward sums (dgrad modes 0, 3)
-template <int WM, int TM, int TN>
-static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a) {
+template <int WM, int TM, int TN, int NS>
+static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a) {
   switch (mode) {
     case 0:
-      if (sk == 1) g2_go<WM, TM, TN, 0, 1>(g, s, a);
-      else if (sk == 2) g2_go<WM, TM, TN, 0, 2>(g, s, a);
-      else g2_go<WM, TM, TN, 0, 0>(g, s, a);
+      if (sk == 1) g2_go<WM, TM, TN, 0, 1, NS>(g, s, a);
+      else if (sk == 2) g2_go<WM, TM, TN, 0, 2, NS>(g, s, a);
+      else g2_go<WM, TM, TN, 0, 0, NS>(g, s, a);
       break;
-    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1>(g, s, a) : g2_go<WM, TM, TN, 1, 0>(g, s, a); break;
-    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1>(g, s, a) : g2_go<WM, TM, TN, 2, 0>(g, s, a); break;
-    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2>(g, s, a) : g2_go<WM, TM, TN, 3, 0>(g, s, a); break;
+    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1, NS>(g, s, a) : g2_go<WM, TM, TN, 1, 0, NS>(g, s, a); break;
+    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1, NS>(g, s, a) : g2_go<WM, TM, TN, 2, 0, NS>(g, s, a); break;
+    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2, NS>(g, s, a) : g2_go<WM, TM, TN, 3, 0, NS>(g, s, a); break;
   }
 }
 
@@ -415,21 +431,73 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   if (gs && (p.splits > 1 || mode == 1 || mode == 2)) throw std::runtime_error("gemm: unsupported GradSink");
   gsk.P = p.gx;
   const int sk = kstats ? 1 : gs ? 2 : 0;
-  Gemm2Args a{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
-              p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles, gsk};
+  Gemm2Group<1> a{};
+  a.n = 1;
+  a.a[0] = Gemm2Args{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
+                     p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles, gsk};
   dim3 g(p.gx, p.gy, p.splits);
   const int key = p.wm * 100 + p.tm * 10 + p.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1>(mode, sk, g, s, a); break;
-    case 412: g2_launch_cfg<4, 1, 2>(mode, sk, g, s, a); break;
-    case 413: g2_launch_cfg<4, 1, 3>(mode, sk, g, s, a); break;
-    case 415: g2_launch_cfg<4, 1, 5>(mode, sk, g, s, a); break;
-    case 222: g2_launch_cfg<2, 2, 2>(mode, sk, g, s, a); break;
+    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a); break;
+    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a); break;
+    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a); break;
+    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a); break;
+    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
   if (p.splits > 1) return gemm_splitk_finish(partial, p.splits, M, N, bias, C, acc, sink, s);
   return p.gx;
+}
+
+bool gemm_group_ok(const int* M, int n, int N, int K) {
+  if (n < 1 || n > kMaxSeg || gemm_impl_for(N) != 2) return false;
+  for (int i = 0; i < n; ++i)
+    if (plan_gemm2(M[i], N, K, gemm2_target_wgs()).splits != 1) return false;
+  return true;
+}
+
+int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s) {
+  std::vector<int> M(n);
+  for (int i = 0; i < n; ++i) M[i] = segs[i].M;
+  if (!gemm_group_ok(M.data(), n, N, K)) throw std::runtime_error("gemm group: unsupported shapes");
+  if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
+  const bool stats = segs[0].sink.part != nullptr, gs = segs[0].gsk.part != nullptr;
+  if (stats && (mode == 3 || (N & 3))) throw std::runtime_error("gemm group: unsupported statistics");
+  if (gs && (mode == 1 || mode == 2)) throw std::runtime_error("gemm group: unsupported GradSink");
+  Gemm2Group<kMaxSeg> a{};
+  a.n = n;
+  int gx = 1;
+  Gemm2Plan p0{};
+  for (int i = 0; i < n; ++i) {
+    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs());
+    if (i == 0) p0 = p;
+    gx = std::max(gx, p.gx);
+  }
+  for (int i = 0; i < n; ++i) {
+    const GemmSeg& g = segs[i];
+    if ((g.sink.part != nullptr) != stats || (g.gsk.part != nullptr) != gs)
+      throw std::runtime_error("gemm group: members differ in their sinks");
+    StatSink sink = g.sink;
+    sink.P = gx;
+    GradSink gsk = g.gsk;
+    gsk.P = gx;
+    a.a[i] = Gemm2Args{g.A, g.G, Bt, g.bias, g.C, g.M, N, K, g.acc ? 1 : 0, nullptr, 1, K, nullptr, sink,
+                       cdiv(g.M, p0.wm * p0.tm * 32), gsk};
+  }
+  const int sk = stats ? 1 : gs ? 2 : 0;
+  dim3 grid(gx, p0.gy, n);
+  const int key = p0.wm * 100 + p0.tm * 10 + p0.tn;
+  switch (key) {
+    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a); break;
+    default: throw std::runtime_error("gemm2: no kernel for this configuration");
+  }
+  PHX_LAUNCH_CHECK();
+  return gx;
 }
 
 }  // namespace phx

@@ -303,9 +303,26 @@ void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, f
 // channel.  Forward (StatSink): partial = (sum, M2) of cnt[p] rows, folded as S1 = sum x and
 // S2 = sum x^2 = M2 + sum^2/n.  Backward (GradSink): partial = (sum dz, sum dz*xhat), plain sums.
 // Fixed summation order: bit-reproducible run to run.
-template <bool BWD, class E>
-__global__ __launch_bounds__(256) void k_bn_finalize(const float2* __restrict__ part,
-                                                     const float* __restrict__ cnt, int P, E e) {
+// grouped: blockIdx.y = member (the per-level BNs of a head conv), each with its own partials
+template <class E>
+struct FinSeg {
+  const float2* part;
+  const float* cnt;
+  int P;
+  E e;
+};
+template <class E, int NS>  // NS argument slots: 1 (ordinary launch) or kMaxSeg
+struct FinGroup {
+  FinSeg<E> s[NS];
+};
+
+template <bool BWD, class E, int NS>
+__global__ __launch_bounds__(256) void k_bn_finalize(FinGroup<E, NS> grp) {
+  const FinSeg<E> sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
+  const float2* __restrict__ part = sg.part;
+  const float* __restrict__ cnt = sg.cnt;
+  const int P = sg.P;
+  const E& e = sg.e;
   __shared__ double r1[256], r2[256];
   const int c = blockIdx.x, t = threadIdx.x;
   const float2* pc = part + (long)c * P;
@@ -349,8 +366,21 @@ void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int
                         float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
                         float eps, hipStream_t s) {
   // StatsEpi's shift is 0 here: S1, S2 are plain sums of x and x^2 in fp64
-  StatsEpi e{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps};
-  hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi>), dim3(C), dim3(256), 0, s, part, cnt, P, e);
+  FinGroup<StatsEpi, 1> g{};
+  g.s[0] = FinSeg<StatsEpi>{part, cnt, P, StatsEpi{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps}};
+  hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi, 1>), dim3(C), dim3(256), 0, s, g);
+  PHX_LAUNCH_CHECK();
+}
+
+void launch_bn_finalize_group(const BnFinSeg* segs, int n, int C, float eps, hipStream_t s) {
+  if (n < 1 || n > kMaxSeg) throw std::runtime_error("bn finalize group: bad member count");
+  FinGroup<StatsEpi, kMaxSeg> g{};
+  for (int i = 0; i < n; ++i) {
+    const BnFinSeg& d = segs[i];
+    g.s[i] = FinSeg<StatsEpi>{d.part, d.cnt, d.P,
+                              StatsEpi{nullptr, d.M, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps}};
+  }
+  hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
   PHX_LAUNCH_CHECK();
 }
 
@@ -502,8 +532,18 @@ struct BwdEpi2 {
 
 void launch_bn_bwd_finalize(const float2* part, int P, long M, int C, float* mdz, float* mdzx,
                             hipStream_t s) {
-  hipLaunchKernelGGL((k_bn_finalize<true, BwdEpi2>), dim3(C), dim3(256), 0, s, part, nullptr, P,
-                     BwdEpi2{M, mdz, mdzx});
+  FinGroup<BwdEpi2, 1> g{};
+  g.s[0] = FinSeg<BwdEpi2>{part, nullptr, P, BwdEpi2{M, mdz, mdzx}};
+  hipLaunchKernelGGL((k_bn_finalize<true, BwdEpi2, 1>), dim3(C), dim3(256), 0, s, g);
+  PHX_LAUNCH_CHECK();
+}
+
+void launch_bn_bwd_finalize_group(const BnFinSeg* segs, int n, int C, hipStream_t s) {
+  if (n < 1 || n > kMaxSeg) throw std::runtime_error("bn finalize group: bad member count");
+  FinGroup<BwdEpi2, kMaxSeg> g{};
+  for (int i = 0; i < n; ++i)
+    g.s[i] = FinSeg<BwdEpi2>{segs[i].part, nullptr, segs[i].P, BwdEpi2{segs[i].M, segs[i].mdz, segs[i].mdzx}};
+  hipLaunchKernelGGL((k_bn_finalize<true, BwdEpi2, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
   PHX_LAUNCH_CHECK();
 }
 

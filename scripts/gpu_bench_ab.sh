@@ -1,0 +1,9 @@
+# GPU: bench line only (no tests) under several environment settings, for A/B timing
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+for setting in "$@"; do
+  env $setting timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile > gpurun_out/bench_ab.json 2> gpurun_out/bench_ab.err
+  rc=$?; echo "[$setting] rc=$rc $(python -c 'import json;d=json.load(open("gpurun_out/bench_ab.json"));print(d["value"],d["ms_per_step"])')"
+  [ $rc -eq 0 ] || exit $rc
+done
