@@ -81,11 +81,11 @@ def cpu_baseline(size, batch, threads, budget_s=15.0):
 
 # kernels behind each launch-group kind of the library profiler (for the rocprof cross-check)
 KIND_KERNELS = {
-    "gemm": "k_gemm<NT,WM,MODE> + k_gemm_splitk_reduce",
-    "bn_stats": "k_colred_part<StatsAcc> + k_colred_final<StatsEpi>",
-    "bn_bwd_reduce": "k_colred_part<BwdAcc> + k_colred_final<BwdEpi2>",
-    "dw_fwd": "k_dw_fwd<K,S,RPT>",
-    "dw_bwd": "k_dw_bwd<K,S,RPT>",
+    "gemm": "k_gemm2<WM,TM,TN,MODE,SK,NS> (+ k_gemm<NT,WM,MODE,SK> for N<=16, k_gemm_splitk_reduce(_stats))",
+    "bn_stats": "k_bn_finalize<false,StatsEpi,NS> (statistics partials from the producer's epilogue)",
+    "bn_bwd_reduce": "k_bn_finalize<true,BwdEpi2,NS> (BN-backward sums from the consumer's dgrad)",
+    "dw_fwd": "k_dw_fwd<K,S,RPT,STATS,NS>",
+    "dw_bwd": "k_dw_bwd<K,S,RPT,GS,NS>",
 }
 
 
