@@ -130,6 +130,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--model", default="efficientdet-d0",
+                    help="victim (the headline metric is D0; others for the secondary configs)")
     args = ap.parse_args()
 
     from mladversarialobjectdetection_amd import distributed as ddp
@@ -141,7 +143,7 @@ def main():
 
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker, _pad_boxes
     B, S = args.batch, args.image_size
-    victim = EfficientDetVictim("efficientdet-d0", "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
+    victim = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
                                 device=local)
     att = PatchAttacker(victim, seed=7, device=dev)
     ws_gb = victim.ctx.workspace_bytes(B) / 1e9
@@ -186,13 +188,14 @@ def main():
         step_roof["frac_of_roofline"] = round(roof_ms / (1e3 * elapsed / args.steps), 4)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "efficientdet-d0":
         threads = min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(S, args.cpu_batch, threads)
 
     if rank == 0:
         line = {
-            "metric": "patch-opt images/sec (EffDet-D0 512px fwd+bwd)",
+            "metric": "patch-opt images/sec (EffDet-D0 512px fwd+bwd)" if args.model == "efficientdet-d0"
+                      else f"patch-opt images/sec ({args.model} {S}px fwd+bwd)",
             "value": round(images_per_s, 3),
             "unit": "images/s",
             "n_gpus": world,
@@ -204,7 +207,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (U(-1,1) images, 1-3 injected person boxes/image, synthetic D0 weights)",
-            "config": {"workload": f"C{2 if world == 1 else 3}: EfficientDet-D0 patch attack {S}x{S}, "
+            "config": {"workload": (f"C{2 if world == 1 else 3}: EfficientDet-D0" if args.model == "efficientdet-d0"
+                                    else args.model) + f" patch attack {S}x{S}, "
                                    f"{B} images/GPU, bn=local", "global_batch": world * B, "image_size": S,
                        "workspace_gb_per_gpu": round(ws_gb, 3),
                        "parallelism": f"dp{world}"},

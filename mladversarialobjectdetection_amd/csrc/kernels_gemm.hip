@@ -393,6 +393,14 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
   p.splits = (K + p.kslice - 1) / p.kslice;
   const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
   p.gx = (int)std::min<long>(p.mtiles, want);
+  // with several N tiles, a multiple of 8 workgroups along M puts the gy workgroups that stream
+  // the same A rows on one XCD (dispatch is round-robin over the 8 XCDs), so A is read from HBM
+  // once per XCD L2 instead of once per N tile
+  static const bool xcd8 = [] {
+    const char* e = std::getenv("PHX_GX8");
+    return !(e && e[0] == '0');
+  }();
+  if (xcd8 && p.gy > 1 && p.gx > 8) p.gx = p.gx / 8 * 8;
   return p;
 }
 

@@ -627,6 +627,23 @@ constexpr int kSeThreads = 1024;
 __device__ __forceinline__ void se_fold(const double* __restrict__ part, int chunks, int C, int b,
                                         double* red, float* v) {
   const int t = threadIdx.x;
+  if (C > kSeThreads / 4) {
+    // wide layers: passes of 256 channels, 4 chunk groups per pass (coalesced along c)
+    const int cl = t & 255, grp = t >> 8;
+    for (int c0 = 0; c0 < C; c0 += 256) {
+      const int c = c0 + cl;
+      double s = 0.0;
+      if (c < C) {
+#pragma unroll 4
+        for (int k = grp; k < chunks; k += 4) s += part[(((long)b * chunks + k) * C + c) * 2];
+      }
+      red[grp * 256 + cl] = s;
+      __syncthreads();
+      if (t < 256 && c < C) v[c] = (float)(((red[cl] + red[256 + cl]) + red[512 + cl]) + red[768 + cl]);
+      __syncthreads();
+    }
+    return;
+  }
   if (2 * C <= kSeThreads) {
     const int ng = min(chunks, kSeThreads / C);
     const int c = t % C, grp = t / C;
