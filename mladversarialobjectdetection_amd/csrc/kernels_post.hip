@@ -141,7 +141,6 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   __shared__ float sel_box[PHX_MAX_OUT_DEV][4];
   __shared__ float sel_score[PHX_MAX_OUT_DEV];
   __shared__ int s_nsel;
-  __shared__ float red_s[kNmsThreads];
   __shared__ int red_i[kNmsThreads];
   __shared__ int s_done;
 
@@ -181,58 +180,87 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   if (t == 0) { s_nsel = 0; s_done = 0; }
   __syncthreads();
 
-  // 2. lazy priority-queue loop
+  // 2. lazy priority-queue loop.  Lane t owns candidates t, t+256, ... and caches the best
+  //    (score desc, index asc) of its subset; only the owner of the candidate an iteration changed
+  //    rescans.  The decay factors of the selections since the candidate's last visit are computed
+  //    by one wave in parallel, then applied newest-first in order by one lane (same product, same
+  //    early exit as the sequential rule).
+  auto better = [](float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); };
+  float myv = -INFINITY;
+  int myi = 0x7fffffff;
+  for (int i = t; i < n; i += kNmsThreads) {
+    const float v = ws[i];
+    if (better(v, i, myv, myi)) { myv = v; myi = i; }
+  }
+  __shared__ float wv_s[kNmsThreads / 64];
+  __shared__ int wv_i[kNmsThreads / 64];
+  __shared__ float fac[PHX_MAX_OUT_DEV];
+  __shared__ int s_c, s_from;
+  __shared__ float s_orig;
+  const int lane = t & 63, wave = t >> 6;
   while (true) {
     if (s_nsel >= max_out) break;
-    // argmax of (score desc, index asc) over alive candidates (alive <=> score > thresh;
-    // removed candidates are marked with -inf)
-    float best = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int i = t; i < n; i += kNmsThreads) {
-      float v = ws[i];
-      if (v > best || (v == best && i < bi)) { best = v; bi = i; }
+    float v = myv;
+    int i = myi;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float v2 = __shfl_xor(v, o);
+      const int i2 = __shfl_xor(i, o);
+      if (better(v2, i2, v, i)) { v = v2; i = i2; }
     }
-    red_s[t] = best;
-    red_i[t] = bi;
+    if (lane == 0) { wv_s[wave] = v; wv_i[wave] = i; }
     __syncthreads();
-    for (int off = kNmsThreads / 2; off > 0; off >>= 1) {
-      if (t < off) {
-        float v = red_s[t + off];
-        int j = red_i[t + off];
-        if (v > red_s[t] || (v == red_s[t] && j < red_i[t])) { red_s[t] = v; red_i[t] = j; }
-      }
-      __syncthreads();
-    }
     if (t == 0) {
-      float sc = red_s[0];
-      int c = red_i[0];
-      if (!(sc > score_thresh) || c == 0x7fffffff) {
+      float bv = wv_s[0];
+      int bi = wv_i[0];
+      for (int w = 1; w < kNmsThreads / 64; ++w)
+        if (better(wv_s[w], wv_i[w], bv, bi)) { bv = wv_s[w]; bi = wv_i[w]; }
+      if (!(bv > score_thresh) || bi == 0x7fffffff) {
         s_done = 1;
       } else {
-        const float orig = sc;
-        const float* cb = bb + (long)wi[c] * 4;
-        const int nsel = s_nsel;
-        for (int j = nsel - 1; j >= wb[c]; --j) {
-          float sim = tf_iou(cb, sel_box[j]);
-          sc *= expf(scale * sim * sim);
-          if (sc <= score_thresh) break;
-        }
-        wb[c] = nsel;
-        if (sc == orig) {
-          sel_box[nsel][0] = cb[0]; sel_box[nsel][1] = cb[1];
-          sel_box[nsel][2] = cb[2]; sel_box[nsel][3] = cb[3];
-          sel_score[nsel] = sc;
-          s_nsel = nsel + 1;
-          ws[c] = -INFINITY;
-        } else if (sc > score_thresh) {
-          ws[c] = sc;
-        } else {
-          ws[c] = -INFINITY;
-        }
+        s_c = bi;
+        s_orig = bv;
+        s_from = wb[bi];
       }
     }
     __syncthreads();
     if (s_done) break;
+    const int c = s_c, from = s_from, nsel = s_nsel;
+    const float* cb = bb + (long)wi[c] * 4;
+    if (wave == 0)
+      for (int j = from + lane; j < nsel; j += 64) {
+        const float sim = tf_iou(cb, sel_box[j]);
+        fac[j] = expf(scale * sim * sim);
+      }
+    __syncthreads();
+    if (t == 0) {
+      const float orig = s_orig;
+      float sc = orig;
+      for (int j = nsel - 1; j >= from; --j) {
+        sc *= fac[j];
+        if (sc <= score_thresh) break;
+      }
+      wb[c] = nsel;
+      if (sc == orig) {
+        sel_box[nsel][0] = cb[0]; sel_box[nsel][1] = cb[1];
+        sel_box[nsel][2] = cb[2]; sel_box[nsel][3] = cb[3];
+        sel_score[nsel] = sc;
+        s_nsel = nsel + 1;
+        ws[c] = -INFINITY;
+      } else if (sc > score_thresh) {
+        ws[c] = sc;
+      } else {
+        ws[c] = -INFINITY;
+      }
+    }
+    __syncthreads();
+    if (t == c % kNmsThreads) {
+      myv = -INFINITY;
+      myi = 0x7fffffff;
+      for (int k = t; k < n; k += kNmsThreads) {
+        const float vv = ws[k];
+        if (better(vv, k, myv, myi)) { myv = vv; myi = k; }
+      }
+    }
   }
   __syncthreads();
   // 3. outputs: padded to max_out, boxes clipped to [0, image_size] (postprocess.py:61-64)
