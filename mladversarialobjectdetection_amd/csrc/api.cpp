@@ -53,6 +53,8 @@ struct Exec {
   float* se_g = nullptr;                       // SE backward scratch
   float* gpart = nullptr;                      // split-K GEMM partial slabs
   std::vector<int> se_of_tensor;               // tensor id -> SE op index producing it (-1)
+  // BiFPN node fuse folded into the depthwise conv after it (computed on load, never written)
+  std::vector<char> fuse_folded;               // op id of the fuse -> 1
   std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
   std::vector<int> bn_consumer;                // tensor id -> BN op index reading it (-1)
   std::vector<float*> slot_d, slot_e;          // BN backward: mean(dz), mean(dz*xhat)
@@ -381,6 +383,24 @@ Exec& phx_ctx::exec_for(int B) {
     }
   }
   plan_groups(E, bn_mode == PHX_BN_LOCAL);
+  E.fuse_folded.assign(P.ops.size(), 0);
+  {
+    static const bool fold = [] {
+      const char* e = std::getenv("PHX_FOLD");
+      return !(e && e[0] == '0');
+    }();
+    std::vector<int> nuse(P.tensors.size(), 0);
+    for (const Op& op : P.ops)
+      for (int j = 0; j < op.nin; ++j) ++nuse[op.in[j]];
+    for (size_t i = 0; fold && i + 1 < P.ops.size(); ++i) {
+      const Op& f = P.ops[i];
+      const Op& d = P.ops[i + 1];
+      if (f.t != OP_FUSE || d.t != OP_DW || d.in[0] != f.out || nuse[f.out] != 1) continue;
+      if (d.k != 3 || d.stride != 1 || E.grp_of[i + 1] >= 0 || P.tensors[f.out].c % 4) continue;
+      if (i + 2 < P.ops.size() && E.fused_bn[i + 2]) continue;
+      E.fuse_folded[i] = 1;
+    }
+  }
   const size_t nreg = E.groups.empty() ? 1 : kMaxSeg;
   E.sp_region = sp_need;
   E.sc_region = sc_need;
@@ -830,6 +850,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
       if (E.groups[E.grp_of[i]].front() == (int)i) run_group_fwd(ctx, E, E.grp_of[i], input, s);
       continue;
     }
+    if (E.fuse_folded[i]) continue;  // computed by the depthwise conv that follows
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
@@ -871,6 +892,20 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         break;
       }
       case OP_DW:
+        if (i > 0 && E.fuse_folded[i - 1]) {
+          const Op& f = P.ops[i - 1];
+          FuseView fv{};
+          fv.nin = f.nin;
+          for (int k = 0; k < f.nin; ++k) {
+            fv.x[k] = view(ctx, E, f.in[k], input);
+            fv.w[k] = f.wsm[k] >= 0 ? W + f.wsm[k] : nullptr;
+          }
+          fv.method = f.fuse_method;
+          fv.act = f.act;
+          launch_dw_fwd_fused(fv, W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
+                              op.pad_l, s);
+          break;
+        }
         np = launch_dw_fwd(view(ctx, E, op.in[0], input), W + op.w, y, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k,
                            op.stride, op.pad_t, op.pad_l, s, sink);
         break;

@@ -170,6 +170,45 @@ __device__ __forceinline__ float4 gx_load4(const GradX& g, long e, int c) {
 // partials contiguously (one workgroup per channel, fp64, fixed order: bit-reproducible), then
 // writes mean / rstd / gamma*rstd and updates the moving statistics.
 // ------------------------------------------------------------------------------------------
+// BiFPN node fuse (efficientdet_keras.py:91-110): y = act(sum_i x_i * w_i / (sum_j w_j + 1e-4))
+// with w = relu(wsm) (fastattn, method 0) or act(sum_i x_i) (method 1); inputs through InX views
+struct FuseView {
+  InX x[3];
+  int nin;
+  const float* w[3];
+  int method, act;
+};
+
+__device__ __forceinline__ void fuse_weights(const float* w0, const float* w1, const float* w2,
+                                             int nin, int method, float* wv, float* den) {
+  if (method == 0) {
+    wv[0] = fmaxf(w0[0], 0.f);
+    wv[1] = fmaxf(w1[0], 0.f);
+    wv[2] = nin > 2 ? fmaxf(w2[0], 0.f) : 0.f;
+    float s = wv[0] + wv[1];
+    if (nin > 2) s += wv[2];
+    *den = s + 0.0001f;
+  } else {
+    wv[0] = wv[1] = wv[2] = 1.f;
+    *den = 1.f;
+  }
+}
+
+// one fused value from the three (already BN-applied) inputs, in k_fuse_fwd's operation order
+__device__ __forceinline__ float fuse_combine(float x0, float x1, float x2, int nin, int method,
+                                              const float* wv, float den, int act) {
+  float v;
+  if (method == 0) {
+    v = x0 * wv[0] / den;
+    v = v + x1 * wv[1] / den;
+    if (nin > 2) v = v + x2 * wv[2] / den;
+  } else {
+    v = x0 + x1;
+    if (nin > 2) v = v + x2;
+  }
+  return act_fwd(v, act);
+}
+
 // members of one grouped launch (the per-level convs of a class/box head)
 constexpr int kMaxSeg = 5;
 

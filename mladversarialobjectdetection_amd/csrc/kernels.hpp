@@ -94,6 +94,9 @@ struct DwSeg {
 };
 void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
                          hipStream_t s, int* nps);
+// depthwise 3x3 s1 whose input is a BiFPN fuse computed on load (FuseView); no statistics
+void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, int H, int W, int C, int Ho,
+                         int Wo, int k, int stride, int pt, int pl, hipStream_t s);
 void launch_dw_bwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
                          hipStream_t s, int* nps);
 void launch_transpose(const float* in, float* out, int rows, int cols, hipStream_t s);

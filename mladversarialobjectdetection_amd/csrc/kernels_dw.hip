@@ -21,6 +21,7 @@
 // for the others.
 #include <algorithm>
 #include <stdexcept>
+#include <type_traits>
 
 #include "kernels.hpp"
 
@@ -40,15 +41,19 @@ struct DwGeom {
 
 // Grouped launch: up to kMaxSeg convolutions with the same taps, kernel size, stride and channel
 // count (the per-level members of a class/box-head conv) run as one grid, blockIdx.y = member.
-struct DwFwdSeg {
-  InX x;
+// XV: the input view — InX (BN view) or FuseView (a BiFPN node's fuse computed on load, so the
+// node's fused tensor is never written)
+template <class XV>
+struct DwFwdSegT {
+  XV x;
   float* y;
   DwGeom g;
   StatSink sink;
 };
-template <int NS>  // argument slots: 1 (ordinary launch, small kernarg) or kMaxSeg
+using DwFwdSeg = DwFwdSegT<InX>;
+template <int NS, class XV = InX>  // argument slots: 1 (ordinary launch, small kernarg) or kMaxSeg
 struct DwFwdGroup {
-  DwFwdSeg s[NS];
+  DwFwdSegT<XV> s[NS];
   const float* w;
 };
 struct DwBwdSeg {
@@ -94,6 +99,42 @@ struct StageInX {
   }
   __device__ __forceinline__ float4 finish(const Raw& x) const {
     return f ? inx_apply4(v, k, x) : x;
+  }
+};
+
+struct StageFuse {
+  struct Raw {
+    float4 v[3];
+  };
+  FuseView f;
+  Chan4 k[3];
+  float wv[3], den;
+  __device__ __forceinline__ void init(const FuseView& fv, int c) {
+    f = fv;
+    for (int i = 0; i < 3; ++i)
+      if (i < f.nin && f.x[i].mu) k[i] = inx_chan4(f.x[i], c);
+    fuse_weights(f.w[0], f.w[1], f.w[2], f.nin, f.method, wv, &den);
+  }
+  __device__ __forceinline__ Raw zero() const {
+    Raw r;
+    r.v[0] = r.v[1] = r.v[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    return r;
+  }
+  __device__ __forceinline__ Raw load(long e) const {
+    Raw r;
+    r.v[0] = *reinterpret_cast<const float4*>(f.x[0].p + e);
+    r.v[1] = *reinterpret_cast<const float4*>(f.x[1].p + e);
+    r.v[2] = f.nin > 2 ? *reinterpret_cast<const float4*>(f.x[2].p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    return r;
+  }
+  __device__ __forceinline__ float4 finish(const Raw& r) const {
+    float4 a[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) a[i] = (i < f.nin && f.x[i].mu) ? inx_apply4(f.x[i], k[i], r.v[i]) : r.v[i];
+    return make_float4(fuse_combine(a[0].x, a[1].x, a[2].x, f.nin, f.method, wv, den, f.act),
+                       fuse_combine(a[0].y, a[1].y, a[2].y, f.nin, f.method, wv, den, f.act),
+                       fuse_combine(a[0].z, a[1].z, a[2].z, f.nin, f.method, wv, den, f.act),
+                       fuse_combine(a[0].w, a[1].w, a[2].w, f.nin, f.method, wv, den, f.act));
   }
 };
 
@@ -251,10 +292,11 @@ __device__ __forceinline__ void dw_stats(const float4 (&acc)[RPT], unsigned vmas
 }
 
 // ---- forward: y[oy][ox] = sum_ij a[oy*S - pt + i][ox*S - pl + j] * w[i][j] ----------------
-template <int K, int S, int RPT, bool STATS, int NS>
-__global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS> grp) {
-  const DwFwdSeg sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
-  const InX& xv = sg.x;
+template <int K, int S, int RPT, bool STATS, int NS, class XV>
+__global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
+  using Stage = std::conditional_t<std::is_same<XV, InX>::value, StageInX, StageFuse>;
+  const DwFwdSegT<XV> sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
+  const XV& xv = sg.x;
   const DwGeom& g = sg.g;
   const StatSink& sink = sg.sink;
   const float* __restrict__ w = grp.w;
@@ -270,7 +312,7 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS> grp) {
   const int col = q % g.otw, rg = q / g.otw;
   const int c = (cgi * CG + cg) * 4;
 
-  StageInX src;
+  Stage src;
   src.init(xv, c);
   float4* wt = tile + g.rin * g.cin * CG;
   Taps<K> wr;
@@ -485,8 +527,8 @@ static size_t dw_lds(const DwGeom& g, int k) {
   return ((size_t)g.rin * g.cin + (k > 3 ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
 }
 
-template <int K, int S, int NS>
-static void dw_fwd_go(const DwFwdGroup<NS>& grp, int n, int B, bool stats, hipStream_t s) {
+template <int K, int S, int NS, class XV>
+static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, hipStream_t s) {
   constexpr int RPT = S == 1 ? 4 : 2;
   int gx = 1;
   size_t lds = 0;
@@ -496,20 +538,20 @@ static void dw_fwd_go(const DwFwdGroup<NS>& grp, int n, int B, bool stats, hipSt
   }
   dim3 grid(gx, n, B);
   if (stats)
-    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS>), grid, dim3(256), lds, s, grp);
+    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV>), grid, dim3(256), lds, s, grp);
   else
-    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS>), grid, dim3(256), lds, s, grp);
+    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS, XV>), grid, dim3(256), lds, s, grp);
 }
 
-template <int NS>
-static void dw_fwd_dispatch(const DwFwdGroup<NS>& grp, int n, int B, bool stats, int k, int stride,
+template <int NS, class XV>
+static void dw_fwd_dispatch(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, int k, int stride,
                             hipStream_t s) {
   for (int i = 0; i < n; ++i)
     if (dw_lds(grp.s[i].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  if (k == 3 && stride == 1) dw_fwd_go<3, 1, NS>(grp, n, B, stats, s);
-  else if (k == 3 && stride == 2) dw_fwd_go<3, 2, NS>(grp, n, B, stats, s);
-  else if (k == 5 && stride == 1) dw_fwd_go<5, 1, NS>(grp, n, B, stats, s);
-  else if (k == 5 && stride == 2) dw_fwd_go<5, 2, NS>(grp, n, B, stats, s);
+  if (k == 3 && stride == 1) dw_fwd_go<3, 1, NS, XV>(grp, n, B, stats, s);
+  else if (k == 3 && stride == 2) dw_fwd_go<3, 2, NS, XV>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 1) dw_fwd_go<5, 1, NS, XV>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 2) dw_fwd_go<5, 2, NS, XV>(grp, n, B, stats, s);
   else throw std::invalid_argument("dw: unsupported kernel/stride");
   PHX_LAUNCH_CHECK();
 }
@@ -530,6 +572,19 @@ int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, i
   grp.s[0].sink.P = B * grp.s[0].g.ntiles;
   dw_fwd_dispatch(grp, 1, B, sink.part != nullptr, k, stride, s);
   return B * grp.s[0].g.ntiles;
+}
+
+// BiFPN node: depthwise conv of the node's fuse, computed on load (3x3 stride 1 only)
+void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, int H, int W, int C, int Ho,
+                         int Wo, int k, int stride, int pt, int pl, hipStream_t s) {
+  if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
+  if (k != 3 || stride != 1) throw std::invalid_argument("dw fused: 3x3 stride 1 only");
+  DwFwdGroup<1, FuseView> grp{};
+  grp.w = w;
+  grp.s[0] = DwFwdSegT<FuseView>{fv, y, dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, false), StatSink{}};
+  if (dw_lds(grp.s[0].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
+  dw_fwd_go<3, 1, 1, FuseView>(grp, 1, B, false, s);
+  PHX_LAUNCH_CHECK();
 }
 
 void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,

@@ -1097,20 +1097,6 @@ struct FuseArgs {
   int acc[3];
 };
 
-__device__ __forceinline__ void fuse_weights(const float* w0, const float* w1, const float* w2,
-                                             int nin, int method, float* wv, float* den) {
-  if (method == 0) {
-    wv[0] = fmaxf(w0[0], 0.f);
-    wv[1] = fmaxf(w1[0], 0.f);
-    wv[2] = nin > 2 ? fmaxf(w2[0], 0.f) : 0.f;
-    float s = wv[0] + wv[1];
-    if (nin > 2) s += wv[2];
-    *den = s + 0.0001f;
-  } else {
-    wv[0] = wv[1] = wv[2] = 1.f;
-    *den = 1.f;
-  }
-}
 
 __global__ void k_fuse_fwd(FuseArgs fa, int nin, const float* __restrict__ w0,
                            const float* __restrict__ w1, const float* __restrict__ w2, int method,
@@ -1122,16 +1108,7 @@ __global__ void k_fuse_fwd(FuseArgs fa, int nin, const float* __restrict__ w0,
   const int c = (int)(i % C);
   const float x0 = inx_load1(fa.x[0], i, c), x1 = inx_load1(fa.x[1], i, c);
   const float x2 = nin > 2 ? inx_load1(fa.x[2], i, c) : 0.f;
-  float v;
-  if (method == 0) {
-    v = x0 * wv[0] / den;
-    v = v + x1 * wv[1] / den;
-    if (nin > 2) v = v + x2 * wv[2] / den;
-  } else {
-    v = x0 + x1;
-    if (nin > 2) v = v + x2;
-  }
-  y[i] = act_fwd(v, act);
+  y[i] = fuse_combine(x0, x1, x2, nin, method, wv, den, act);
 }
 
 __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
