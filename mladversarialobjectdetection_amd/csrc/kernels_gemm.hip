@@ -27,6 +27,7 @@
 //    statistics sinks (the per-level members of a class/box-head conv, whose weights are shared
 //    across pyramid levels) run as one grid; blockIdx.z = segment * splits + split.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "common.hpp"
@@ -64,7 +65,7 @@ template <int WM, int TM, int TN, int MODE>
 struct G2 {
   static constexpr int WN = 4 / WM;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 16, LD = BK + 4;
-  static constexpr int NA = BM / 64;                  // A float4 per thread per chunk
+  static constexpr int NA = (BM * 4 + 255) / 256;    // A float4 per thread per chunk
   static constexpr int NB = (BN * 4 + 255) / 256;     // B float4 per thread per chunk
   static constexpr int LDS_FLOATS = 2 * (BM + BN) * LD;
 };
@@ -97,7 +98,7 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE>& r, const Gemm2
 #pragma unroll
   for (int u = 0; u < P::NA; ++u) {
     const int row = m0 + ((t + 256 * u) >> 2);
-    const bool ok = kok && row < a.M;
+    const bool ok = kok && row < a.M && t + 256 * u < P::BM * 4;
     const long e = (long)row * a.K + kk;
     if (MODE == 3) {
       r.a[u] = ok ? *reinterpret_cast<const float4*>(a.G.da + e) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -130,6 +131,7 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE>& r, cons
   float* Bs = As + P::BM * P::LD;
 #pragma unroll
   for (int u = 0; u < P::NA; ++u) {
+    if (t + 256 * u >= P::BM * 4) continue;
     const int rl = (t + 256 * u) >> 2;
     float4 v = r.a[u];
     if (kok && m0 + rl < a.M) {
@@ -382,13 +384,33 @@ static G2Cfg g2_pick(int N) {
 
 Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
   Gemm2Plan p;
-  const G2Cfg c = g2_pick(N);
+  G2Cfg c = g2_pick(N);
+  // few 128x128 tiles (small M, wide N, no split-K): 64-row tiles double the workgroups so
+  // every CU gets MFMA work
+  static const bool half_rows = [] {
+    const char* e = std::getenv("PHX_G212");
+    return !(e && e[0] == '0');
+  }();
+  if (half_rows) {
+    auto wgs = [&](const G2Cfg& q) { return (long)cdiv(M, q.bm()) * cdiv(N, q.bn()); };
+    const bool splits = wgs(c) < 256 && K >= 256;  // split-K covers these
+    if (!splits) {
+      if (c.wm == 4 && c.tm == 1 && c.tn == 2 && wgs(c) < 512) c = G2Cfg{2, 1, 1};
+      if (c.wm == 2 && c.tm == 2 && c.tn == 2 && wgs(c) < 512) c = G2Cfg{2, 1, 2};
+      if (c.wm == 2 && c.tm == 1 && c.tn == 2 && wgs(c) < 512) c = G2Cfg{1, 1, 1};
+    }
+  }
   p.wm = c.wm; p.tm = c.tm; p.tn = c.tn;
   p.mtiles = cdiv(M, c.bm());
   p.gy = cdiv(N, c.bn());
   const long tiles = (long)p.mtiles * p.gy;
   p.splits = 1;
-  if (tiles < 256 && K >= 256) p.splits = std::max(1, std::min<int>((int)((512 + tiles - 1) / tiles), K / 128));
+  static const long split_below = [] {
+    const char* e = std::getenv("PHX_SPLIT_TILES");
+    return e ? std::atol(e) : 256L;
+  }();
+  if (tiles < split_below && K >= 256)
+    p.splits = std::max(1, std::min<int>((int)((2 * split_below + tiles - 1) / tiles), K / 128));
   p.kslice = ((K + p.splits - 1) / p.splits + 15) / 16 * 16;
   p.splits = (K + p.kslice - 1) / p.kslice;
   const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
@@ -451,6 +473,9 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
     case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a); break;
     case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a); break;
     case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a); break;
+    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a); break;
+    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a); break;
+    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
@@ -502,6 +527,9 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
     case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a); break;
     case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a); break;
     case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
