@@ -393,7 +393,11 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
   }();
   if (half_rows) {
     auto wgs = [&](const G2Cfg& q) { return (long)cdiv(M, q.bm()) * cdiv(N, q.bn()); };
-    const bool splits = wgs(c) < 256 && K >= 256;  // split-K covers these
+    static const bool tiles_first = [] {
+      const char* e = std::getenv("PHX_TILES_FIRST");
+      return e && e[0] == '1';
+    }();
+    const bool splits = !tiles_first && wgs(c) < 256 && K >= 256;  // split-K covers these
     if (!splits) {
       if (c.wm == 4 && c.tm == 1 && c.tn == 2 && wgs(c) < 512) c = G2Cfg{2, 1, 1};
       if (c.wm == 2 && c.tm == 2 && c.tn == 2 && wgs(c) < 512) c = G2Cfg{2, 1, 2};
