@@ -20,6 +20,7 @@
 // back-to-back on the same XCD, so the NHWC lines they each read a 16*CG-byte piece of are L2 hits
 // for the others.
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <type_traits>
 
@@ -204,7 +205,7 @@ struct Taps {
 };
 
 // stage rows [r0, r0+rin) x cols [c0, c0+cin) of the NHWC source (sh x sw) into LDS
-template <class Src>
+template <class Src, int U = 4>
 __device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, int sh, int sw, int C,
                                          int r0, int c0, int chan, const DwGeom& g) {
   const int CG = 1 << g.lcg;
@@ -212,11 +213,11 @@ __device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, in
   const int pstep = 256 >> g.lcg;
   const int ecg = threadIdx.x & (CG - 1);
   int p = threadIdx.x >> g.lcg;
-  for (; p < npx; p += 4 * pstep) {
-    typename Src::Raw v[4];
-    bool ok[4];
+  for (; p < npx; p += U * pstep) {
+    typename Src::Raw v[U];
+    bool ok[U];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int pp = p + u * pstep;
       const int prow = pp / g.cin, pcol = pp - prow * g.cin;
       const int iy = r0 + prow, ix = c0 + pcol;
@@ -224,7 +225,7 @@ __device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, in
       v[u] = ok[u] ? src.load((((long)b * sh + iy) * sw + ix) * C + chan) : src.zero();
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int pp = p + u * pstep;
       if (pp < npx) tile[(pp << g.lcg) + ecg] = ok[u] ? src.finish(v[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -292,7 +293,7 @@ __device__ __forceinline__ void dw_stats(const float4 (&acc)[RPT], unsigned vmas
 }
 
 // ---- forward: y[oy][ox] = sum_ij a[oy*S - pt + i][ox*S - pl + j] * w[i][j] ----------------
-template <int K, int S, int RPT, bool STATS, int NS, class XV>
+template <int K, int S, int RPT, bool STATS, int NS, class XV, int SU = 4>
 __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
   using Stage = std::conditional_t<std::is_same<XV, InX>::value, StageInX, StageFuse>;
   const DwFwdSegT<XV> sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
   float4* wt = tile + g.rin * g.cin * CG;
   Taps<K> wr;
   wr.stage(wt, w, g.C, cgi, g.lcg);
-  dw_stage(tile, src, b, g.H, g.W, g.C, oy0 * S - g.pt, ox0 * S - g.pl, c, g);
+  dw_stage<Stage, SU>(tile, src, b, g.H, g.W, g.C, oy0 * S - g.pt, ox0 * S - g.pl, c, g);
   __syncthreads();
 
   const int ox = ox0 + col;
@@ -487,6 +488,24 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
 }
 
 // ---- host planning -------------------------------------------------------------------------
+// output rows per lane of a forward launch: 4 at stride 1; stride 2 defaults to 2 (PHX_DW_S2RPT=4
+// trades LDS / occupancy for less halo re-staging)
+static int dw_rpt_fwd(int stride) {
+  static int s2 = [] {
+    const char* e = std::getenv("PHX_DW_S2RPT");
+    return (e && atoi(e) == 4) ? 4 : 2;
+  }();
+  return stride == 1 ? 4 : s2;
+}
+// staging loads in flight per lane for stride-2 forwards (default 8: -4 % on those launches; PHX_DW_S2SU=4)
+static int dw_s2_su() {
+  static int v = [] {
+    const char* e = std::getenv("PHX_DW_S2SU");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return v;
+}
+
 static int dw_lcg(int C) {
   const int c4 = C / 4;
   return (c4 % 8 == 0) ? 3 : (c4 % 4 == 0) ? 2 : (c4 % 2 == 0) ? 1 : 0;
@@ -527,9 +546,8 @@ static size_t dw_lds(const DwGeom& g, int k) {
   return ((size_t)g.rin * g.cin + (k > 3 ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
 }
 
-template <int K, int S, int NS, class XV>
+template <int K, int S, int RPT, int NS, class XV>
 static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, hipStream_t s) {
-  constexpr int RPT = S == 1 ? 4 : 2;
   int gx = 1;
   size_t lds = 0;
   for (int i = 0; i < n; ++i) {
@@ -537,10 +555,20 @@ static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, h
     lds = std::max(lds, dw_lds(grp.s[i].g, K));
   }
   dim3 grid(gx, n, B);
-  if (stats)
+  if constexpr (S == 2) {
+    if (dw_s2_su() == 8) {
+      if (stats)
+        hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV, 8>), grid, dim3(256), lds, s, grp);
+      else
+        hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS, XV, 8>), grid, dim3(256), lds, s, grp);
+      return;
+    }
+  }
+  if (stats) {
     hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV>), grid, dim3(256), lds, s, grp);
-  else
+  } else {
     hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS, XV>), grid, dim3(256), lds, s, grp);
+  }
 }
 
 template <int NS, class XV>
@@ -548,16 +576,19 @@ static void dw_fwd_dispatch(const DwFwdGroup<NS, XV>& grp, int n, int B, bool st
                             hipStream_t s) {
   for (int i = 0; i < n; ++i)
     if (dw_lds(grp.s[i].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  if (k == 3 && stride == 1) dw_fwd_go<3, 1, NS, XV>(grp, n, B, stats, s);
-  else if (k == 3 && stride == 2) dw_fwd_go<3, 2, NS, XV>(grp, n, B, stats, s);
-  else if (k == 5 && stride == 1) dw_fwd_go<5, 1, NS, XV>(grp, n, B, stats, s);
-  else if (k == 5 && stride == 2) dw_fwd_go<5, 2, NS, XV>(grp, n, B, stats, s);
+  const bool r4 = dw_rpt_fwd(2) == 4;
+  if (k == 3 && stride == 1) dw_fwd_go<3, 1, 4, NS, XV>(grp, n, B, stats, s);
+  else if (k == 3 && stride == 2 && r4) dw_fwd_go<3, 2, 4, NS, XV>(grp, n, B, stats, s);
+  else if (k == 3 && stride == 2) dw_fwd_go<3, 2, 2, NS, XV>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 1) dw_fwd_go<5, 1, 4, NS, XV>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 2 && r4) dw_fwd_go<5, 2, 4, NS, XV>(grp, n, B, stats, s);
+  else if (k == 5 && stride == 2) dw_fwd_go<5, 2, 2, NS, XV>(grp, n, B, stats, s);
   else throw std::invalid_argument("dw: unsupported kernel/stride");
   PHX_LAUNCH_CHECK();
 }
 
 int dw_stat_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stride, int pt, int pl) {
-  const int rpt = stride == 1 ? 4 : 2;
+  const int rpt = dw_rpt_fwd(stride);
   DwGeom g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false);
   return B * g.ntiles;
 }
@@ -565,7 +596,7 @@ int dw_stat_partials(int B, int H, int W, int C, int Ho, int Wo, int k, int stri
 int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho, int Wo,
                   int k, int stride, int pt, int pl, hipStream_t s, StatSink sink) {
   if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
-  const int rpt = stride == 1 ? 4 : 2;
+  const int rpt = dw_rpt_fwd(stride);
   DwFwdGroup<1> grp{};
   grp.w = w;
   grp.s[0] = DwFwdSeg{x, y, dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, rpt, false), sink};
@@ -583,7 +614,7 @@ void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, in
   grp.w = w;
   grp.s[0] = DwFwdSegT<FuseView>{fv, y, dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, false), StatSink{}};
   if (dw_lds(grp.s[0].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  dw_fwd_go<3, 1, 1, FuseView>(grp, 1, B, false, s);
+  dw_fwd_go<3, 1, 4, 1, FuseView>(grp, 1, B, false, s);
   PHX_LAUNCH_CHECK();
 }
 
@@ -591,7 +622,7 @@ void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w,
                          hipStream_t s, int* nps) {
   if (C % 4) throw std::runtime_error("dw: C % 4 != 0");
   if (n < 1 || n > kMaxSeg) throw std::runtime_error("dw group: bad member count");
-  const int rpt = stride == 1 ? 4 : 2;
+  const int rpt = dw_rpt_fwd(stride);
   DwFwdGroup<kMaxSeg> grp{};
   grp.w = w;
   const bool stats = segs[0].sink.part != nullptr;

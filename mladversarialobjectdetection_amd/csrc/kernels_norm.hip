@@ -6,6 +6,7 @@
 // batch variance over (N,H,W).  Reductions accumulate in fp64 so the statistics carry no
 // cancellation error at M ~ 1e6 rows.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -27,13 +28,32 @@ struct RedPlan {
   long rpc;      // rows per chunk
 };
 
+// PHX_RED_BLOCKS: workgroups a column reduction aims for (default 1024); PHX_RED_DEPTH: rows a lane
+// of a column reduction loads before consuming any (8 default, 4); the 2-D elementwise producers keep
+// 4 (measured: 8 helps the BN-backward reductions by 14 %, is neutral for the SE pools and slows
+// the SE backward apply)
+static long red_target_blocks() {
+  static long v = [] {
+    const char* e = std::getenv("PHX_RED_BLOCKS");
+    return e ? atol(e) : 1024L;
+  }();
+  return v;
+}
+static int red_depth() {
+  static int v = [] {
+    const char* e = std::getenv("PHX_RED_DEPTH");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return v;
+}
+
 static RedPlan red_plan(long seg_rows, int C, int nseg) {
   RedPlan p;
   int tpr_total = C / 4;
   p.cgroups = (tpr_total + 255) / 256;
   p.tpr = tpr_total < 256 ? tpr_total : 256;
   int rpi = 256 / p.tpr;
-  long target_blocks = 1024;
+  long target_blocks = red_target_blocks();
   long per_seg = target_blocks / (nseg * p.cgroups);
   if (per_seg < 1) per_seg = 1;
   long rpc = (seg_rows + per_seg - 1) / per_seg;
@@ -51,7 +71,7 @@ size_t colred_scratch_doubles(long seg_rows, int C, int nseg) {
 }
 size_t bn_stats_scratch_doubles(long M, int C) { return colred_scratch_doubles(M, C, 1); }
 
-template <class F>
+template <class F, int D>
 __global__ __launch_bounds__(256) void k_colred_part(F f, long seg_rows, int C, long rpc,
                                                      double* __restrict__ part) {
   const int tpr_total = C >> 2;
@@ -75,12 +95,12 @@ __global__ __launch_bounds__(256) void k_colred_part(F f, long seg_rows, int C, 
       // 64-row fp32 runs; rows are loaded 4 at a time before any is consumed so every lane keeps
       // four 16-B loads (eight for two-operand functors) in flight
       int it = 0;
-      for (; it + 4 <= 64 && m + 3 * rpi < m1; it += 4, m += 4 * rpi) {
-        typename F::Raw v[4];
+      for (; it + D <= 64 && m + (D - 1) * rpi < m1; it += D, m += D * rpi) {
+        typename F::Raw v[D];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = f.load(base + m + u * rpi, c4);
+        for (int u = 0; u < D; ++u) v[u] = f.load(base + m + u * rpi, c4);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) f.add(v[u], a0, a1);
+        for (int u = 0; u < D; ++u) f.add(v[u], a0, a1);
       }
       for (; it < 64 && m < m1; ++it, m += rpi) f.add(f.load(base + m, c4), a0, a1);
 #pragma unroll
@@ -147,8 +167,12 @@ template <class F>
 static int colred_parts(F f, long seg_rows, int C, int nseg, double* scratch, hipStream_t s) {
   if (C % 4) throw std::runtime_error("colred: C % 4 != 0");
   RedPlan p = red_plan(seg_rows, C, nseg);
-  hipLaunchKernelGGL((k_colred_part<F>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
-                     C, p.rpc, scratch);
+  if (red_depth() == 8)
+    hipLaunchKernelGGL((k_colred_part<F, 8>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+                       C, p.rpc, scratch);
+  else
+    hipLaunchKernelGGL((k_colred_part<F, 4>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+                       C, p.rpc, scratch);
   PHX_LAUNCH_CHECK();
   return p.chunks;
 }
@@ -166,7 +190,7 @@ static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hi
 // rpi-th row of its chunk, computes and stores the float4 result (functor F::out), and folds it
 // into the BN-backward sums of its channels; the rpi lanes of a channel quad meet in LDS and the
 // block writes partial (seg * chunks + chunk) of the GradSink.
-template <class F>
+template <class F, int D>
 __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, long rpc,
                                                    GradSink g) {
   const int tpr_total = C >> 2;
@@ -187,16 +211,16 @@ __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, lo
     GSChan4 k;
     if (g.part) k = gs_chan4(g, c4 * 4);
     long m = m0 + rr;
-    for (; m + 3 * rpi < m1; m += 4 * rpi) {
-      typename F::Raw v[4];
-      float4 yv[4];
+    for (; m + (D - 1) * rpi < m1; m += D * rpi) {
+      typename F::Raw v[D];
+      float4 yv[D];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < D; ++u) {
         v[u] = f.load(base + m + u * rpi, c4);
         if (g.part) yv[u] = *reinterpret_cast<const float4*>(g.y + (base + m + u * rpi) * C + c4 * 4);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < D; ++u) {
         const float4 o = f.out(v[u], base + m + u * rpi, c4);
         if (g.part) gs_acc4(g, k, o, yv[u], s1, s2);
       }
@@ -230,7 +254,7 @@ static int ew_gstats(F f, long seg_rows, int C, int nseg, GradSink g, hipStream_
   if (C % 4) throw std::runtime_error("ew_gstats: C % 4 != 0");
   RedPlan p = red_plan(seg_rows, C, nseg);
   g.P = nseg * p.chunks;
-  hipLaunchKernelGGL((k_ew_gstats<F>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows, C,
+  hipLaunchKernelGGL((k_ew_gstats<F, 4>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows, C,
                      p.rpc, g);
   PHX_LAUNCH_CHECK();
   return g.P;
