@@ -16,11 +16,11 @@ KINDS = [  # (kind, substring, primary?) — first match wins
     ("gemm", "k_gemm_splitk_reduce", False), ("gemm", "k_gemm2<", True), ("gemm", "k_gemm<", True),
     ("dw_fwd", "k_dw_fwd<", True), ("dw_bwd", "k_dw_bwd<", True),
     ("bn_stats", "k_bn_finalize<false", True),
-    ("bn_stats", "k_colred_part<phx::StatsAcc>", True), ("bn_stats", "k_colred_final<phx::StatsEpi>", False),
+    ("bn_stats", "k_colred_part<phx::StatsAcc", True), ("bn_stats", "k_colred_final<phx::StatsEpi>", False),
     ("bn_bwd_reduce", "k_bn_finalize<true", True),
-    ("bn_bwd_reduce", "k_colred_part<phx::BwdAcc>", True), ("bn_bwd_reduce", "k_colred_final<phx::BwdEpi2>", False),
-    ("se_bwd", "k_se_mlp_bwd", False), ("se_bwd", "k_ew_gstats<phx::SeBwdApply>", True),
-    ("se", "k_se_mlp", False), ("se", "k_colred_part<phx::SumAcc>", True),
+    ("bn_bwd_reduce", "k_colred_part<phx::BwdAcc", True), ("bn_bwd_reduce", "k_colred_final<phx::BwdEpi2>", False),
+    ("se_bwd", "k_se_mlp_bwd", False), ("se_bwd", "k_ew_gstats<phx::SeBwdApply", True),
+    ("se", "k_se_mlp", False), ("se", "k_colred_part<phx::SumAcc", True),
 ]
 
 
