@@ -152,6 +152,25 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
 int phx_adam_clip(phx_ctx* ctx, float* params, const float* grad, float* m, float* v,
                   float lr, int64_t t, void* stream);
 
+/* ---- input pipeline (off the attack step) ----------------------------- */
+/* DataSequence._map_fn (train_data_generator.py:55-77) for a batch of decoded RGB uint8 images:
+ * (x - mean_rgb) / stddev_rgb, resize by min(out_h/h, out_w/w) to (int(h*s), int(w*s)) with
+ * cv2.resize INTER_LINEAR semantics, pasted at the top-left of a zero [out_h,out_w,3] canvas.
+ * src: packed HWC uint8 images; offsets [B] int64 byte offsets into src; dims [B,2] int32
+ * (h, w) — all three device pointers.  mean_rgb / stddev_rgb: 3 floats each (host).
+ * out [B,out_h,out_w,3] float32 (device); out_h*out_w*3 must be a multiple of 4. */
+int phx_letterbox(phx_ctx* ctx, const uint8_t* src, const int64_t* offsets, const int32_t* dims, int B,
+                  const float* mean_rgb, const float* stddev_rgb, int out_h, int out_w, float* out,
+                  void* stream);
+/* The train-set map chain of partition() (train_data_generator.py:201-204, 222-225):
+ * tf.image.random_flip_left_right -> RandomFlip('horizontal') -> RandomContrast(0.2) ->
+ * tf.image.random_brightness(0.2) -> clip [-1, 1], on in [B,H,W,3] -> out (must not alias).
+ * Flips are drawn per image (Philox keyed by ctx seed, step, global image index), the contrast
+ * factor and brightness delta once per step (shared by every rank).  The first call for a
+ * batch size allocates a small scratch (synchronous). */
+int phx_augment(phx_ctx* ctx, const float* in, int B, int H, int W, int64_t step, int global_image_offset,
+                float* out, void* stream);
+
 /* Per-launch-group device timing (HIP events on the launch stream).  enable=1 clears and
  * starts recording; phx_profile_report synchronises and writes JSON
  * {kind: {count, ms, flops, bytes}} with the algorithmic FLOPs / bytes of the launches. */

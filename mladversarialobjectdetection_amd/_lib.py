@@ -72,6 +72,9 @@ _SIGS = [
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
       c_void_p, c_void_p, c_void_p]),
     ("phx_adam_clip", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int64, c_void_p]),
+    ("phx_letterbox", c_int,
+     [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    ("phx_augment", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int64, c_int, c_void_p, c_void_p]),
     ("phx_profile", c_int, [c_void_p, c_int]),
     ("phx_profile_report", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
     ("phx_debug_last_patched", c_int, [c_void_p, c_void_p, c_void_p]),

@@ -191,6 +191,9 @@ struct phx_ctx {
   // scratch for phx_soft_nms standalone
   DPtr sn_ws, sn_wi;
   size_t sn_cap = 0;
+  // scratch for phx_augment (per-image channel-sum partials)
+  DPtr aug_ws;
+  size_t aug_cap = 0;
 
   float* w() const { return reinterpret_cast<float*>(d_w.get()); }
   const float* wt_of(long off) const {
@@ -1337,6 +1340,37 @@ int phx_brightness_match(phx_ctx* ctx, const float* src, int P, const float* tgt
   d.H = H;
   d.W = W;
   launch_eot_match(d, src, nullptr, tgt, out, E.ysum, E.ymean, false, s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_letterbox(phx_ctx* ctx, const uint8_t* src, const int64_t* offsets, const int32_t* dims, int B,
+                  const float* mean_rgb, const float* stddev_rgb, int out_h, int out_w, float* out,
+                  void* stream) {
+  if (!ctx) return PHX_EINVAL;
+  if (!src || !offsets || !dims || !mean_rgb || !stddev_rgb || !out || B <= 0 || out_h <= 0 || out_w <= 0)
+    return fail(ctx, PHX_EINVAL, "letterbox: null pointer or empty shape");
+  PHX_TRY(ctx)
+  PHX_HIP(hipSetDevice(ctx->device));
+  launch_letterbox(src, offsets, dims, B, mean_rgb, stddev_rgb, out_h, out_w, out, (hipStream_t)stream);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_augment(phx_ctx* ctx, const float* in, int B, int H, int W, int64_t step, int global_image_offset,
+                float* out, void* stream) {
+  if (!ctx) return PHX_EINVAL;
+  if (!in || !out || B <= 0 || H <= 0 || W <= 0) return fail(ctx, PHX_EINVAL, "augment: null pointer or empty shape");
+  if (in == out) return fail(ctx, PHX_EINVAL, "augment: in and out alias (the mirror reads other pixels)");
+  PHX_TRY(ctx)
+  PHX_HIP(hipSetDevice(ctx->device));
+  const size_t need = augment_scratch_doubles(B) * sizeof(double);
+  if (need > ctx->aug_cap) {  // first call for this batch size allocates (synchronous)
+    ctx->aug_ws.reset(dalloc<char>(need));
+    ctx->aug_cap = need;
+  }
+  launch_augment(in, out, B, H, W, ctx->seed, step, global_image_offset,
+                 reinterpret_cast<double*>(ctx->aug_ws.get()), (hipStream_t)stream);
   return PHX_OK;
   PHX_CATCH(ctx)
 }

@@ -336,6 +336,8 @@ enum RngStream : uint32_t {
   RNG_BOX = 3,        // per box: brightness delta, angle (attacker.py:427, 436)
   RNG_NOISE = 4,      // per box element: U(-.01,.01) noise (attacker.py:426)
   RNG_DROP = 5,       // per (MBConv block, pass, image): drop-connect uniform (utils.py:336-339)
+  RNG_AUG = 6,        // input pipeline: per image flips, per batch contrast / brightness
+                      // (train_data_generator.py:201-204, 222-225)
 };
 
 }  // namespace phx

@@ -219,4 +219,14 @@ void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* kee
 void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m,
                       int* argmax, int* nties, int* scratch, hipStream_t s);
 size_t image_max_scratch_ints(int B);
+
+// ---- input pipeline (kernels_data.hip, train_data_generator.py) -----------------------------
+// DataSequence._map_fn for B packed uint8 RGB images (offsets [B] bytes, dims [B,2] = (h, w), device)
+// -> out [B,oh,ow,3] normalised, cv2-INTER_LINEAR-resized, top-left letterboxed, zero padded
+void launch_letterbox(const uint8_t* src, const int64_t* offsets, const int32_t* dims, int B,
+                      const float* mean, const float* stdv, int oh, int ow, float* out, hipStream_t s);
+// flip -> RandomFlip -> RandomContrast(.2) -> random_brightness(.2) -> clip; in/out [B,H,W,3]
+size_t augment_scratch_doubles(int B);
+void launch_augment(const float* in, float* out, int B, int H, int W, uint64_t seed, int64_t step,
+                    int gimg0, double* scratch, hipStream_t s);
 }  // namespace phx

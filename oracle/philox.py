@@ -14,7 +14,7 @@ W0 = np.uint32(0x9E3779B9)
 W1 = np.uint32(0xBB67AE85)
 MASK32 = np.uint64(0xFFFFFFFF)
 
-RNG_PRINT, RNG_PLACE, RNG_BOX, RNG_NOISE, RNG_DROP = 1, 2, 3, 4, 5
+RNG_PRINT, RNG_PLACE, RNG_BOX, RNG_NOISE, RNG_DROP, RNG_AUG = 1, 2, 3, 4, 5, 6
 
 
 def philox4x32_10(c0, c1, c2, c3, k0, k1):
