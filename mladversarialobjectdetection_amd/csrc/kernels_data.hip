@@ -84,6 +84,64 @@ __global__ __launch_bounds__(256) void k_letterbox(LbArgs a) {
   reinterpret_cast<float4*>(a.out + (long)b * a.oh * a.ow * 3)[i4] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// ow % 4 == 0: a lane owns 4 consecutive canvas pixels of one row (12 floats, three 16-B stores),
+// so the row's y taps / weights and the image constants are computed once per lane and the
+// channel loop is static (no per-element divisions)
+__global__ __launch_bounds__(256) void k_letterbox_px4(LbArgs a) {
+  const int b = blockIdx.y;
+  const long nq = (long)a.oh * a.ow / 4;
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const int h = a.dims[2 * b], w = a.dims[2 * b + 1];
+  const uint8_t* s = a.src + a.offsets[b];
+  const double sc = fmin((double)a.ow / w, (double)a.oh / h);
+  const int sh = (int)(h * sc), sw = (int)(w * sc);
+  const long p0 = q * 4;
+  const int oy = (int)(p0 / a.ow), ox0 = (int)(p0 - (long)oy * a.ow);
+  float v[12];
+  if (oy >= sh || ox0 >= sw) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) v[j] = 0.f;
+  } else {
+    const double scx = 1.0 / ((double)sw / w), scy = 1.0 / ((double)sh / h);
+    float fy = (float)((oy + 0.5) * scy - 0.5);
+    const int sy = (int)floorf(fy);
+    fy -= (float)sy;
+    const int y0 = min(max(sy, 0), h - 1), y1 = min(max(sy + 1, 0), h - 1);
+    const float ay0 = 1.f - fy;
+    const uint8_t* r0p = s + (long)y0 * w * 3;
+    const uint8_t* r1p = s + (long)y1 * w * 3;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ox = ox0 + j;
+      if (ox >= sw) {
+        v[3 * j] = v[3 * j + 1] = v[3 * j + 2] = 0.f;
+        continue;
+      }
+      float fx = (float)((ox + 0.5) * scx - 0.5);
+      int sx = (int)floorf(fx);
+      fx -= (float)sx;
+      if (sx < 0) { sx = 0; fx = 0.f; }
+      if (sx >= w - 1) { sx = w - 1; fx = 0.f; }
+      const int sx1 = min(sx + 1, w - 1);
+      const float ax0 = 1.f - fx;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float m = a.mean[c], sd = a.std[c];
+        const float t00 = ((float)r0p[sx * 3 + c] - m) / sd, t01 = ((float)r0p[sx1 * 3 + c] - m) / sd;
+        const float t10 = ((float)r1p[sx * 3 + c] - m) / sd, t11 = ((float)r1p[sx1 * 3 + c] - m) / sd;
+        const float r0 = t00 * ax0 + t01 * fx;
+        const float r1 = t10 * ax0 + t11 * fx;
+        v[3 * j + c] = r0 * ay0 + r1 * fy;
+      }
+    }
+  }
+  float4* o = reinterpret_cast<float4*>(a.out + ((long)b * a.oh * a.ow + p0) * 3);
+  o[0] = make_float4(v[0], v[1], v[2], v[3]);
+  o[1] = make_float4(v[4], v[5], v[6], v[7]);
+  o[2] = make_float4(v[8], v[9], v[10], v[11]);
+}
+
 void launch_letterbox(const uint8_t* src, const int64_t* offsets, const int32_t* dims, int B,
                       const float* mean, const float* stdv, int oh, int ow, float* out, hipStream_t s) {
   if (((long)oh * ow * 3) % 4) throw std::invalid_argument("letterbox: out_h*out_w*3 % 4 != 0");
@@ -99,8 +157,13 @@ void launch_letterbox(const uint8_t* src, const int64_t* offsets, const int32_t*
   a.oh = oh;
   a.ow = ow;
   a.out = out;
-  const long n4 = (long)oh * ow * 3 / 4;
-  hipLaunchKernelGGL(k_letterbox, dim3((unsigned)cdiv(n4, 256), B), dim3(256), 0, s, a);
+  if (ow % 4 == 0) {
+    const long nq = (long)oh * ow / 4;
+    hipLaunchKernelGGL(k_letterbox_px4, dim3((unsigned)cdiv(nq, 256), B), dim3(256), 0, s, a);
+  } else {
+    const long n4 = (long)oh * ow * 3 / 4;
+    hipLaunchKernelGGL(k_letterbox, dim3((unsigned)cdiv(n4, 256), B), dim3(256), 0, s, a);
+  }
   PHX_LAUNCH_CHECK();
 }
 

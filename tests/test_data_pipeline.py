@@ -90,9 +90,16 @@ def test_letterbox_matches_oracle():
     shapes = [(480, 640), (640, 480), (256, 256), (1024, 1024), (100, 37), (512, 512), (1, 300), (333, 1)]
     ims = [rng.integers(0, 256, (h, w, 3), dtype=np.uint8) for h, w in shapes]
     src, off, dims = D.pack_images(ims, torch.device("cuda", 0))
-    for out_size in [(512, 512), (384, 640)]:
+    for out_size in [(512, 512), (384, 640), (100, 102)]:  # the last: ow % 4 != 0 (per-element kernel)
         got = D.letterbox(v, src, off, dims, out_size, MEAN, STD).cpu().numpy()
         for i, im in enumerate(ims):
+            h, w = shapes[i]
+            sc = min(out_size[1] / w, out_size[0] / h)
+            if int(h * sc) == 0 or int(w * sc) == 0:
+                # the reference's cv2.resize raises on an empty destination; the kernel leaves
+                # the zero canvas
+                assert np.all(got[i] == 0)
+                continue
             ref = OD.map_fn(im, out_size, MEAN, STD)
             err = np.abs(got[i] - ref).max()
             assert err <= 2e-6, (shapes[i], out_size, err)
