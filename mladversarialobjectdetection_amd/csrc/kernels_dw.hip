@@ -506,9 +506,19 @@ static int dw_s2_su() {
   return v;
 }
 
-static int dw_lcg(int C) {
+// log2 of the float4 channel groups a workgroup owns: up to 8 (32 channels), capped at 4 (16
+// channels, twice as wide spatial tiles) for the stride-1 forwards and the 5x5 data gradients,
+// where the narrower slices measured faster (-0.1 ms/step; the stride-2 and 3x3 stride-1 data
+// gradients are faster at 8).  PHX_DW_MAXLCG overrides the cap for every launch.
+static int dw_lcg(int C, int k, int s, bool bwd) {
+  static int env_cap = [] {
+    const char* e = std::getenv("PHX_DW_MAXLCG");
+    return e ? std::min(3, std::max(0, atoi(e))) : -1;
+  }();
+  const int cap = env_cap >= 0 ? env_cap : ((!bwd && s == 1) || (bwd && k == 5)) ? 2 : 3;
   const int c4 = C / 4;
-  return (c4 % 8 == 0) ? 3 : (c4 % 4 == 0) ? 2 : (c4 % 2 == 0) ? 1 : 0;
+  const int l = (c4 % 8 == 0) ? 3 : (c4 % 4 == 0) ? 2 : (c4 % 2 == 0) ? 1 : 0;
+  return std::min(l, cap);
 }
 
 // tile over an output space of (oh x ow) written by this launch
@@ -516,7 +526,7 @@ static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k
                       bool bwd) {
   DwGeom g{};
   g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo; g.pt = pt; g.pl = pl;
-  g.lcg = dw_lcg(C);
+  g.lcg = dw_lcg(C, k, s, bwd);
   const int px = 256 >> g.lcg;
   const int oh = bwd ? H : Ho, ow = bwd ? W : Wo;
   g.otw = ow < px ? ow : px;
