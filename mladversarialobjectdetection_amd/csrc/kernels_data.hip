@@ -251,14 +251,99 @@ __global__ __launch_bounds__(256) void k_aug_apply(AugArgs a) {
   reinterpret_cast<float4*>(a.out + (long)b * a.H * a.W * 3)[i4] = make_float4(v[0], v[1], v[2], v[3]);
 }
 
+// W % 4 == 0 variants: a lane owns a quad of 4 pixels (three float4 = 12 floats, channel pattern
+// 0,1,2,0 | 1,2,0,1 | 2,0,1,2), so loads and stores are 16 B and the mirror is a quad-reversal
+__global__ __launch_bounds__(256) void k_aug_sums_q(const float4* __restrict__ in, long nq,
+                                                    double* __restrict__ part) {
+  const int b = blockIdx.y, k = blockIdx.x;
+  const long per = (nq + kAugChunks - 1) / kAugChunks;
+  const long q0 = (long)k * per, q1 = min(nq, q0 + per);
+  const float4* x = in + (long)b * nq * 3;
+  double d[3] = {0.0, 0.0, 0.0};
+  long q = q0 + threadIdx.x;
+  while (q < q1) {
+    float f[3] = {0.f, 0.f, 0.f};
+    for (int it = 0; it < 64 && q < q1; ++it, q += 256) {
+      const float4 a = x[q * 3], bb = x[q * 3 + 1], c = x[q * 3 + 2];
+      f[0] += (a.x + a.w) + (bb.z + c.y);
+      f[1] += (a.y + bb.x) + (bb.w + c.z);
+      f[2] += (a.z + bb.y) + (c.x + c.w);
+    }
+    d[0] += f[0];
+    d[1] += f[1];
+    d[2] += f[2];
+  }
+  __shared__ double sh[3][256];
+  for (int c = 0; c < 3; ++c) sh[c][threadIdx.x] = d[c];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int c = 0; c < 3; ++c) sh[c][threadIdx.x] += sh[c][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) part[((long)b * kAugChunks + k) * 3 + threadIdx.x] = sh[threadIdx.x][0];
+}
+
+__global__ __launch_bounds__(256) void k_aug_apply_q(AugArgs a) {
+  const int b = blockIdx.y;
+  __shared__ float mean_s[3];
+  if (threadIdx.x < 3) {
+    double s = 0.0;
+    for (int k = 0; k < kAugChunks; ++k) s += a.part[((long)b * kAugChunks + k) * 3 + threadIdx.x];
+    mean_s[threadIdx.x] = (float)(s / ((double)a.H * a.W));
+  }
+  __syncthreads();
+  const int wq = a.W / 4;
+  const long nq = (long)a.H * wq;
+  const long q = (long)blockIdx.x * 256 + threadIdx.x;
+  if (q >= nq) return;
+  const uint32_t k0 = (uint32_t)a.seed, k1 = (uint32_t)(a.seed >> 32);
+  const uint32_t ctr = (uint32_t)(((uint64_t)a.step << 8) | RNG_AUG);
+  const u32x4 ri = philox4x32_10(u32x4{0u, 0u, (uint32_t)(a.gimg0 + b), ctr}, k0, k1);
+  const bool mirror = (u01(ri.x) < 0.5f) != (u01(ri.y) < 0.5f);
+  const u32x4 rb = philox4x32_10(u32x4{1u, 0u, 0xFFFFFFFFu, ctr}, k0, k1);
+  const float f = u01(rb.x) * (1.2f - 0.8f) + 0.8f;
+  const float delta = u01(rb.y) * (0.2f - -0.2f) + -0.2f;
+  const long y = q / wq, xq = q - y * wq;
+  const long sq = mirror ? y * wq + (wq - 1 - xq) : q;
+  const float4* x = reinterpret_cast<const float4*>(a.in) + (long)b * nq * 3 + sq * 3;
+  const float4 l0 = x[0], l1 = x[1], l2 = x[2];
+  float px[4][3] = {{l0.x, l0.y, l0.z}, {l0.w, l1.x, l1.y}, {l1.z, l1.w, l2.x}, {l2.y, l2.z, l2.w}};
+  float v[12];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int sj = mirror ? 3 - j : j;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float m = mean_s[c];
+      float t = (px[sj][c] - m) * f + m;
+      t = t + delta;
+      v[3 * j + c] = fminf(fmaxf(t, -1.f), 1.f);
+    }
+  }
+  float4* o = reinterpret_cast<float4*>(a.out) + (long)b * nq * 3 + q * 3;
+  o[0] = make_float4(v[0], v[1], v[2], v[3]);
+  o[1] = make_float4(v[4], v[5], v[6], v[7]);
+  o[2] = make_float4(v[8], v[9], v[10], v[11]);
+}
+
 size_t augment_scratch_doubles(int B) { return (size_t)B * kAugChunks * 3; }
 
 void launch_augment(const float* in, float* out, int B, int H, int W, uint64_t seed, int64_t step,
                     int gimg0, double* scratch, hipStream_t s) {
   if (((long)H * W * 3) % 4) throw std::invalid_argument("augment: H*W*3 % 4 != 0");
+  AugArgs a{in, out, scratch, H, W, seed, step, gimg0};
+  if (W % 4 == 0) {
+    const long nq = (long)H * W / 4;
+    hipLaunchKernelGGL(k_aug_sums_q, dim3(kAugChunks, B), dim3(256), 0, s, reinterpret_cast<const float4*>(in),
+                       nq, scratch);
+    PHX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(k_aug_apply_q, dim3((unsigned)cdiv(nq, 256), B), dim3(256), 0, s, a);
+    PHX_LAUNCH_CHECK();
+    return;
+  }
   hipLaunchKernelGGL(k_aug_sums, dim3(kAugChunks, B), dim3(256), 0, s, in, (long)H * W, scratch);
   PHX_LAUNCH_CHECK();
-  AugArgs a{in, out, scratch, H, W, seed, step, gimg0};
   const long n4 = (long)H * W * 3 / 4;
   hipLaunchKernelGGL(k_aug_apply, dim3((unsigned)cdiv(n4, 256), B), dim3(256), 0, s, a);
   PHX_LAUNCH_CHECK();

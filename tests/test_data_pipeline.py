@@ -110,12 +110,16 @@ def test_augment_matches_oracle():
     import torch
     from mladversarialobjectdetection_amd import data as D
     v = _victim()
+    # W = 52: pixel-quad kernels; W = 50: per-element kernels (W % 4 != 0)
+    for W in (50, 52):
+        xw = np.random.default_rng(W).uniform(-1, 1, (6, 40, W, 3)).astype(np.float32)
+        xwt = torch.as_tensor(xw, device="cuda")
+        for step in (0, 1, 5):
+            got = D.augment(v, xwt, step).cpu().numpy()
+            ref = OD.augment(xw, 11, step)
+            assert np.abs(got - ref).max() <= 2e-6, (W, step)
     x = np.random.default_rng(4).uniform(-1, 1, (6, 40, 52, 3)).astype(np.float32)
     xt = torch.as_tensor(x, device="cuda")
-    for step in (0, 1, 5):
-        got = D.augment(v, xt, step).cpu().numpy()
-        ref = OD.augment(x, 11, step)
-        assert np.abs(got - ref).max() <= 2e-6, step
     # data-parallel shard: images 2..5 as rank 1 with global offset 2 equal the global batch's
     full = D.augment(v, xt, 9).cpu().numpy()
     part = D.augment(v, xt[2:], 9, global_image_offset=2).cpu().numpy()
