@@ -828,10 +828,15 @@ int gemm2_target_wgs() {
   return v;
 }
 
-// rows per block of the split-K reduce-with-statistics kernel
+// rows per block of the split-K reduce-with-statistics kernel: about PHX_SKR_BLOCKS blocks
+// (default 512: a lane walks half as many rows, -0.06 ms/step against 256)
 static int splitk_stats_rb(int M, int N) {
+  static const long blocks = [] {
+    const char* e = getenv("PHX_SKR_BLOCKS");
+    return e ? std::max(1L, atol(e)) : 512L;
+  }();
   const int rpi = 256 / (N / 4);
-  return rpi * std::max(1, cdiv(M, (long)rpi * 256));
+  return rpi * std::max(1, cdiv(M, (long)rpi * blocks));
 }
 
 int gemm_splitk_stats_partials(int M, int N) { return cdiv(M, splitk_stats_rb(M, N)); }
