@@ -497,6 +497,14 @@ static int dw_rpt_fwd(int stride) {
   }();
   return stride == 1 ? 4 : s2;
 }
+// staging loads in flight per lane for stride-1 InX forwards (default 8: -0.035 ms/step; PHX_DW_S1SU=4)
+static int dw_s1_su() {
+  static int v = [] {
+    const char* e = std::getenv("PHX_DW_S1SU");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return v;
+}
 // staging loads in flight per lane for stride-2 forwards (default 8: -4 % on those launches; PHX_DW_S2SU=4)
 static int dw_s2_su() {
   static int v = [] {
@@ -565,8 +573,11 @@ static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, h
     lds = std::max(lds, dw_lds(grp.s[i].g, K));
   }
   dim3 grid(gx, n, B);
-  if constexpr (S == 2) {
-    if (dw_s2_su() == 8) {
+  bool su8 = false;
+  if constexpr (S == 2) su8 = dw_s2_su() == 8;
+  if constexpr (S == 1 && std::is_same<XV, InX>::value) su8 = dw_s1_su() == 8;
+  if constexpr (S == 2 || std::is_same<XV, InX>::value) {
+    if (su8) {
       if (stats)
         hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV, 8>), grid, dim3(256), lds, s, grp);
       else
