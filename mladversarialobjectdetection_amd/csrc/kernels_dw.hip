@@ -388,7 +388,7 @@ __device__ __forceinline__ void dw_gsums(float4 s1, float4 s2, int lcg, int c, l
   }
 }
 
-template <int K, int S, int RPT, bool GS, int NS>
+template <int K, int S, int RPT, bool GS, int NS, int SU = 4>
 __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   const DwBwdSeg sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
   const GradX& gv = sg.gv;
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   float4* wt = tile + g.rin * g.cin * CG;
   Taps<K> wr;
   wr.stage(wt, w, g.C, cgi, g.lcg);
-  dw_stage(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
+  dw_stage<StageGradX, SU>(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
   __syncthreads();
 
   const int ix = ix0 + col;
@@ -666,6 +666,17 @@ static void dw_bwd_go(const DwBwdGroup<NS>& grp, int n, int B, bool gsums, hipSt
     lds = std::max(lds, dw_lds(grp.s[i].g, K));
   }
   dim3 grid(gx, n, B);
+  static const bool su8 = [] {
+    const char* e = std::getenv("PHX_DW_BSU");
+    return e && atoi(e) == 8;
+  }();
+  if (su8) {
+    if (gsums)
+      hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS, 8>), grid, dim3(256), lds, s, grp);
+    else
+      hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false, NS, 8>), grid, dim3(256), lds, s, grp);
+    return;
+  }
   if (gsums)
     hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS>), grid, dim3(256), lds, s, grp);
   else
