@@ -47,17 +47,45 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
   const int nf = n * nclass;
   const int nf4 = nf >> 2;
   const float4* src4 = reinterpret_cast<const float4*>(src);
-  for (int i = threadIdx.x; i < nf4; i += blockDim.x) smem4[i] = src4[i];
-  for (int i = (nf4 << 2) + threadIdx.x; i < nf; i += blockDim.x) lg_s[i] = src[i];
+  // staging: four 16-B loads in flight per lane before any LDS store
+  int i = threadIdx.x;
+  for (; i + 768 < nf4; i += 1024) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = v[u];
+  }
+  for (; i < nf4; i += blockDim.x) smem4[i] = src4[i];
+  for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
   __syncthreads();
-  const int t = threadIdx.x;
-  if (t >= n) return;
-  const float* lg = lg_s + t * nclass;
-  float m = lg[0];
-  int am = 0;
-  for (int c = 1; c < nclass; ++c) {
-    float v = lg[c];
-    if (v > m) { m = v; am = c; }
+  // two lanes per anchor (lanes t and t + 128 of the block are in different waves, so the halves
+  // meet in LDS): each scans half the classes for (max, first argmax); the second half wins only
+  // when strictly greater, which keeps the first-occurrence argmax of the sequential scan
+  const int t = threadIdx.x & (kPreTile - 1), half = threadIdx.x >> 7;
+  const int hc = (nclass + 1) / 2;
+  const int c0 = half * hc, c1 = min(nclass, c0 + hc);
+  float m = -INFINITY;
+  int am = c0;
+  if (t < n && c0 < c1) {
+    const float* lg = lg_s + t * nclass;
+    m = lg[c0];
+    for (int c = c0 + 1; c < c1; ++c) {
+      float v = lg[c];
+      if (v > m) { m = v; am = c; }
+    }
+  }
+  __shared__ float hm[kPreTile];
+  __shared__ int ha_[kPreTile];
+  if (half == 1) {
+    hm[t] = m;
+    ha_[t] = am;
+  }
+  __syncthreads();
+  if (half == 1 || t >= n) return;
+  if (c0 + hc < nclass && hm[t] > m) {
+    m = hm[t];
+    am = ha_[t];
   }
   const int a = L.anchor0 + a0 + t;
   const long idx = (long)b * A + a;
