@@ -132,6 +132,11 @@ def main():
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--model", default="efficientdet-d0",
                     help="victim (the headline metric is D0; others for the secondary configs)")
+    ap.add_argument("--placement", choices=("injected", "first-pass"), default="injected",
+                    help="injected: 1-3 synthetic person boxes per image (SURVEY.md 8d); first-pass: the "
+                         "reference's own flow, patches go onto the first pass's soft-NMS boxes")
+    ap.add_argument("--person-bias", type=float, default=0.0,
+                    help="lift the person class-logit bias so the clean pass yields real soft-NMS candidates")
     args = ap.parse_args()
 
     from mladversarialobjectdetection_amd import distributed as ddp
@@ -144,13 +149,13 @@ def main():
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker, _pad_boxes
     B, S = args.batch, args.image_size
     victim = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
-                                device=local)
+                                device=local, person_bias=args.person_bias)
     att = PatchAttacker(victim, seed=7, device=dev)
     ws_gb = victim.ctx.workspace_bytes(B) / 1e9
     gidx = list(range(rank * B, (rank + 1) * B))
     images = torch.as_tensor(synth_images(gidx, S), device=dev)
     # injected placement boxes, resident on the device like the images ([B,maxb,4] + counts)
-    boxes = _pad_boxes(synth_boxes(gidx, S), B, dev)
+    boxes = _pad_boxes(synth_boxes(gidx, S), B, dev) if args.placement == "injected" else None
 
     for _ in range(args.warmup):
         att.train_step(images, boxes=boxes)
@@ -193,6 +198,7 @@ def main():
         cpu = cpu_baseline(S, args.cpu_batch, threads)
 
     if rank == 0:
+        met = att.step_metrics()
         line = {
             "metric": "patch-opt images/sec (EffDet-D0 512px fwd+bwd)" if args.model == "efficientdet-d0"
                       else f"patch-opt images/sec ({args.model} {S}px fwd+bwd)",
@@ -206,11 +212,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (U(-1,1) images, 1-3 injected person boxes/image, synthetic D0 weights)",
+            "data": ("synthetic (U(-1,1) images, " + ("1-3 injected person boxes/image" if boxes is not None else
+                     "placement from the first pass's soft-NMS boxes") + f", synthetic {args.model} weights"
+                     + (f", person_bias {args.person_bias}" if args.person_bias else "") + ")"),
             "config": {"workload": (f"C{2 if world == 1 else 3}: EfficientDet-D0" if args.model == "efficientdet-d0"
                                     else args.model) + f" patch attack {S}x{S}, "
                                    f"{B} images/GPU, bn=local", "global_batch": world * B, "image_size": S,
-                       "workspace_gb_per_gpu": round(ws_gb, 3),
+                       "workspace_gb_per_gpu": round(ws_gb, 3), "placement": args.placement,
+                       "patches_per_step": int(met["patches"]),
                        "parallelism": f"dp{world}"},
             "roofline": roofline,
             "step_roofline": step_roof,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define PHX_ABI_VERSION 1
+#define PHX_ABI_VERSION 2
 
 #define PHX_PATCH_SIZE 640                               /* attacker.py:43 */
 #define PHX_NPATCH (PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3)
@@ -54,7 +54,10 @@ typedef struct phx_config {
   int image_size;           /* 0 = model default; square images only                         */
   int max_batch;            /* per-rank batch capacity (workspace is sized for it)            */
   int bn_mode;              /* PHX_BN_LOCAL / PHX_BN_FROZEN                                   */
-  float score_thresh;       /* nms_configs.score_thresh (attacker_train.py:31 override = 0.5) */
+  float score_thresh;       /* nms_configs.score_thresh (hparams_config.py:258-266 default 0;
+                               attacker_train.py:31 override 0.5).  As the reference: the first
+                               pass keeps scores >= it (attacker.py:83-84) and gaussian soft-NMS
+                               keeps scores > (it, or 0.001 when it is 0) (postprocess.py:186-188) */
   uint64_t seed;            /* Philox key for all EOT randomness                              */
 } phx_config;
 
@@ -65,13 +68,14 @@ typedef struct phx_ctx phx_ctx;
 enum {
   PHX_M_LOSS = 0,        /* sum_b m_b^2 + scale_loss (+ 1e-5*TV on the rank that owns TV)  */
   PHX_M_SCALE_LOSS = 1,  /* sum_b (m_b - s)^2                                              */
-  PHX_M_TV = 2,          /* total_variation(patch)                                         */
+  PHX_M_TV = 2,          /* total_variation(patch) (written by the rank that owns TV, else 0)  */
   PHX_M_SUM_M = 3,       /* sum_b m_b      (mean_max_score = SUM_M / B)                    */
   PHX_M_SUM_M2 = 4,      /* sum_b m_b^2    (std_max_score)                                 */
   PHX_M_ASR_NUM = 5,     /* #second-pass boxes >= 0.5 after soft-NMS                       */
   PHX_M_ASR_DEN = 6,     /* #first-pass boxes >= 0.5                                       */
   PHX_M_NBOX = 7,        /* #patches pasted                                                */
-  PHX_NMETRIC = 8
+  PHX_M_NIMG = 8,        /* #images of the step (B): the metric row is SUM-all-reducible     */
+  PHX_NMETRIC = 9
 };
 
 /* ---- lifetime --------------------------------------------------------------------------- */
@@ -79,8 +83,19 @@ enum {
  * (infer_lib.py:385-403): builds the EfficientDet program for `cfg` on `device`. */
 int phx_create(const phx_config* cfg, int device, phx_ctx** out);
 void phx_destroy(phx_ctx* ctx);
+/* ctx == NULL: the message of this thread's last failed phx_create. */
 const char* phx_last_error(const phx_ctx* ctx);
 int phx_abi_version(void);
+/* The effective model configuration as JSON (hparams_config.get_efficientdet_config,
+ * hparams_config.py:301-480, + the BiFPN node list of fpn_configs.get_fpn_config,
+ * tf2/fpn_configs.py:166-176): name, backbone_name, image_size, fpn_num_filters,
+ * fpn_cell_repeats, box_class_repeats, anchor_scale, num_scales, aspect_ratios, min_level,
+ * max_level, act_type, fpn_weight_method, mean_rgb, stddev_rgb, num_classes, survival_prob,
+ * fpn_nodes, score_thresh, nms_score_thresh.  Buffer protocol as phx_weight_manifest. */
+int phx_model_info(const phx_ctx* ctx, char* buf, size_t cap, size_t* needed);
+/* Config.override({'nms_configs': {'score_thresh': t}}) (hparams_config.py:91-109) after
+ * creation: first-pass filter >= t, soft-NMS threshold t (0.001 when t == 0, method gaussian). */
+int phx_set_score_thresh(phx_ctx* ctx, float score_thresh);
 
 /* JSON list of the victim's tensors in blob order: [{"name","shape","offset","kind"}...].
  * kind: "kernel","bias","gamma","beta","moving_mean","moving_variance","wsm".
@@ -145,6 +160,16 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
                   const int32_t* count, int maxb, const float* params, int64_t step,
                   int global_image_offset, int add_tv, float* grad, float* metrics,
                   void* stream);
+
+/* PatchAttacker.call(images, training=False) as run by test_step (attacker.py:318-326): the
+ * victim in inference mode (BN from the moving statistics, no drop connect, moving statistics
+ * unchanged), first pass (or injected boxes), EOT paste, second pass, loss and the metric row; no
+ * gradient.  Optional outputs (NULL = skip): the second pass's soft-NMS person boxes / scores /
+ * counts ([B,100,4], [B,100], [B]) that call returns as (boxes_pred, scores_pred). */
+int phx_eval_step(phx_ctx* ctx, const float* images, int B, const float* boxes,
+                  const int32_t* count, int maxb, const float* params, int64_t step,
+                  int global_image_offset, int add_tv, float* metrics, float* out_boxes,
+                  float* out_scores, int32_t* out_count, void* stream);
 
 /* Keras Adam (ResourceApplyAdam, beta1 .9, beta2 .999, eps 1e-7; attacker_train.py:38) on
  * [patch | scale] followed by the variable constraints clip(patch,-1,1), clip(scale,0,1)

@@ -12,15 +12,15 @@ import json
 import os
 from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_size_t, c_uint64, c_void_p
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 PATCH_SIZE = 640
 NPATCH = PATCH_SIZE * PATCH_SIZE * 3
 NPARAM = NPATCH + 1
 MAX_OUT = 100
 
 # metric slots (phx.h PHX_M_*)
-M_LOSS, M_SCALE_LOSS, M_TV, M_SUM_M, M_SUM_M2, M_ASR_NUM, M_ASR_DEN, M_NBOX = range(8)
-NMETRIC = 8
+M_LOSS, M_SCALE_LOSS, M_TV, M_SUM_M, M_SUM_M2, M_ASR_NUM, M_ASR_DEN, M_NBOX, M_NIMG = range(9)
+NMETRIC = 9
 
 BN_LOCAL, BN_FROZEN = 0, 1
 
@@ -52,6 +52,8 @@ _SIGS = [
     ("phx_create", c_int, [POINTER(_Config), c_int, POINTER(c_void_p)]),
     ("phx_destroy", None, [c_void_p]),
     ("phx_last_error", c_char_p, [c_void_p]),
+    ("phx_model_info", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
+    ("phx_set_score_thresh", c_int, [c_void_p, c_float]),
     ("phx_weight_manifest", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
     ("phx_weight_count", c_size_t, [c_void_p]),
     ("phx_load_weights", c_int, [c_void_p, c_void_p, c_size_t]),
@@ -71,6 +73,9 @@ _SIGS = [
     ("phx_step_grad", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
       c_void_p, c_void_p, c_void_p]),
+    ("phx_eval_step", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
+      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_adam_clip", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_float, c_int64, c_void_p]),
     ("phx_letterbox", c_int,
      [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
@@ -126,7 +131,8 @@ class Context:
         h = c_void_p()
         rc = lib.phx_create(ctypes.byref(cfg), int(device), ctypes.byref(h))
         if rc != 0:
-            raise PhxError(f"phx_create({model_name}) failed ({rc})")
+            msg = lib.phx_last_error(None)
+            raise PhxError(f"phx_create({model_name}) failed ({rc}): {msg.decode() if msg else ''}")
         self.h = h
         self.model_name = model_name
         self.max_batch = int(max_batch)
@@ -145,6 +151,17 @@ class Context:
         buf = ctypes.create_string_buffer(need.value)
         self.lib.phx_weight_manifest(self.h, buf, need.value, ctypes.byref(need))
         return json.loads(buf.value.decode())
+
+    def model_info(self) -> dict:
+        """The configuration the program was built from (hparams_config key names + fpn_nodes)."""
+        need = c_size_t()
+        self.lib.phx_model_info(self.h, None, 0, ctypes.byref(need))
+        buf = ctypes.create_string_buffer(need.value)
+        self.lib.phx_model_info(self.h, buf, need.value, ctypes.byref(need))
+        return json.loads(buf.value.decode())
+
+    def set_score_thresh(self, t: float):
+        self.call("phx_set_score_thresh", float(t))
 
     def weight_count(self) -> int:
         return int(self.lib.phx_weight_count(self.h))

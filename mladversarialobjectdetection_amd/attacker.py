@@ -26,6 +26,7 @@ import torch
 
 from . import _lib
 from . import distributed as ddp
+from . import tiff
 from . import weights as wmod
 
 MEAN_RGB = {"efficientdet": [0.485 * 255, 0.456 * 255, 0.406 * 255], "lite": [127.0] * 3}
@@ -54,14 +55,30 @@ class VictimConfig:
     stddev_rgb: list
     nms_configs: NmsConfig = field(default_factory=NmsConfig)
 
-    def override(self, d: dict):
-        """Config.override (hparams_config.py:91-109) for the keys the attack uses."""
+    def override(self, d: dict, ctx=None):
+        """Config.override (hparams_config.py:91-109) for the keys the attack uses.  The values that
+        change the computation are forwarded to the library context (score_thresh); overrides the
+        library does not implement raise instead of diverging silently from the reference."""
         for k, v in d.items():
-            if k == "nms_configs":
-                for kk, vv in v.items():
-                    setattr(self.nms_configs, kk, vv)
-            else:
-                setattr(self, k, v)
+            if k != "nms_configs":
+                raise ValueError(f"config_override: unsupported key {k!r} (only nms_configs)")
+            for kk, vv in v.items():
+                if kk == "score_thresh":
+                    if ctx is not None:
+                        ctx.set_score_thresh(float(vv))
+                elif kk == "iou_thresh":
+                    pass  # unused by the gaussian method: iou_thresh = 1.0 (postprocess.py:184-188)
+                elif kk == "method" and vv != "gaussian":
+                    raise ValueError("config_override: only nms method 'gaussian' (the reference's) is built")
+                elif kk == "sigma" and vv not in (None, 0.5):
+                    raise ValueError("config_override: soft-NMS sigma is fixed at the default 0.5")
+                elif kk == "max_output_size" and vv != 100:
+                    raise ValueError("config_override: max_output_size is fixed at 100")
+                elif kk not in ("method", "sigma", "max_output_size", "pyfunc", "max_nms_inputs"):
+                    raise ValueError(f"config_override: unsupported nms_configs key {kk!r}")
+                elif kk in ("pyfunc", "max_nms_inputs") and vv:
+                    raise ValueError(f"config_override: nms_configs.{kk} = {vv!r} is not built")
+                setattr(self.nms_configs, kk, vv)
 
 
 class EfficientDetVictim:
@@ -259,7 +276,7 @@ class PatchAttacker:
         self.model = model
         self.config = model.config
         if config_override:
-            self.config.override(config_override)
+            self.config.override(config_override, model.ctx)
         dev = torch.device("cuda", model.device) if device is None else torch.device(device)
         if initial_patch is None:
             # np.random.uniform(-1, 1, (640, 640, 3)), scale .4 (attacker.py:42-44)
@@ -269,10 +286,14 @@ class PatchAttacker:
             patch_img, scale = load_patch(initial_patch)
         params = np.concatenate([np.asarray(patch_img, np.float32).reshape(-1), [np.float32(scale)]])
         self.params = torch.as_tensor(params, dtype=torch.float32, device=dev).contiguous()
-        self.grad = torch.zeros_like(self.params)
+        # [d patch | d scale | metric row]: one SUM all-reduce per step carries the gradient and the
+        # per-rank metric sums (loss, counts, #images; TV only on the rank that adds it), so every
+        # rank issues exactly the same collective at the same point of train_step
+        self._red = torch.zeros(_lib.NPARAM + _lib.NMETRIC, device=dev)
+        self.grad = self._red[:_lib.NPARAM]
+        self.metrics_buf = self._red[_lib.NPARAM:]
         self.m = torch.zeros_like(self.params)
         self.v = torch.zeros_like(self.params)
-        self.metrics_buf = torch.zeros(_lib.NMETRIC, device=dev)
         self.learning_rate = learning_rate
         self.iterations = 0
         self.cur_step = 0
@@ -283,8 +304,6 @@ class PatchAttacker:
         self._pending = []      # (step id, device metric row) not yet folded into self.metrics
         self._snapshots = {}    # step id -> running-mean dict after that step
         self._step_id = 0
-        self._bconst = {}
-        self._last_B = 0
         self.bins = np.arange(self.config.nms_configs.score_thresh, .805, .01, dtype="float32")
 
     # ---- variables -----------------------------------------------------------------------------
@@ -308,8 +327,11 @@ class PatchAttacker:
         return self.model.first_pass(images)
 
     def call(self, images, *, training=True, boxes=None, add_tv=None):
-        """PatchAttacker.call: returns [d scale, d patch] (attacker.py:217); `boxes` optionally
-        replaces the first-pass detections for placement (injected boxes)."""
+        """PatchAttacker.call (attacker.py:172-219).  training=True: the attack step, returns
+        [d scale, d patch] (attacker.py:217).  training=False: the victim in inference mode, returns
+        the second pass's soft-NMS person detections (boxes_pred, scores_pred) as padded [B,100,4],
+        [B,100] plus counts [B].  `boxes` optionally replaces the first-pass detections for
+        placement (injected boxes).  The metric row of the step is left in metrics_buf."""
         images = self.model._check_images(images)
         B = images.shape[0]
         if add_tv is None:
@@ -320,13 +342,19 @@ class PatchAttacker:
             self._keep = (bx, cnt)
         else:
             bp, cp, maxb = None, None, 0
+        if not training:
+            ob = torch.empty(B, _lib.MAX_OUT, 4, device=images.device)
+            os_ = torch.empty(B, _lib.MAX_OUT, device=images.device)
+            oc = torch.empty(B, dtype=torch.int32, device=images.device)
+            self.model.ctx.call("phx_eval_step", images.data_ptr(), B, bp, cp, maxb, self.params.data_ptr(),
+                                int(self.cur_step), self.global_offset(B), int(bool(add_tv)),
+                                self.metrics_buf.data_ptr(), ob.data_ptr(), os_.data_ptr(), oc.data_ptr(),
+                                _stream())
+            return ob, os_, oc
         self.model.ctx.call("phx_step_grad", images.data_ptr(), B, bp, cp, maxb, self.params.data_ptr(),
                             int(self.cur_step), self.global_offset(B), int(bool(add_tv)), self.grad.data_ptr(),
                             self.metrics_buf.data_ptr(), _stream())
-        self._last_B = B
-        if training:
-            return [self.grad[_lib.NPATCH:], self.grad[:_lib.NPATCH].view(640, 640, 3)]
-        return None
+        return [self.grad[_lib.NPATCH:], self.grad[:_lib.NPATCH].view(640, 640, 3)]
 
     __call__ = call
 
@@ -337,21 +365,18 @@ class PatchAttacker:
                             self.v.data_ptr(), float(self.learning_rate), int(self.iterations), _stream())
 
     def allreduce_gradients(self):
-        ddp.allreduce_sum_(self.grad)
+        """SUM over ranks of [d patch | d scale | metric row] (the step's one collective)."""
+        ddp.allreduce_sum_(self._red)
 
     def _metric_row(self):
-        """Device row [metrics_buf | batch | scale] of the step just run (scale before the update,
-        as the reference's add_metric(self._scale_regressor) inside call, attacker.py:197)."""
-        B = self._last_B
-        bt = self._bconst.get(B)
-        if bt is None:
-            bt = self._bconst[B] = torch.tensor([float(B)], device=self.params.device)
-        return torch.cat([self.metrics_buf, bt, self.params[_lib.NPATCH:]])
+        """Device row [metric row | scale] of the step just run (scale before the update, as the
+        reference's add_metric(self._scale_regressor) inside call, attacker.py:197)."""
+        return torch.cat([self.metrics_buf, self.params[_lib.NPATCH:]])
 
     @staticmethod
     def _derive(v):
-        """add_metric values (attacker.py:196-207) from a rank-summed [metrics | n | scale] row."""
-        n, scale = float(v[_lib.NMETRIC]), float(v[_lib.NMETRIC + 1])
+        """add_metric values (attacker.py:196-207) from a rank-summed [metrics | scale] row."""
+        n, scale = float(v[_lib.M_NIMG]), float(v[_lib.NMETRIC])
         mean = v[_lib.M_SUM_M] / n
         var = max(v[_lib.M_SUM_M2] / n - mean * mean, 0.0)
         asr = 1.0 - v[_lib.M_ASR_NUM] / (v[_lib.M_ASR_DEN] + 1e-7)
@@ -360,29 +385,20 @@ class PatchAttacker:
                 "asr": asr, "asr_to_scale": asr / scale if scale else float("inf"),
                 "patches": float(v[_lib.M_NBOX])}
 
-    def _reduce_rows(self, rows):
-        """Sum per-rank metric rows over ranks (the replicated scale column is kept as is)."""
-        m = torch.stack(rows)
-        if ddp.is_dist():
-            scale = m[:, -1].clone()
-            ddp.allreduce_sum_(m)
-            m[:, -1] = scale
-        return m.cpu().numpy().astype(np.float64)
-
-    def step_metrics(self, reduce=True):
+    def step_metrics(self):
         """Per-step values of the reference's add_metric set (attacker.py:196-207) for the step
-        just run (synchronises with the device)."""
-        row = self._metric_row()
-        v = self._reduce_rows([row]) if reduce else row[None].cpu().numpy().astype(np.float64)
-        return self._derive(v[0])
+        just run: global over ranks after train_step (its all-reduce), this rank's after a bare
+        call().  Synchronises with the device; issues no collective."""
+        return self._derive(self._metric_row().cpu().numpy().astype(np.float64))
 
     def _flush_metrics(self):
-        """Fold the queued per-step rows into the Keras-style running means: one all-reduce and one
-        device->host copy for all of them, so train_step itself never waits on the GPU."""
+        """Fold the queued per-step rows (already reduced by train_step's all-reduce) into the
+        Keras-style running means with one device->host copy, so train_step never waits on the GPU
+        and reading metrics never issues a collective (any rank may read them, or none)."""
         if not self._pending:
             return
         ids = [i for i, _ in self._pending]
-        rows = self._reduce_rows([r for _, r in self._pending])
+        rows = torch.stack([r for _, r in self._pending]).cpu().numpy().astype(np.float64)
         self._pending.clear()
         for sid, v in zip(ids, rows):
             sm = self._derive(v)
@@ -398,13 +414,22 @@ class PatchAttacker:
         self.call(inputs, boxes=boxes)
         sid = self._step_id
         self._step_id += 1
+        self.allreduce_gradients()
         self._pending.append((sid, self._metric_row()))
         if len(self._pending) >= 256:  # bound the queue when nobody reads the metrics
             self._flush_metrics()
-        self.allreduce_gradients()
         self.apply_gradients()
         self.cur_step += 1
         return _StepMetrics(self, sid)
+
+    def test_step(self, inputs, boxes=None):
+        """attacker.py:318-326: self(inputs, training=False) — the victim in inference mode (BN
+        from the moving statistics, no drop connect), the same EOT paste, loss and metrics, no
+        gradient and no update.  Returns (metrics, (boxes_pred, scores_pred, count)) where the
+        predictions are call()'s soft-NMS person detections on the patched images."""
+        preds = self.call(inputs, training=False, boxes=boxes)
+        ddp.allreduce_sum_(self.metrics_buf)  # every rank, same point: the metric row's one collective
+        return self.step_metrics(), preds
 
     def reset_metrics(self):
         """Keras reset at epoch boundaries: queued steps are folded first (they belong to the
@@ -415,30 +440,26 @@ class PatchAttacker:
         self._snapshots = {}
 
     def save_weights(self, dirpath, **kwargs):
-        """attacker.py:328-341: scale.txt, patch.png (de-normalised uint8), patch.npy (float32;
-        the reference writes patch.tiff through tifffile, not installed here)."""
+        """attacker.py:328-341, same three files: scale.txt (str of the float32 scale), patch.png
+        (clip(patch*std + mean, 0, 255) as uint8) and patch.tiff (the raw float32 normalised patch,
+        written by our own baseline-TIFF writer since tifffile is not installed)."""
         os.makedirs(dirpath)
         with open(os.path.join(dirpath, "scale.txt"), "w") as f:
             f.write(str(np.float32(self.scale.item())))
         patch = self.patch.detach().cpu().numpy()
-        np.save(os.path.join(dirpath, "patch.npy"), patch)
-        img = np.clip(patch * np.asarray(self.config.stddev_rgb) + np.asarray(self.config.mean_rgb), 0, 255)
-        try:
-            from PIL import Image
-            Image.fromarray(img.astype(np.uint8)).save(os.path.join(dirpath, "patch.png"))
-        except ImportError:  # pragma: no cover
-            pass
+        tiff.write_float_tiff(os.path.join(dirpath, "patch.tiff"), patch)
+        img = np.clip(patch * np.asarray(self.config.stddev_rgb, np.float32)
+                      + np.asarray(self.config.mean_rgb, np.float32), 0, 255)
+        from PIL import Image
+        Image.fromarray(img.astype(np.uint8)).save(os.path.join(dirpath, "patch.png"))
 
 
 def load_patch(dirpath):
-    """initial_patch=dir (attacker.py:46-48): patch.npy (or patch.tiff if tifffile exists) + scale.txt."""
+    """initial_patch=dir (attacker.py:46-48): tifffile.imread(patch.tiff) + float(scale.txt)."""
     import ast
-    p = os.path.join(dirpath, "patch.npy")
-    if os.path.exists(p):
-        patch = np.load(p, allow_pickle=False)
-    else:
-        import tifffile  # noqa: F401  (reference format)
-        patch = tifffile.imread(os.path.join(dirpath, "patch.tiff"))
+    patch = tiff.read_float_tiff(os.path.join(dirpath, "patch.tiff"))
+    if patch.shape != (640, 640, 3):
+        raise ValueError(f"patch.tiff holds {patch.shape}, expected (640, 640, 3)")
     with open(os.path.join(dirpath, "scale.txt")) as f:
         scale = ast.literal_eval(f.read())
     return patch, float(scale)

@@ -122,8 +122,10 @@ struct Exec {
   // caller-injected placement boxes ([B,100,4] slot layout + counts)
   float* inj_boxes = nullptr;
   int* inj_count = nullptr;
+  float* dscale_scratch = nullptr;  // dL/dscale of a gradient-free (eval) step
 
   size_t bytes = 0;  // device bytes owned by this executor
+  uint64_t used = 0;  // phx_ctx::clock at the last use
   template <typename T>
   T* alloc(size_t n) {
     T* p = dalloc<T>(n);
@@ -174,7 +176,10 @@ struct phx_ctx {
   int device = 0;
   int max_batch = 0;
   int bn_mode = PHX_BN_LOCAL;
-  float score_thresh = 0.5f;
+  // nms_configs.score_thresh: the first pass keeps scores >= filter_thresh (attacker.py:83-84);
+  // gaussian soft-NMS keeps scores > nms_thresh = score_thresh or 0.001 (postprocess.py:186-188)
+  float score_thresh = 0.f;
+  float filter_thresh = 0.f, nms_thresh = 0.001f;
   uint64_t seed = 0;
   std::vector<WeightEntry> weights;
   size_t wfloats = 0;
@@ -194,6 +199,17 @@ struct phx_ctx {
   // scratch for phx_augment (per-image channel-sum partials)
   DPtr aug_ws;
   size_t aug_cap = 0;
+  // scratch for phx_brightness_match (Y-mean partials), grown on demand
+  DPtr bm_ws;
+  size_t bm_cap = 0;
+  // executor use clock (least-recently-used eviction, see exec_for)
+  uint64_t clock = 0;
+
+  void set_score_thresh(float t) {
+    score_thresh = t;
+    filter_thresh = t;
+    nms_thresh = t != 0.f ? t : 0.001f;
+  }
 
   float* w() const { return reinterpret_cast<float*>(d_w.get()); }
   const float* wt_of(long off) const {
@@ -202,6 +218,7 @@ struct phx_ctx {
     throw std::runtime_error("no transposed kernel for weight offset");
   }
   Exec& exec_for(int B);
+  std::string model_info() const;
 };
 
 namespace {
@@ -260,6 +277,61 @@ std::vector<float> make_anchors(const ModelConfig& mc) {
   return out;
 }
 
+thread_local std::string g_create_err;  // phx_last_error(NULL): the last failed phx_create
+
+}  // namespace
+
+// phx_model_info: the configuration the program builder used (model.cpp get_model_config) in
+// hparams_config's key names, plus the BiFPN node list (fpn_configs.py:24-72)
+std::string phx_ctx::model_info() const {
+  const ModelConfig& c = mc;
+  std::ostringstream js;
+  js.precision(9);
+  auto arr3 = [&](const float* v) {
+    std::ostringstream o;
+    o.precision(9);
+    o << "[" << v[0] << "," << v[1] << "," << v[2] << "]";
+    return o.str();
+  };
+  js << "{\"name\":\"" << json_escape(c.name) << "\",\"backbone_name\":\"" << json_escape(c.backbone)
+     << "\",\"image_size\":" << c.image_size << ",\"fpn_num_filters\":" << c.fpn_num_filters
+     << ",\"fpn_cell_repeats\":" << c.fpn_cell_repeats << ",\"box_class_repeats\":" << c.box_class_repeats
+     << ",\"anchor_scale\":" << c.anchor_scale << ",\"num_scales\":" << c.num_scales << ",\"aspect_ratios\":[";
+  for (size_t i = 0; i < c.aspect_ratios.size(); ++i) js << (i ? "," : "") << c.aspect_ratios[i];
+  js << "],\"min_level\":" << c.min_level << ",\"max_level\":" << c.max_level << ",\"act_type\":\""
+     << (c.act == ACT_RELU6 ? "relu6" : c.act == ACT_SWISH ? "swish" : "none") << "\",\"fpn_weight_method\":\""
+     << (c.fpn_weight_method == 1 ? "sum" : "fastattn") << "\",\"mean_rgb\":" << arr3(c.mean_rgb)
+     << ",\"stddev_rgb\":" << arr3(c.stddev_rgb) << ",\"num_classes\":" << c.num_classes
+     << ",\"survival_prob\":" << c.survival_prob << ",\"width_coefficient\":" << c.width_coefficient
+     << ",\"depth_coefficient\":" << c.depth_coefficient << ",\"score_thresh\":" << filter_thresh
+     << ",\"nms_score_thresh\":" << nms_thresh << ",\"fpn_nodes\":[";
+  const int nlev = c.max_level - c.min_level + 1;
+  std::map<int, std::vector<int>> ids;
+  for (int i = 0; i < nlev; ++i) ids[c.min_level + i] = {i};
+  int cnt = nlev;
+  bool first = true;
+  auto node = [&](int level, const std::vector<int>& in) {
+    js << (first ? "" : ",") << "{\"feat_level\":" << level << ",\"inputs_offsets\":[";
+    for (size_t k = 0; k < in.size(); ++k) js << (k ? "," : "") << in[k];
+    js << "]}";
+    first = false;
+  };
+  for (int i = c.max_level - 1; i >= c.min_level; --i) {
+    node(i, {ids[i].back(), ids[i + 1].back()});
+    ids[i].push_back(cnt++);
+  }
+  for (int i = c.min_level + 1; i <= c.max_level; ++i) {
+    std::vector<int> in = ids[i];
+    in.push_back(ids[i - 1].back());
+    node(i, in);
+    ids[i].push_back(cnt++);
+  }
+  js << "]}";
+  return js.str();
+}
+
+namespace {
+
 int fail(phx_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
   return code;
@@ -292,9 +364,27 @@ void plan_groups(Exec& E, bool local_bn);
 bool is_cls_out(const Program& P, int t);
 }  // namespace
 
+// One executor per batch size (the program and its arenas are shaped by B).  At most
+// kMaxExecs stay alive: a new batch size evicts the least recently used one (after the device
+// has drained, so no queued kernel still reads its memory), which bounds the workspace of a
+// driver that mixes batch sizes (last partial batch, validation) to two executors.
+constexpr size_t kMaxExecs = 2;
+
 Exec& phx_ctx::exec_for(int B) {
+  ++clock;
   for (auto& e : execs)
-    if (e->B == B) return *e;
+    if (e->B == B) {
+      e->used = clock;
+      return *e;
+    }
+  if (execs.size() >= kMaxExecs) {
+    size_t lru = 0;
+    for (size_t i = 1; i < execs.size(); ++i)
+      if (execs[i]->used < execs[lru]->used) lru = i;
+    PHX_HIP(hipDeviceSynchronize());
+    if (last == execs[lru].get()) last = nullptr;
+    execs.erase(execs.begin() + (long)lru);
+  }
   auto ex = std::make_unique<Exec>();
   Exec& E = *ex;
   E.B = B;
@@ -526,6 +616,8 @@ Exec& phx_ctx::exec_for(int B) {
   }
   E.inj_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
   E.inj_count = E.alloc<int>(B);
+  E.dscale_scratch = E.alloc<float>(1);
+  E.used = clock;
   execs.push_back(std::move(ex));
   return *execs.back();
 }
@@ -669,7 +761,7 @@ void plan_groups(Exec& E, bool local_bn) {
   }
 }
 
-void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream_t s) {
+void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream_t s, bool frozen) {
   const Program& P = E.prog;
   const std::vector<int>& g = E.groups[gid];
   const int n = (int)g.size();
@@ -677,7 +769,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
   const Tensor& ti0 = P.tensors[o0.in[0]];
   const Tensor& to0 = P.tensors[o0.out];
   float* W = ctx->w();
-  const bool sink_on = g[0] + 1 < (int)P.ops.size() && E.fused_bn[g[0] + 1];
+  const bool sink_on = !frozen && g[0] + 1 < (int)P.ops.size() && E.fused_bn[g[0] + 1];
   auto sink_of = [&](int r) {
     return sink_on ? StatSink{E.spart + (size_t)r * E.sp_region, E.scnt + (size_t)r * E.sc_region, to0.c, 0}
                    : StatSink{};
@@ -728,6 +820,14 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
       break;
     }
     case OP_BN: {
+      if (frozen) {  // inference BN (test_step): statistics from the moving averages
+        for (int r = 0; r < n; ++r) {
+          const Op& op = P.ops[g[r]];
+          launch_bn_frozen_stats(W + op.mmean, W + op.mvar, E.slot_a[op.slot], E.slot_b[op.slot],
+                                 W + op.gamma, E.slot_c[op.slot], ti0.c, kBnEps, s);
+        }
+        break;
+      }
       BnFinSeg segs[kMaxSeg];
       for (int r = 0; r < n; ++r) {
         const Op& op = P.ops[g[r]];
@@ -841,16 +941,18 @@ DropView drop_view(const Exec& E, int op) {
   return DropView{E.drop_keep + (long)d * E.B, E.prog.ops[op].survival, (long)t.h * t.w};
 }
 
+// train = false: Keras training=False (test_step, attacker.py:325) — inference BN from the moving
+// statistics (not updated) and no drop connect, whatever the context's BN mode
 void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int pass, int64_t step,
-                 int gimg0) {
+                 int gimg0, bool train = true) {
   const Program& P = E.prog;
   float* W = ctx->w();
-  const bool frozen = ctx->bn_mode == PHX_BN_FROZEN;
-  if (E.ndrop)
+  const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train;
+  if (E.ndrop && train)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   for (size_t i = 0; i < P.ops.size(); ++i) {
     if (E.grp_of[i] >= 0) {
-      if (E.groups[E.grp_of[i]].front() == (int)i) run_group_fwd(ctx, E, E.grp_of[i], input, s);
+      if (E.groups[E.grp_of[i]].front() == (int)i) run_group_fwd(ctx, E, E.grp_of[i], input, s, frozen);
       continue;
     }
     if (E.fuse_folded[i]) continue;  // computed by the depthwise conv that follows
@@ -870,7 +972,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
       default: break;
     }
     // the BN right after this op takes its statistics from this launch (StatSink)
-    const bool sink_on = i + 1 < P.ops.size() && E.fused_bn[i + 1];
+    const bool sink_on = !frozen && i + 1 < P.ops.size() && E.fused_bn[i + 1];
     const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0} : StatSink{};
     if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
     Scope scope(ctx, kind, fl, by, s);
@@ -937,7 +1039,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         break;
       case OP_ADD:
         launch_add(view(ctx, E, op.in[0], input), view(ctx, E, op.in[1], input), y,
-                   (long)to.numel(), to.c, s, drop_view(E, (int)i));
+                   (long)to.numel(), to.c, s, train ? drop_view(E, (int)i) : DropView{});
         break;
       case OP_MAXPOOL:
         launch_maxpool_fwd(view(ctx, E, op.in[0], input), y, E.pool_amax[i], ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
@@ -1128,14 +1230,14 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
   const float S = (float)ctx->mc.image_size;
   launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
-                 ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->score_thresh,
+                 ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->filter_thresh,
                  E.scores, E.classes, E.boxes, E.keep, E.ntiles, s);
 }
 
 // postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25
 void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s) {
   Scope scope(ctx, "soft_nms", 0.0, (double)E.B * ctx->A * 5.0, s);
-  launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->score_thresh,
+  launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->nms_thresh,
                   0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s);
 }
 
@@ -1166,16 +1268,27 @@ extern "C" {
 int phx_abi_version(void) { return PHX_ABI_VERSION; }
 
 int phx_create(const phx_config* cfg, int device, phx_ctx** out) {
-  if (!cfg || !out || !cfg->model_name) return PHX_EINVAL;
+  g_create_err.clear();
+  if (!cfg || !out || !cfg->model_name) {
+    g_create_err = "phx_create: null config, model name or output pointer";
+    return PHX_EINVAL;
+  }
   *out = nullptr;
   auto ctx = std::make_unique<phx_ctx>();
   try {
-    if (!get_model_config(cfg->model_name, &ctx->mc)) return PHX_EINVAL;
+    if (!get_model_config(cfg->model_name, &ctx->mc)) {
+      g_create_err = std::string("unknown model '") + cfg->model_name +
+                     "' (efficientdet-d0..d7, efficientdet-lite0..lite4)";
+      return PHX_EINVAL;
+    }
+    if (cfg->image_size < 0 || cfg->max_batch < 0) throw std::invalid_argument("negative image_size / max_batch");
+    if (cfg->bn_mode != PHX_BN_LOCAL && cfg->bn_mode != PHX_BN_FROZEN) throw std::invalid_argument("unknown bn_mode");
+    if (!(cfg->score_thresh >= 0.f && cfg->score_thresh <= 1.f)) throw std::invalid_argument("score_thresh outside [0, 1]");
     if (cfg->image_size > 0) ctx->mc.image_size = cfg->image_size;
     ctx->device = device;
     ctx->max_batch = cfg->max_batch > 0 ? cfg->max_batch : 1;
     ctx->bn_mode = cfg->bn_mode;
-    ctx->score_thresh = cfg->score_thresh > 0.f ? cfg->score_thresh : 0.5f;
+    ctx->set_score_thresh(cfg->score_thresh);
     ctx->seed = cfg->seed;
     NetBuilder nb(ctx->mc, 0);
     nb.build();
@@ -1199,15 +1312,35 @@ int phx_create(const phx_config* cfg, int device, phx_ctx** out) {
     }
     ctx->A = a;
   } catch (const std::exception& e) {
+    g_create_err = std::string("phx_create(") + cfg->model_name + "): " + e.what();
     return PHX_EINVAL;
   }
   *out = ctx.release();
   return PHX_OK;
 }
 
+int phx_set_score_thresh(phx_ctx* ctx, float t) {
+  if (!ctx) return PHX_EINVAL;
+  if (!(t >= 0.f && t <= 1.f)) return fail(ctx, PHX_EINVAL, "score_thresh outside [0, 1]");
+  ctx->set_score_thresh(t);
+  return PHX_OK;
+}
+
+int phx_model_info(const phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
+  if (!ctx) return PHX_EINVAL;
+  const std::string js = ctx->model_info();
+  if (needed) *needed = js.size() + 1;
+  if (buf && cap > 0) {
+    size_t c = std::min(cap - 1, js.size());
+    memcpy(buf, js.data(), c);
+    buf[c] = 0;
+  }
+  return PHX_OK;
+}
+
 void phx_destroy(phx_ctx* ctx) { delete ctx; }
 
-const char* phx_last_error(const phx_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* phx_last_error(const phx_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
 int phx_weight_manifest(const phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   if (!ctx) return PHX_EINVAL;
@@ -1321,7 +1454,7 @@ int phx_soft_nms(phx_ctx* ctx, const float* boxes, const float* scores, const in
     ctx->sn_wi.reset(dalloc<int>(need * 2));
     ctx->sn_cap = need;
   }
-  launch_soft_nms(boxes, scores, nullptr, 0, count, B, N, ctx->score_thresh, 0.25f, PHX_MAX_OUT,
+  launch_soft_nms(boxes, scores, nullptr, 0, count, B, N, ctx->nms_thresh, 0.25f, PHX_MAX_OUT,
                   (float)ctx->mc.image_size, ob, os, oc, (float*)ctx->sn_ws.get(),
                   (int*)ctx->sn_wi.get(), s);
   return PHX_OK;
@@ -1332,14 +1465,25 @@ int phx_brightness_match(phx_ctx* ctx, const float* src, int P, const float* tgt
                          int B, float* out, void* stream) {
   if (!ctx || !src || !tgt || !out || B <= 0 || B > ctx->max_batch) return PHX_EINVAL;
   PHX_TRY(ctx)
+  PHX_HIP(hipSetDevice(ctx->device));
   hipStream_t s = (hipStream_t)stream;
-  Exec& E = ctx->exec_for(ctx->max_batch);
-  EotDims d = E.ed;
+  // its own small scratch (per-image Y partial sums + means), not an executor
+  const size_t need = (size_t)B * 2 * 64 * sizeof(double) + (size_t)B * 2 * sizeof(float);
+  if (need > ctx->bm_cap) {
+    PHX_HIP(hipStreamSynchronize(s));
+    ctx->bm_ws.reset(dalloc<char>(need));
+    ctx->bm_cap = need;
+  }
+  double* ysum = reinterpret_cast<double*>(ctx->bm_ws.get());
+  float* ymean = reinterpret_cast<float*>(ysum + (size_t)B * 2 * 64);
+  EotDims d{};
   d.B = B;
   d.P = P;
   d.H = H;
   d.W = W;
-  launch_eot_match(d, src, nullptr, tgt, out, E.ysum, E.ymean, false, s);
+  d.maxb = PHX_MAX_OUT;
+  d.span_stride = std::max(H, W);
+  launch_eot_match(d, src, nullptr, tgt, out, ysum, ymean, false, s);
   return PHX_OK;
   PHX_CATCH(ctx)
 }
@@ -1462,7 +1606,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);
   run_pre_nms(ctx, E, s);
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
-  launch_loss(E.mraw, B, params, E.dm, grad, metrics, s);
+  launch_loss(E.mraw, B, params, E.dm, grad + PHX_NPATCH, metrics, s);
   // 4. victim data-gradient -> d(patched images)
   run_backward(ctx, E, E.patched, s);
   // 5. ASR metric: soft-NMS over second-pass person boxes (attacker.py:203-205)
@@ -1477,6 +1621,42 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.rstore, E.dmatched, s);
   launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_eval_step(phx_ctx* ctx, const float* images, int B, const float* boxes, const int32_t* count,
+                  int maxb, const float* params, int64_t step, int gimg0, int add_tv, float* metrics,
+                  float* out_boxes, float* out_scores, int32_t* out_count, void* stream) {
+  if (!ctx || !images || !params || !metrics) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  check_ready(ctx, B);
+  hipStream_t s = (hipStream_t)stream;
+  Exec& E = ctx->exec_for(B);
+  ctx->last = &E;
+  PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
+  run_forward(ctx, E, images, s, 0, step, gimg0, false);
+  run_pre_nms(ctx, E, s);
+  run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
+  launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
+  const bool inject = boxes != nullptr;
+  if (inject) {
+    if (!count) throw std::invalid_argument("boxes without count");
+    stage_boxes(E, boxes, count, B, maxb, s);
+  }
+  eot_forward(ctx, E, images, B, inject ? E.inj_boxes : E.nms1_boxes, inject ? E.inj_count : E.nms1_count,
+              params, step, gimg0, s);
+  launch_eot_count(E.ed, E.place, metrics, s);
+  run_forward(ctx, E, E.patched, s, 1, step, gimg0, false);
+  run_pre_nms(ctx, E, s);
+  launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
+  launch_loss(E.mraw, B, params, E.dm, E.dscale_scratch, metrics, s);
+  run_nms(ctx, E, 1, E.nms2_boxes, E.nms2_scores, E.nms2_count, s);
+  launch_count_ge(E.nms2_scores, E.nms2_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_NUM, s);
+  launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
+  if (out_boxes) PHX_HIP(hipMemcpyAsync(out_boxes, E.nms2_boxes, (size_t)B * PHX_MAX_OUT * 16, hipMemcpyDeviceToDevice, s));
+  if (out_scores) PHX_HIP(hipMemcpyAsync(out_scores, E.nms2_scores, (size_t)B * PHX_MAX_OUT * 4, hipMemcpyDeviceToDevice, s));
+  if (out_count) PHX_HIP(hipMemcpyAsync(out_count, E.nms2_count, (size_t)B * 4, hipMemcpyDeviceToDevice, s));
   return PHX_OK;
   PHX_CATCH(ctx)
 }

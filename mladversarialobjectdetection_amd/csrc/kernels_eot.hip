@@ -855,12 +855,17 @@ __global__ void k_tv_final(const double* __restrict__ part, int n, float* __rest
   if (threadIdx.x) return;
   double s = 0.0;
   for (int i = 0; i < 64; ++i) s += sh[i];
-  metrics[PHX_M_TV] = (float)s;
-  if (add) metrics[PHX_M_LOSS] += 1e-5f * (float)s;
+  // TV is a global term: only the rank that adds it to the loss reports it, so the metric row
+  // stays SUM-all-reducible over data-parallel ranks
+  if (add) {
+    metrics[PHX_M_TV] = (float)s;
+    metrics[PHX_M_LOSS] += 1e-5f * (float)s;
+  }
 }
 
 void launch_tv(const float* patch, int P, double* scratch, float* metrics, bool add_to_loss,
                hipStream_t s) {
+  if (!add_to_loss) return;  // neither the loss term nor the metric on this rank
   const int nb = 256;
   hipLaunchKernelGGL(k_tv_part, dim3(nb), dim3(256), 0, s, patch, P, scratch);
   PHX_LAUNCH_CHECK();

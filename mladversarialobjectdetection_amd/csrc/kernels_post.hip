@@ -47,17 +47,23 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
   const int nf = n * nclass;
   const int nf4 = nf >> 2;
   const float4* src4 = reinterpret_cast<const float4*>(src);
-  // staging: four 16-B loads in flight per lane before any LDS store
-  int i = threadIdx.x;
-  for (; i + 768 < nf4; i += 1024) {
-    float4 v[4];
+  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    // staging: four 16-B loads in flight per lane before any LDS store
+    int i = threadIdx.x;
+    for (; i + 768 < nf4; i += 1024) {
+      float4 v[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
+      for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = v[u];
+      for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = v[u];
+    }
+    for (; i < nf4; i += blockDim.x) smem4[i] = src4[i];
+    for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
+  } else {
+    // a run that starts off a 16-B boundary (an image of a level with an odd pixel count, e.g. a
+    // 1x1 or 5x5 P7: h*w*9*90 floats per image): scalar staging
+    for (int j = threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
   }
-  for (; i < nf4; i += blockDim.x) smem4[i] = src4[i];
-  for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
   __syncthreads();
   // two lanes per anchor (lanes t and t + 128 of the block are in different waves, so the halves
   // meet in LDS): each scans half the classes for (max, first argmax); the second half wins only
@@ -428,7 +434,7 @@ void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, fl
 //   dL/draw_b = (4 m_b - 2 s) if raw_b >= 0 (tf.maximum grad goes to x on ties), else 0
 // ------------------------------------------------------------------------------------------
 __global__ void k_loss(const float* __restrict__ mraw, int B, const float* __restrict__ params,
-                       int npatch, float* __restrict__ dm, float* __restrict__ grad,
+                       int npatch, float* __restrict__ dm, float* __restrict__ dscale,
                        float* __restrict__ metrics) {
   if (threadIdx.x != 0) return;
   const float s = params[npatch];
@@ -444,16 +450,17 @@ __global__ void k_loss(const float* __restrict__ mraw, int B, const float* __res
     dsc += -2.0f * d;
     dm[b] = raw >= 0.0f ? (2.0f * mb + 2.0f * d) : 0.0f;
   }
-  grad[npatch] = dsc;
+  *dscale = dsc;
   metrics[PHX_M_LOSS] = sum_sq + scale_loss;
   metrics[PHX_M_SCALE_LOSS] = scale_loss;
   metrics[PHX_M_SUM_M] = sm;
   metrics[PHX_M_SUM_M2] = sm2;
+  metrics[PHX_M_NIMG] = (float)B;
 }
 
-void launch_loss(const float* mraw, int B, const float* params, float* dm, float* grad,
+void launch_loss(const float* mraw, int B, const float* params, float* dm, float* dscale,
                  float* metrics, hipStream_t s) {
-  hipLaunchKernelGGL(k_loss, dim3(1), dim3(64), 0, s, mraw, B, params, PHX_NPATCH_DEV, dm, grad,
+  hipLaunchKernelGGL(k_loss, dim3(1), dim3(64), 0, s, mraw, B, params, PHX_NPATCH_DEV, dm, dscale,
                      metrics);
   PHX_LAUNCH_CHECK();
 }

@@ -14,7 +14,8 @@
 
 namespace phx {
 
-void launch_loss(const float* mraw, int B, const float* params, float* dm, float* grad,
+// loss + metrics (PHX_M_LOSS, _SCALE_LOSS, _SUM_M, _SUM_M2, _NIMG), dL/dm per image, dL/dscale
+void launch_loss(const float* mraw, int B, const float* params, float* dm, float* dscale,
                  float* metrics, hipStream_t s);
 void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* mraw,
                         const int* nties, const float* dm, const float* cls_base,

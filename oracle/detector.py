@@ -23,13 +23,31 @@ import torch.nn.functional as F
 
 from . import philox as ph
 
-# hparams_config.py:301-467
+# hparams_config.py:301-467 (checked against the reference's own config module by
+# tests/test_kats.py::test_oracle_model_table_matches_reference_configs via
+# tests/golden/hparams_configs.json); backbone width/depth: efficientnet_builder.py:31-46,
+# efficientnet_lite_builder.py:31-41.  lite: lite_common_param (hparams_config.py:392-397) —
+# relu6 everywhere, BiFPN fuse 'sum', mean/std 127/128; backbone without SE and with the stem and the
+# first/last block rows unscaled (efficientnet_lite_builder.py:54-79, fix_head_stem in
+# efficientnet_model.py:643-662).
+_D = dict(act="swish", fuse="fastattn", anchor_scale=4.0, lite=False)
+_L = dict(act="relu6", fuse="sum", anchor_scale=4.0, lite=True)
 MODELS = {
-    "efficientdet-d0": dict(backbone="efficientnet-b0", image_size=512, fpn=64, cells=3, rep=3, w=1.0, d=1.0),
-    "efficientdet-d1": dict(backbone="efficientnet-b1", image_size=640, fpn=88, cells=4, rep=3, w=1.0, d=1.1),
-    "efficientdet-d2": dict(backbone="efficientnet-b2", image_size=768, fpn=112, cells=5, rep=3, w=1.1, d=1.2),
-    "efficientdet-d3": dict(backbone="efficientnet-b3", image_size=896, fpn=160, cells=6, rep=4, w=1.2, d=1.4),
-    "efficientdet-d4": dict(backbone="efficientnet-b4", image_size=1024, fpn=224, cells=7, rep=4, w=1.4, d=1.8),
+    "efficientdet-d0": dict(_D, backbone="efficientnet-b0", image_size=512, fpn=64, cells=3, rep=3, w=1.0, d=1.0),
+    "efficientdet-d1": dict(_D, backbone="efficientnet-b1", image_size=640, fpn=88, cells=4, rep=3, w=1.0, d=1.1),
+    "efficientdet-d2": dict(_D, backbone="efficientnet-b2", image_size=768, fpn=112, cells=5, rep=3, w=1.1, d=1.2),
+    "efficientdet-d3": dict(_D, backbone="efficientnet-b3", image_size=896, fpn=160, cells=6, rep=4, w=1.2, d=1.4),
+    "efficientdet-d4": dict(_D, backbone="efficientnet-b4", image_size=1024, fpn=224, cells=7, rep=4, w=1.4, d=1.8),
+    "efficientdet-lite0": dict(_L, backbone="efficientnet-lite0", image_size=320, fpn=64, cells=3, rep=3, w=1.0, d=1.0,
+                               anchor_scale=3.0),
+    "efficientdet-lite1": dict(_L, backbone="efficientnet-lite1", image_size=384, fpn=88, cells=4, rep=3, w=1.0, d=1.1,
+                               anchor_scale=3.0),
+    "efficientdet-lite2": dict(_L, backbone="efficientnet-lite2", image_size=448, fpn=112, cells=5, rep=3, w=1.1,
+                               d=1.2, anchor_scale=3.0),
+    "efficientdet-lite3": dict(_L, backbone="efficientnet-lite3", image_size=512, fpn=160, cells=6, rep=4, w=1.2,
+                               d=1.4),
+    "efficientdet-lite4": dict(_L, backbone="efficientnet-lite4", image_size=640, fpn=224, cells=7, rep=4, w=1.4,
+                               d=1.8),
 }
 BLOCKS = [  # efficientnet_builder.py:163-168: (r, k, s, e, i, o, se)
     (1, 3, 1, 1, 32, 16, 0.25), (2, 3, 2, 6, 16, 24, 0.25), (2, 5, 2, 6, 24, 40, 0.25),
@@ -108,6 +126,38 @@ class TieMax(torch.autograd.Function):
         return g.unsqueeze(-1) * mask / mask.sum(-1, keepdim=True)
 
 
+def fuse_nodes(nodes, wsm, method):
+    """FNode.fuse_features (efficientdet_keras.py:75-110): 'fastattn' = sum_i x_i * relu(w_i) /
+    (sum_j relu(w_j) + 1e-4) accumulated in input order (tf.add_n); 'sum' = add_n(nodes)."""
+    if method == "sum":
+        out = nodes[0]
+        for v in nodes[1:]:
+            out = out + v
+        return out
+    ws = [torch.relu(w) for w in wsm]
+    wsum = ws[0]
+    for v in ws[1:]:
+        wsum = wsum + v
+    out = nodes[0] * ws[0] / (wsum + 0.0001)
+    for i in range(1, len(nodes)):
+        out = out + nodes[i] * ws[i] / (wsum + 0.0001)
+    return out
+
+
+class Relu6(torch.autograd.Function):
+    """tf.nn.relu6 with TF's Relu6Grad: the gradient passes on the open interval (0, 6)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return torch.clamp(x, 0.0, 6.0)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * ((x > 0) & (x < 6)).to(g.dtype)
+
+
 class Detector:
     """EfficientDetNet.call(images, training) restated; weights: name -> HWIO array."""
 
@@ -121,7 +171,7 @@ class Detector:
         # drop-connect draws: dict(seed, step, gimg0, pass) — pass 0 first, 1 second, 2 detect
         self.drop = drop
         self._cache = {}
-        self.bn_stats = {}
+        self.bn_stats = {}   # BN prefix -> list of (batch mean, biased batch var), one per training pass
 
     # ---- weights -----------------------------------------------------------------------------
     def w(self, name):
@@ -159,16 +209,31 @@ class Detector:
         if self.training:
             mean = x.mean(dim=(0, 2, 3), keepdim=True)
             var = ((x - mean) ** 2).mean(dim=(0, 2, 3), keepdim=True)
-            self.bn_stats[pfx] = (mean.detach().flatten(), var.detach().flatten())
+            self.bn_stats.setdefault(pfx, []).append((mean.detach().flatten(), var.detach().flatten(),
+                                                      x.shape[0] * x.shape[2] * x.shape[3]))
         else:
             mean = self.w(pfx + "/moving_mean").view(1, -1, 1, 1)
             var = self.w(pfx + "/moving_variance").view(1, -1, 1, 1)
         xh = (x - mean) / torch.sqrt(var + BN_EPS)
         return xh * g.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
 
-    @staticmethod
-    def act(x):
-        return x * torch.sigmoid(x)  # tf.nn.swish (utils.py:36-40)
+    def act(self, x):
+        """utils.activation_fn (utils.py:36-53): swish = x*sigmoid(x) (tf.nn.swish), relu6 (lite)"""
+        if self.cfg["act"] == "relu6":
+            return Relu6.apply(x)
+        return x * torch.sigmoid(x)
+
+    def moving_stats(self, pfx, mean0, var0):
+        """Moving statistics after this detector's training passes (Keras BN, momentum 0.99,
+        util_keras.py:33-35: moving -= (moving - batch) * 0.01; the fused op hands the
+        Bessel-corrected variance to the update [TF-recall])."""
+        m = np.asarray(mean0, np.float64).copy()
+        v = np.asarray(var0, np.float64).copy()
+        for mu, var, n in self.bn_stats.get(pfx, []):
+            uv = var.numpy() * n / (n - 1) if n > 1 else var.numpy()
+            m = m - (m - mu.numpy()) * 0.01
+            v = v - (v - uv) * 0.01
+        return m, v
 
     def sepconv(self, x, pfx):
         """keras SeparableConv2D(depth_multiplier=1, 3x3, same, bias)"""
@@ -194,12 +259,16 @@ class Detector:
     def backbone(self, x):
         bb = self.cfg["backbone"]
         wc, dc = self.cfg["w"], self.cfg["d"]
+        lite = self.cfg["lite"]
         x = self.act(self.bn(self.conv(x, bb + "/stem/conv2d/kernel", 2), bb + "/stem/tpu_batch_normalization"))
         blocks = []
-        for (r, k, s, e, i, o, se) in BLOCKS:
+        for a, (r, k, s, e, i, o, se) in enumerate(BLOCKS):
             inf, outf = round_filters(i, wc), round_filters(o, wc)
+            if lite:
+                se = 0  # use_se=False (efficientnet_lite_builder.py:79)
             blocks.append((k, s, e, inf, outf, se))
-            for _ in range(round_repeats(r, dc) - 1):
+            reps = r if lite and a in (0, len(BLOCKS) - 1) else round_repeats(r, dc)
+            for _ in range(reps - 1):
                 blocks.append((k, 1, e, outf, outf, se))
         reductions = []
         for idx, (k, s, e, inf, outf, se) in enumerate(blocks):
@@ -220,11 +289,11 @@ class Detector:
             x = self.act(self.bn(self.dwconv(x, f"{pfx}/depthwise_conv2d/depthwise_kernel", s),
                                  f"{pfx}/{bname(bid)}"))
             bid += 1
-            # SE (efficientnet_model.py:184-196)
-            sq = x.mean(dim=(2, 3), keepdim=True)
-            sq = self.act(self.conv(sq, f"{pfx}/se/conv2d/kernel", bias=f"{pfx}/se/conv2d/bias"))
-            sq = self.conv(sq, f"{pfx}/se/conv2d_1/kernel", bias=f"{pfx}/se/conv2d_1/bias")
-            x = torch.sigmoid(sq) * x
+            if se:  # SE (efficientnet_model.py:184-196)
+                sq = x.mean(dim=(2, 3), keepdim=True)
+                sq = self.act(self.conv(sq, f"{pfx}/se/conv2d/kernel", bias=f"{pfx}/se/conv2d/bias"))
+                sq = self.conv(sq, f"{pfx}/se/conv2d_1/kernel", bias=f"{pfx}/se/conv2d_1/bias")
+                x = torch.sigmoid(sq) * x
             x = self.bn(self.conv(x, f"{pfx}/{cname(cid)}/kernel"), f"{pfx}/{bname(bid)}")
             if s == 1 and inf == outf:
                 if self.training and "b0" not in bb:
@@ -291,14 +360,10 @@ class Detector:
                 for i, off in enumerate(nd["inputs_offsets"]):
                     ins.append(self.resample(allf[off], target.shape[2], target.shape[3],
                                              f"{npfx}/resample_{i}_{off}_{len(allf)}"))
-                # fastattn (efficientdet_keras.py:91-100), add_n in order
-                ws = [torch.relu(self.w(f"{npfx}/WSM" + ("" if i == 0 else f"_{i}")).reshape(())) for i in range(len(ins))]
-                wsum = ws[0]
-                for v in ws[1:]:
-                    wsum = wsum + v
-                nd_out = ins[0] * ws[0] / (wsum + 0.0001)
-                for i in range(1, len(ins)):
-                    nd_out = nd_out + ins[i] * ws[i] / (wsum + 0.0001)
+                wsm = None
+                if self.cfg["fuse"] != "sum":
+                    wsm = [self.w(f"{npfx}/WSM" + ("" if i == 0 else f"_{i}")).reshape(()) for i in range(len(ins))]
+                nd_out = fuse_nodes(ins, wsm, self.cfg["fuse"])
                 oac = f"{npfx}/op_after_combine{len(allf)}"
                 v = self.act(nd_out)
                 v = self.sepconv(v, oac + "/conv")
@@ -348,7 +413,7 @@ def anchors(image_size, anchor_scale=4.0, num_scales=3, aspect_ratios=(1.0, 2.0,
     return np.vstack(boxes_all).astype(np.float32)
 
 
-def pre_nms(cls_outs, box_outs, image_size):
+def pre_nms(cls_outs, box_outs, image_size, anchor_scale=4.0):
     """postprocess.pre_nms (postprocess.py:119-156) with max_nms_inputs = 0:
     returns scores [B,A] (differentiable), classes [B,A] (argmax), boxes [B,A,4] (decoded)."""
     B = cls_outs[0].shape[0]
@@ -356,7 +421,7 @@ def pre_nms(cls_outs, box_outs, image_size):
     box = torch.cat([b.permute(0, 2, 3, 1).reshape(B, -1, 4) for b in box_outs], 1)
     classes = torch.argmax(cls, dim=-1)
     logit = TieMax.apply(cls)
-    an = torch.as_tensor(anchors(image_size), dtype=box.dtype)
+    an = torch.as_tensor(anchors(image_size, anchor_scale), dtype=box.dtype)
     yca = (an[:, 0] + an[:, 2]) / 2
     xca = (an[:, 1] + an[:, 3]) / 2
     ha = an[:, 2] - an[:, 0]

@@ -19,39 +19,54 @@ def _ragged_max(scores, mask):
     return D.TieMax.apply(s)
 
 
+def nms_thresh(score_thresh):
+    """postprocess.nms, method 'gaussian': score_threshold = score_thresh or 0.001 (postprocess.py:186-188)"""
+    return score_thresh or 0.001
+
+
 def first_pass(det, images_t, image_size, score_thresh=0.5):
     """PatchAttacker.first_pass (attacker.py:91-116): boxes per image after soft-NMS + clip."""
     with torch.no_grad():
         cls, box = det(images_t)
-        scores, classes, boxes = D.pre_nms(cls, box, image_size)
+        scores, classes, boxes = D.pre_nms(cls, box, image_size, det.cfg["anchor_scale"])
     out = []
     H = W = image_size
     for b in range(images_t.shape[0]):
         sc = scores[b].numpy().astype(np.float32)
         bx = boxes[b].numpy().astype(np.float32)
         keep = (classes[b].numpy() == 0) & pp.valid_mask(bx, H, W, sc, score_thresh)
-        ob, os_, n = pp.nms_padded(bx[keep], sc[keep], image_size, 100, score_thresh)
+        ob, os_, n = pp.nms_padded(bx[keep], sc[keep], image_size, 100, nms_thresh(score_thresh))
         out.append((ob[:n], os_[:n]))
     return out
 
 
+def asr_counts(first, second):
+    """calc_asr (attacker.py:238-255) numerator / denominator: soft-NMS boxes with score >= 0.5
+    after (second) and before (first) the patch."""
+    num = sum(int((s >= np.float32(0.5)).sum()) for _, s in second)
+    den = sum(int((s >= np.float32(0.5)).sum()) for _, s in first)
+    return num, den
+
+
 def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0=0,
                 model="efficientdet-d0", image_size=None, add_tv=True, score_thresh=0.5,
-                dtype=torch.float64):
+                dtype=torch.float64, training=True):
     """Returns dict(loss, grad (NPARAM float64: [patch | scale]), m (per image), patched, ...).
 
     boxes: None -> first-pass soft-NMS boxes (the reference); else a list per image of [n,4]
-    arrays used for placement (the first pass still runs, as in the product)."""
+    arrays used for placement (the first pass still runs, as in the product).
+    training=False: call(training=False) as test_step runs it (attacker.py:318-326): inference BN
+    from the moving statistics, no drop connect; no gradient is taken (grad is None)."""
     image_size = image_size or D.MODELS[model]["image_size"]
-    det = D.Detector(weights, model, image_size, dtype=dtype, training=True,
+    det = D.Detector(weights, model, image_size, dtype=dtype, training=training,
                      drop=dict(seed=seed, step=step, gimg0=gimg0, **{"pass": 0}))
     images_t = torch.as_tensor(np.asarray(images, dtype=np.float64), dtype=dtype)
     B = images_t.shape[0]
     fp = first_pass(det, images_t, image_size, score_thresh)
     det.drop = dict(det.drop, **{"pass": 1})  # the second pass draws its own drop-connect masks
     place_boxes = [fp[b][0] for b in range(B)] if boxes is None else [np.asarray(bx, np.float32) for bx in boxes]
-    patch_t = torch.as_tensor(np.asarray(patch, dtype=np.float64), dtype=dtype).requires_grad_(True)
-    scale_t = torch.tensor(float(np.float32(scale)), dtype=dtype, requires_grad=True)
+    patch_t = torch.as_tensor(np.asarray(patch, dtype=np.float64), dtype=dtype).requires_grad_(training)
+    scale_t = torch.tensor(float(np.float32(scale)), dtype=dtype, requires_grad=training)
     patched, places = [], []
     for b in range(B):
         img, pl = eot.patch_image(images_t[b], patch_t, place_boxes[b], np.float32(scale), seed, step,
@@ -60,11 +75,16 @@ def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0
         places.append(pl)
     patched = torch.stack(patched)
     cls, box = det(patched)
-    scores, classes, dboxes = D.pre_nms(cls, box, image_size)
-    m_raw, m = [], []
+    scores, classes, dboxes = D.pre_nms(cls, box, image_size, det.cfg["anchor_scale"])
+    m_raw, m, second = [], [], []
     for b in range(B):
         keep = torch.as_tensor((classes[b].numpy() == 0)
                                & pp.valid_mask(dboxes[b].numpy().astype(np.float32), image_size, image_size))
+        # the ASR metric's soft-NMS of the second pass (attacker.py:203-205): person & valid only
+        sb = scores[b].detach().numpy().astype(np.float32)[keep.numpy()]
+        bb = dboxes[b].numpy().astype(np.float32)[keep.numpy()]
+        ob, os_, n = pp.nms_padded(bb, sb, image_size, 100, nms_thresh(score_thresh))
+        second.append((ob[:n], os_[:n]))
         r = _ragged_max(scores[b], keep)
         m_raw.append(r)
         m.append(torch.where(r >= 0, r, torch.zeros_like(r)))  # tf.maximum(x, 0): grad to x on ties
@@ -74,11 +94,15 @@ def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0
     loss = (m ** 2 + scale_losses).sum()
     if add_tv:
         loss = loss + 1e-5 * tv
-    gp, gs = torch.autograd.grad(loss, [patch_t, scale_t])
-    grad = np.concatenate([gp.detach().numpy().reshape(-1), [gs.item()]])
+    grad = None
+    if training:
+        gp, gs = torch.autograd.grad(loss, [patch_t, scale_t])
+        grad = np.concatenate([gp.detach().numpy().reshape(-1), [gs.item()]])
+    num, den = asr_counts(fp, second)
     return dict(loss=loss.item(), grad=grad, m=m.detach().numpy(), m_raw=np.array([float(v.detach()) for v in m_raw]),
                 scale_loss=scale_losses.sum().item(), tv=tv.item(), patched=patched.detach().numpy(),
-                places=places, first_pass=fp)
+                places=places, first_pass=fp, second_nms=second, asr_num=num, asr_den=den,
+                nbox=sum(int(p["valid"]) for pl in places for p in pl), det=det)
 
 
 def adam_clip(params, grad, m, v, lr, t):

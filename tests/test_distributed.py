@@ -5,6 +5,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -71,3 +72,33 @@ def test_two_rank_gradient_equals_sum_of_shards():
                            image_size=S, add_tv=(b == 0))
         ref += r["grad"]
     np.testing.assert_allclose(reduced, ref, rtol=1e-10, atol=1e-15)
+
+
+def test_metric_row_is_sum_reducible():
+    """The metric row (phx.h PHX_M_*) of a global batch is the SUM of the per-rank rows: train_step
+    all-reduces it together with the gradient (one collective), and _derive turns the sums into the
+    reference's add_metric values (attacker.py:196-207) — mean / std over all images, ASR over all
+    boxes, TV counted once (only rank 0 writes it)."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd.attacker import PatchAttacker
+    m = np.array([[0.3, 0.1], [0.7, 0.2, 0.5]], dtype=object)
+    rows = []
+    for r, mb in enumerate(m):
+        mb = np.asarray(mb, np.float64)
+        row = np.zeros(_lib.NMETRIC + 1)
+        row[_lib.M_SCALE_LOSS] = ((mb - 0.4) ** 2).sum()
+        row[_lib.M_TV] = 123.0 if r == 0 else 0.0
+        row[_lib.M_LOSS] = (mb ** 2).sum() + row[_lib.M_SCALE_LOSS] + 1e-5 * row[_lib.M_TV]
+        row[_lib.M_SUM_M], row[_lib.M_SUM_M2] = mb.sum(), (mb ** 2).sum()
+        row[_lib.M_ASR_NUM], row[_lib.M_ASR_DEN], row[_lib.M_NIMG] = r, 2 + r, len(mb)
+        row[_lib.NMETRIC] = 0.4  # the replicated scale column is not summed
+        rows.append(row)
+    tot = rows[0] + rows[1]
+    tot[_lib.NMETRIC] = 0.4
+    d = PatchAttacker._derive(tot)
+    allm = np.array([0.3, 0.1, 0.7, 0.2, 0.5])
+    assert d["mean_max_score"] == pytest.approx(allm.mean())
+    assert d["std_max_score"] == pytest.approx(allm.std())  # tf.math.reduce_std: population std
+    assert d["tv_loss"] == 123.0
+    assert d["asr"] == pytest.approx(1 - 1 / (5 + 1e-7))
+    assert d["loss"] == pytest.approx((allm ** 2).sum() + ((allm - 0.4) ** 2).sum() + 1e-5 * 123)

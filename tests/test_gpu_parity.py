@@ -132,10 +132,24 @@ def test_step_grad_matches_oracle(victim, wdict):
     rel = np.linalg.norm(gp - rp) / np.linalg.norm(rp)
     assert cos >= 0.99999, cos
     assert rel <= 1e-3, rel
-    m = np.empty(2, np.float32)
     mt = torch.empty(2, device="cuda")
     victim.ctx.call("phx_debug_last_maxscores", mt.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     np.testing.assert_allclose(mt.cpu().numpy(), ref["m_raw"], rtol=1e-5, atol=1e-6)
+    check_metric_row(met, ref, 2)
+
+
+def check_metric_row(met, ref, B, add_tv=True):
+    """R17: the metric row (attacker.py:196-207, calc_asr :238-255) against the oracle's values."""
+    from mladversarialobjectdetection_amd import _lib
+    assert abs(met[_lib.M_SCALE_LOSS] - ref["scale_loss"]) <= 1e-5 * max(abs(ref["scale_loss"]), 1e-6)
+    if add_tv:
+        assert abs(met[_lib.M_TV] - ref["tv"]) <= 1e-6 * ref["tv"]
+    else:
+        assert met[_lib.M_TV] == 0.0
+    np.testing.assert_allclose(met[_lib.M_SUM_M], ref["m"].sum(), rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(met[_lib.M_SUM_M2], (ref["m"] ** 2).sum(), rtol=1e-5, atol=1e-7)
+    assert met[_lib.M_ASR_NUM] == ref["asr_num"] and met[_lib.M_ASR_DEN] == ref["asr_den"]
+    assert met[_lib.M_NBOX] == ref["nbox"] and met[_lib.M_NIMG] == B
 
 
 def test_adam_clip_matches_oracle(victim):
@@ -152,43 +166,6 @@ def test_adam_clip_matches_oracle(victim):
         att.apply_gradients()
         p0, m, v = ST.adam_clip(p0, g, m, v, 1e-2, t)
     np.testing.assert_allclose(att.params.cpu().numpy(), p0, rtol=1e-6, atol=1e-7)
-
-
-def test_d4_full_size_step_deterministic():
-    """EfficientDet-D4 at 1024x1024 (BASELINE config 4's model and size, fp32, 2 images): drop
-    connect active, 224-channel BiFPN / heads, grouped head launches; finite, non-trivial and
-    bit-reproducible gradient (size-independent checks)."""
-    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
-    v = EfficientDetVictim("efficientdet-d4", "synthetic", seed=0, max_batch=2, rng_seed=5)
-    imgs = torch.as_tensor(_images(2, seed=3, size=1024)).cuda()
-    boxes = [np.array([[100, 120, 600, 400]], np.float32), np.array([[300, 300, 900, 700]], np.float32)]
-    att = PatchAttacker(v, seed=7)
-    att.cur_step = 3
-    att.call(imgs, boxes=boxes)
-    g1 = att.grad.clone()
-    att.call(imgs, boxes=boxes)
-    g2 = att.grad.clone()
-    torch.cuda.synchronize()
-    assert torch.isfinite(g1).all()
-    assert g1[:-1].abs().sum() > 0
-    assert torch.equal(g1, g2)
-
-
-def test_full_size_step_deterministic():
-    """D0 at 512x512: finite, non-trivial and bit-reproducible gradient (size-independent checks)."""
-    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
-    v = EfficientDetVictim("efficientdet-d0", "synthetic", seed=0, max_batch=4, rng_seed=5)
-    imgs = torch.as_tensor(_images(4, seed=2, size=512)).cuda()
-    boxes = [np.array([[50, 60, 300, 200]], np.float32)] * 4
-    att = PatchAttacker(v, seed=7)
-    att.call(imgs, boxes=boxes)
-    g1 = att.grad.clone()
-    att.call(imgs, boxes=boxes)
-    g2 = att.grad.clone()
-    torch.cuda.synchronize()
-    assert torch.isfinite(g1).all()
-    assert g1[:-1].abs().sum() > 0
-    assert torch.equal(g1, g2)
 
 
 def test_step_grad_matches_golden(victim):
@@ -212,6 +189,11 @@ def test_step_grad_matches_golden(victim):
     assert cos >= 0.99999
     assert np.linalg.norm(vals - g["grad_vals"]) <= 2e-3 * np.linalg.norm(g["grad_vals"])
     assert abs(gr[-1] - float(g["dscale"])) <= 1e-5 * abs(float(g["dscale"]))
+    from mladversarialobjectdetection_amd import _lib
+    met = att.metrics_buf.cpu().numpy()
+    assert abs(met[_lib.M_LOSS] - float(g["loss"])) <= 1e-5 * abs(float(g["loss"]))
+    assert abs(met[_lib.M_TV] - float(g["tv"])) <= 1e-6 * float(g["tv"])
+    assert abs(met[_lib.M_SCALE_LOSS] - float(g["scale_loss"])) <= 1e-5 * float(g["scale_loss"])
 
 
 def test_drop_connect_step_matches_oracle():

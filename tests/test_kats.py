@@ -1,6 +1,8 @@
 """Known-answer tests taken from the reference's own test-suite (vendored automl), applied to the
 product's architecture builder (libphx manifest) and to the oracle."""
+import json
 import math
+import os
 
 import numpy as np
 import pytest
@@ -27,10 +29,11 @@ def test_param_count_matches_reference(model, count):
     assert W.trainable_count(man) == count
 
 
-def test_oracle_touches_exactly_the_manifest():
+@pytest.mark.parametrize("model", ["efficientdet-d0", "efficientdet-lite0", "efficientdet-lite4"])
+def test_oracle_touches_exactly_the_manifest(model):
     """The oracle's independent architecture walk reads every trainable tensor of the product's
-    manifest (and nothing else) — both agree with the 3,880,067-parameter KAT."""
-    man = _lib.Context("efficientdet-d0").manifest()
+    manifest (and nothing else) — both agree with the reference's parameter-count KAT."""
+    man = _lib.Context(model).manifest()
     blob = W.synthetic_blob(man, seed=0)
     wd = W.unpack(man, blob)
 
@@ -42,12 +45,13 @@ def test_oracle_touches_exactly_the_manifest():
             return dict.__getitem__(self, k)
 
     rec = Rec(wd)
-    det = D.Detector(rec, "efficientdet-d0", 64, training=True)
+    Rec.seen = set()
+    det = D.Detector(rec, model, 64, training=True, drop=dict(seed=0, step=0, gimg0=0, **{"pass": 0}))
     with torch.no_grad():
-        det(torch.zeros(1, 64, 64, 3, dtype=torch.float64))
+        det(torch.zeros(2, 64, 64, 3, dtype=torch.float64))
     trainable = {e["name"] for e in man if e["kind"] in ("kernel", "bias", "gamma", "beta", "wsm")}
     assert Rec.seen == trainable
-    assert sum(int(np.prod(wd[k].shape)) for k in Rec.seen) == PARAMS["efficientdet-d0"]
+    assert sum(int(np.prod(wd[k].shape)) for k in Rec.seen) == PARAMS[model]
 
 
 def test_bifpn_nodes_l3l7():
@@ -86,19 +90,85 @@ def test_feat_sizes():
 
 
 def test_activations():
-    """utils_test.py:113-141: swish == x*sigmoid(x), relu6([.5, 10]) == [.5, 6]"""
+    """utils_test.py:113-141 on the oracle's activation_fn: swish == x*sigmoid(x) for D0,
+    relu6([.5, 10]) == [.5, 6] for lite (+ TF's Relu6Grad: gradient only on (0, 6))."""
     x = torch.tensor([0.5, 10.0], dtype=torch.float64)
-    assert torch.allclose(D.Detector.act(x), x * torch.sigmoid(x))
-    assert torch.allclose(torch.nn.functional.hardtanh(x, 0, 6), torch.tensor([0.5, 6.0], dtype=torch.float64))
+    d0 = D.Detector({}, "efficientdet-d0", 64)
+    assert torch.allclose(d0.act(x), x * torch.sigmoid(x))
+    lite = D.Detector({}, "efficientdet-lite0", 64)
+    np.testing.assert_array_equal(lite.act(x).numpy(), [0.5, 6.0])
+    xg = torch.tensor([-1.0, 0.0, 0.5, 6.0, 7.0], dtype=torch.float64, requires_grad=True)
+    lite.act(xg).sum().backward()
+    np.testing.assert_array_equal(xg.grad.numpy(), [0, 0, 1, 0, 0])
 
 
 def test_fastattn_fuse():
-    """efficientdet_arch_test.py:207-215: fastattn of [1,3] and [1,3] with unit weights."""
-    nodes = [torch.tensor([1.0, 3.0]), torch.tensor([1.0, 3.0])]
-    ws = [torch.relu(torch.tensor(1.0)), torch.relu(torch.tensor(1.0))]
-    wsum = ws[0] + ws[1]
-    fused = nodes[0] * ws[0] / (wsum + 0.0001) + nodes[1] * ws[1] / (wsum + 0.0001)
-    np.testing.assert_allclose(fused.numpy(), [0.99995, 2.99985], rtol=1e-6)
+    """efficientdet_arch_test.py:207-215: the oracle's BiFPN fuse (fastattn) of [1,3] and [1,3] with
+    unit WSM weights is [0.99995, 2.99985]; 'sum' (lite) is [2, 6]."""
+    nodes = [torch.tensor([1.0, 3.0], dtype=torch.float64)] * 2
+    ones = [torch.tensor(1.0, dtype=torch.float64)] * 2
+    np.testing.assert_allclose(D.fuse_nodes(nodes, ones, "fastattn").numpy(), [0.99995, 2.99985], rtol=1e-6)
+    np.testing.assert_array_equal(D.fuse_nodes(nodes, None, "sum").numpy(), [2.0, 6.0])
+
+
+# ---- model tables vs the reference's own config module ---------------------------------------
+# tests/golden/hparams_configs.json is produced by tests/golden/make_hparams_golden.py, which imports
+# the reference's hparams_config.py / tf2/fpn_configs.py (stub tensorflow) in the build container.
+_HP = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "hparams_configs.json")))
+_HP_MODELS = sorted(k for k in _HP if not k.startswith("_"))
+
+
+def _ref_weight_method(ref):
+    return ref["fpn_effective_weight_method"]
+
+
+def _as3(v):
+    return [float(v)] * 3 if np.isscalar(v) else [float(x) for x in v]
+
+
+@pytest.mark.parametrize("model", _HP_MODELS)
+def test_product_model_table_matches_reference_configs(model):
+    ref = _HP[model]
+    info = _lib.Context(model).model_info()
+    for k in ("image_size", "fpn_num_filters", "fpn_cell_repeats", "box_class_repeats", "num_scales",
+              "min_level", "max_level", "num_classes", "backbone_name", "act_type"):
+        assert info[k] == ref[k], (k, info[k], ref[k])
+    assert info["anchor_scale"] == pytest.approx(ref["anchor_scale"])
+    assert info["aspect_ratios"] == pytest.approx(ref["aspect_ratios"])
+    assert info["fpn_weight_method"] == _ref_weight_method(ref)
+    np.testing.assert_allclose(info["mean_rgb"], _as3(ref["mean_rgb"]), rtol=1e-6)
+    np.testing.assert_allclose(info["stddev_rgb"], _as3(ref["stddev_rgb"]), rtol=1e-6)
+    assert info["fpn_nodes"] == ref["fpn_nodes"]
+    # the architecture options the program builder hard-codes
+    assert ref["separable_conv"] and ref["apply_bn_for_resampling"]
+    assert not ref["conv_after_downsample"] and not ref["conv_bn_act_pattern"]
+    assert ref["nms_configs"]["method"] == "gaussian" and ref["nms_configs"]["max_output_size"] == 100
+    assert ref["nms_configs"]["max_nms_inputs"] == 0 and not ref["nms_configs"]["pyfunc"]
+
+
+@pytest.mark.parametrize("model", [m for m in _HP_MODELS if m in D.MODELS])
+def test_oracle_model_table_matches_reference_configs(model):
+    ref, m = _HP[model], D.MODELS[model]
+    assert (m["backbone"], m["image_size"], m["fpn"], m["cells"], m["rep"]) == (
+        ref["backbone_name"], ref["image_size"], ref["fpn_num_filters"], ref["fpn_cell_repeats"],
+        ref["box_class_repeats"])
+    assert m["act"] == ref["act_type"] and m["fuse"] == _ref_weight_method(ref)
+    assert m["anchor_scale"] == ref["anchor_scale"]
+    assert D.bifpn_nodes(ref["min_level"], ref["max_level"]) == ref["fpn_nodes"]
+
+
+def test_score_thresh_semantics_match_reference():
+    """Default nms_configs.score_thresh 0 -> first-pass filter >= 0, gaussian NMS threshold 0.001
+    (postprocess.py:186-188); attacker_train.py:31's override 0.5 -> both 0.5."""
+    assert _HP["efficientdet-d0"]["nms_configs"]["score_thresh"] == 0.0
+    c = _lib.Context("efficientdet-d0", score_thresh=_HP["efficientdet-d0"]["nms_configs"]["score_thresh"])
+    info = c.model_info()
+    assert info["score_thresh"] == 0.0 and info["nms_score_thresh"] == pytest.approx(0.001)
+    c.set_score_thresh(_HP["_attacker_train_override"]["nms_configs"]["score_thresh"])
+    info = c.model_info()
+    assert info["score_thresh"] == 0.5 and info["nms_score_thresh"] == 0.5
+    with pytest.raises(_lib.PhxError):
+        c.set_score_thresh(1.5)
 
 
 def test_anchor_normalisation():
