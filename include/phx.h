@@ -207,6 +207,9 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed);
 int phx_debug_last_patched(phx_ctx* ctx, float* out, void* stream);
 /* Last step's per-image max scores m_b [B] and loss-anchor index [B] (device->device). */
 int phx_debug_last_maxscores(phx_ctx* ctx, float* m, int32_t* anchor, void* stream);
+/* Last step's d loss / d patched images [B,H,W,3] as the EOT backward reads it (the stem dgrad
+ * writes it only at pixels a paste owns; elsewhere 0) (device->device). */
+int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream);
 
 #ifdef __cplusplus
 }

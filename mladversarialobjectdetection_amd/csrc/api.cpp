@@ -1733,6 +1733,18 @@ int phx_debug_last_patched(phx_ctx* ctx, float* out, void* stream) {
   PHX_CATCH(ctx)
 }
 
+int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream) {
+  if (!ctx || !out || ctx->execs.empty()) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->last) throw std::logic_error("no step has run");
+  Exec& E = *ctx->last;
+  const int S = ctx->mc.image_size;
+  PHX_HIP(hipMemcpyAsync(out, E.gptr(E.prog.input), (size_t)E.B * S * S * 12, hipMemcpyDeviceToDevice,
+                         (hipStream_t)stream));
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
 int phx_debug_last_maxscores(phx_ctx* ctx, float* m, int32_t* anchor, void* stream) {
   if (!ctx || ctx->execs.empty()) return PHX_EINVAL;
   PHX_TRY(ctx)

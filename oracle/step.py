@@ -50,7 +50,7 @@ def asr_counts(first, second):
 
 def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0=0,
                 model="efficientdet-d0", image_size=None, add_tv=True, score_thresh=0.5,
-                dtype=torch.float64, training=True):
+                dtype=torch.float64, training=True, image_grad=False):
     """Returns dict(loss, grad (NPARAM float64: [patch | scale]), m (per image), patched, ...).
 
     boxes: None -> first-pass soft-NMS boxes (the reference); else a list per image of [n,4]
@@ -94,15 +94,19 @@ def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0
     loss = (m ** 2 + scale_losses).sum()
     if add_tv:
         loss = loss + 1e-5 * tv
-    grad = None
+    grad = dimg = None
     if training:
-        gp, gs = torch.autograd.grad(loss, [patch_t, scale_t])
+        if image_grad:  # d loss / d patched images as well (diagnostics)
+            gp, gs, gi = torch.autograd.grad(loss, [patch_t, scale_t, patched])
+            dimg = gi.detach().numpy()
+        else:
+            gp, gs = torch.autograd.grad(loss, [patch_t, scale_t])
         grad = np.concatenate([gp.detach().numpy().reshape(-1), [gs.item()]])
     num, den = asr_counts(fp, second)
     return dict(loss=loss.item(), grad=grad, m=m.detach().numpy(), m_raw=np.array([float(v.detach()) for v in m_raw]),
                 scale_loss=scale_losses.sum().item(), tv=tv.item(), patched=patched.detach().numpy(),
                 places=places, first_pass=fp, second_nms=second, asr_num=num, asr_den=den,
-                nbox=sum(int(p["valid"]) for pl in places for p in pl), det=det)
+                nbox=sum(int(p["valid"]) for pl in places for p in pl), det=det, dimg=dimg)
 
 
 def adam_clip(params, grad, m, v, lr, t):
