@@ -171,6 +171,7 @@ class Detector:
         # drop-connect draws: dict(seed, step, gimg0, pass) — pass 0 first, 1 second, 2 detect
         self.drop = drop
         self._cache = {}
+        self.taps = None
         self.bn_stats = {}   # BN prefix -> list of (batch mean, biased batch var), one per training pass
 
     # ---- weights -----------------------------------------------------------------------------
@@ -204,7 +205,20 @@ class Detector:
         x = F.pad(x, (pl, pr, pt, pb))
         return F.conv2d(x, wt, stride=stride, groups=x.shape[1])
 
-    def bn(self, x, pfx):
+    def bn(self, x, pfx, act=False):
+        """BatchNormalization (+ the activation that follows it when act=True).  With
+        self.taps = {} it records (BN input, output) per prefix, the output retaining its gradient
+        (per-layer diagnostics against the product's debug hook)."""
+        y = self._bn(x, pfx)
+        if act:
+            y = self.act(y)
+        if self.taps is not None:
+            if y.requires_grad:
+                y.retain_grad()
+            self.taps[pfx] = (x, y)
+        return y
+
+    def _bn(self, x, pfx):
         g, b = self.w(pfx + "/gamma"), self.w(pfx + "/beta")
         if self.training:
             mean = x.mean(dim=(0, 2, 3), keepdim=True)
@@ -260,7 +274,7 @@ class Detector:
         bb = self.cfg["backbone"]
         wc, dc = self.cfg["w"], self.cfg["d"]
         lite = self.cfg["lite"]
-        x = self.act(self.bn(self.conv(x, bb + "/stem/conv2d/kernel", 2), bb + "/stem/tpu_batch_normalization"))
+        x = self.bn(self.conv(x, bb + "/stem/conv2d/kernel", 2), bb + "/stem/tpu_batch_normalization", act=True)
         blocks = []
         for a, (r, k, s, e, i, o, se) in enumerate(BLOCKS):
             inf, outf = round_filters(i, wc), round_filters(o, wc)
@@ -283,11 +297,11 @@ class Detector:
                 return "tpu_batch_normalization" if i == 0 else f"tpu_batch_normalization_{i}"
 
             if e != 1:
-                x = self.act(self.bn(self.conv(x, f"{pfx}/{cname(cid)}/kernel"), f"{pfx}/{bname(bid)}"))
+                x = self.bn(self.conv(x, f"{pfx}/{cname(cid)}/kernel"), f"{pfx}/{bname(bid)}", act=True)
                 cid += 1
                 bid += 1
-            x = self.act(self.bn(self.dwconv(x, f"{pfx}/depthwise_conv2d/depthwise_kernel", s),
-                                 f"{pfx}/{bname(bid)}"))
+            x = self.bn(self.dwconv(x, f"{pfx}/depthwise_conv2d/depthwise_kernel", s),
+                                 f"{pfx}/{bname(bid)}", act=True)
             bid += 1
             if se:  # SE (efficientnet_model.py:184-196)
                 sq = x.mean(dim=(2, 3), keepdim=True)
@@ -382,7 +396,7 @@ class Detector:
             for li, v in enumerate(feats):
                 for i in range(self.cfg["rep"]):
                     v = self.sepconv(v, f"{net}/{tag}-{i}")
-                    v = self.act(self.bn(v, f"{net}/{tag}-{i}-bn-{MIN_LEVEL + li}"))
+                    v = self.bn(v, f"{net}/{tag}-{i}-bn-{MIN_LEVEL + li}", act=True)
                 outs.append(self.sepconv(v, f"{net}/{tag}-predict"))
             return outs
 
