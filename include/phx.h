@@ -210,12 +210,13 @@ int phx_debug_last_maxscores(phx_ctx* ctx, float* m, int32_t* anchor, void* stre
 /* Last step's d loss / d patched images [B,H,W,3] as the EOT backward reads it (the stem dgrad
  * writes it only at pixels a paste owns; elsewhere 0) (device->device). */
 int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream);
-/* Per-layer diagnostics of the last step: for the batch norm whose weight prefix is `bn_name`
- * (e.g. "efficientnet-b0/blocks_3/tpu_batch_normalization_1"), which = 0 copies its input (the
- * producing conv's output) and which = 1 the loss gradient w.r.t. its output (after its activation),
- * NHWC [B,h,w,C] = nfloats floats (device->device).  PHX_EINVAL if the name or size is wrong, or
- * no gradient exists for that tensor. */
-int phx_debug_bn_tap(phx_ctx* ctx, const char* bn_name, int which, float* out, size_t nfloats, void* stream);
+/* Per-layer diagnostics of the last step.  `op_name` names an op of the program: a batch norm by
+ * its weight prefix (e.g. "efficientnet-b0/blocks_3/tpu_batch_normalization_1"), a BiFPN fuse as
+ * "<node>/fuse", a resampling max-pool / upsample as "<resample prefix>/max_pool" / "/upsample".
+ * which = 0 copies the op's output (for a batch norm, which is never materialised: its input), which
+ * = 1 the loss gradient w.r.t. its output (a batch norm's after its activation); NHWC [B,h,w,C] =
+ * nfloats floats (device->device).  PHX_EINVAL if the name or size is wrong, or no gradient exists. */
+int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size_t nfloats, void* stream);
 
 #ifdef __cplusplus
 }

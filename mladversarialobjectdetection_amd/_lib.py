@@ -85,7 +85,7 @@ _SIGS = [
     ("phx_debug_last_patched", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_maxscores", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_image_grad", c_int, [c_void_p, c_void_p, c_void_p]),
-    ("phx_debug_bn_tap", c_int, [c_void_p, c_char_p, c_int, c_void_p, c_size_t, c_void_p]),
+    ("phx_debug_tap", c_int, [c_void_p, c_char_p, c_int, c_void_p, c_size_t, c_void_p]),
 ]
 
 EXPORTED = [s[0] for s in _SIGS]

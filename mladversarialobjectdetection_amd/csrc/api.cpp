@@ -1745,21 +1745,24 @@ int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream) {
   PHX_CATCH(ctx)
 }
 
-int phx_debug_bn_tap(phx_ctx* ctx, const char* bn_name, int which, float* out, size_t nfloats, void* stream) {
-  if (!ctx || !bn_name || !out || ctx->execs.empty()) return PHX_EINVAL;
+int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size_t nfloats, void* stream) {
+  if (!ctx || !op_name || !out || ctx->execs.empty()) return PHX_EINVAL;
   PHX_TRY(ctx)
   if (!ctx->last) throw std::logic_error("no step has run");
   Exec& E = *ctx->last;
-  for (const Op& op : E.prog.ops) {
-    if (op.t != OP_BN || op.name != bn_name) continue;
-    const Tensor& t = E.prog.tensors[op.in[0]];
-    if (nfloats != t.numel()) throw std::invalid_argument("bn tap: size mismatch");
-    const float* src = which == 0 ? E.tptr(op.in[0], nullptr) : E.gptr(op.out);
-    if (!src) throw std::invalid_argument("bn tap: no gradient for this tensor");
+  for (size_t i = 0; i < E.prog.ops.size(); ++i) {
+    const Op& op = E.prog.ops[i];
+    if (op.name != op_name) continue;
+    const int t = (op.t == OP_BN && which == 0) ? op.in[0] : op.out;
+    if (nfloats != E.prog.tensors[t].numel()) throw std::invalid_argument("tap: size mismatch");
+    if (which == 0 && op.t == OP_FUSE && E.fuse_folded[i])
+      throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
+    const float* src = which == 0 ? E.tptr(t, nullptr) : E.gptr(op.out);
+    if (!src) throw std::invalid_argument("tap: no gradient for this tensor");
     PHX_HIP(hipMemcpyAsync(out, src, nfloats * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return PHX_OK;
   }
-  throw std::invalid_argument(std::string("bn tap: no batch norm named ") + bn_name);
+  throw std::invalid_argument(std::string("tap: no op named ") + op_name);
   PHX_CATCH(ctx)
 }
 

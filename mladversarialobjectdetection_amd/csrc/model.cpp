@@ -251,7 +251,7 @@ int NetBuilder::op_maxpool(int x, int k, int stride, int oh, int ow) {
   if (o1 != oh || o2 != ow) throw std::runtime_error("maxpool output size mismatch");
   op.in[0] = x; op.nin = 1;
   op.out = new_tensor(tx.n, oh, ow, tx.c);
-  op.name = "max_pool";
+  op.name = "max_pool";  // renamed by resample() to <prefix>/max_pool
   prog_.ops.push_back(op);
   return op.out;
 }
@@ -389,9 +389,13 @@ int NetBuilder::resample(int x, int th, int tw, const std::string& pfx) {
     int sw = (t.w - 1) / tw + 1;
     if (sh != sw) throw std::runtime_error("non-square pooling unsupported");
     x = op_maxpool(x, sh + 1, sh, th, tw);
+    prog_.ops.back().name = pfx + "/max_pool";
   } else if (t.h <= th && t.w <= tw) {
     x = maybe_1x1(x);
-    if (t.h < th || t.w < tw) x = op_upsample(x, th, tw);
+    if (t.h < th || t.w < tw) {
+      x = op_upsample(x, th, tw);
+      prog_.ops.back().name = pfx + "/upsample";
+    }
   } else {
     throw std::runtime_error("incompatible resampling");
   }

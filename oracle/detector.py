@@ -218,6 +218,13 @@ class Detector:
             self.taps[pfx] = (x, y)
         return y
 
+    def _tap(self, name, y):
+        if self.taps is not None:
+            if y.requires_grad:
+                y.retain_grad()
+            self.taps[name] = (y, y)
+        return y
+
     def _bn(self, x, pfx):
         g, b = self.w(pfx + "/gamma"), self.w(pfx + "/beta")
         if self.training:
@@ -347,11 +354,11 @@ class Detector:
         if h > th and w > tw:
             x = maybe_1x1(x)
             sh = (h - 1) // th + 1
-            x = self.maxpool(x, sh + 1, sh)
+            x = self._tap(pfx + "/max_pool", self.maxpool(x, sh + 1, sh))
         else:
             x = maybe_1x1(x)
             if h < th or w < tw:
-                x = self.upsample(x, th, tw)
+                x = self._tap(pfx + "/upsample", self.upsample(x, th, tw))
         return x
 
     # ---- full network ---------------------------------------------------------------------------
@@ -379,7 +386,7 @@ class Detector:
                     wsm = [self.w(f"{npfx}/WSM" + ("" if i == 0 else f"_{i}")).reshape(()) for i in range(len(ins))]
                 nd_out = fuse_nodes(ins, wsm, self.cfg["fuse"])
                 oac = f"{npfx}/op_after_combine{len(allf)}"
-                v = self.act(nd_out)
+                v = self._tap(f"{npfx}/fuse", self.act(nd_out))
                 v = self.sepconv(v, oac + "/conv")
                 v = self.bn(v, oac + "/bn")
                 allf.append(v)
