@@ -162,12 +162,16 @@ class Detector:
     """EfficientDetNet.call(images, training) restated; weights: name -> HWIO array."""
 
     def __init__(self, weights: dict, model="efficientdet-d0", image_size=None, dtype=torch.float64,
-                 training=True, drop=None):
+                 training=True, drop=None, bn_frozen=False):
         self.W = weights
         self.cfg = MODELS[model]
         self.image_size = image_size or self.cfg["image_size"]
         self.dtype = dtype
         self.training = training
+        # bn_frozen: inference BN (moving statistics) even in a training pass — Keras BN layers with
+        # trainable=False (attack_detection.py:46-47; the library's bn=frozen mode); drop connect
+        # still follows `training`
+        self.bn_frozen = bn_frozen
         # drop-connect draws: dict(seed, step, gimg0, pass) — pass 0 first, 1 second, 2 detect
         self.drop = drop
         self._cache = {}
@@ -227,7 +231,7 @@ class Detector:
 
     def _bn(self, x, pfx):
         g, b = self.w(pfx + "/gamma"), self.w(pfx + "/beta")
-        if self.training:
+        if self.training and not self.bn_frozen:
             mean = x.mean(dim=(0, 2, 3), keepdim=True)
             var = ((x - mean) ** 2).mean(dim=(0, 2, 3), keepdim=True)
             self.bn_stats.setdefault(pfx, []).append((mean.detach().flatten(), var.detach().flatten(),

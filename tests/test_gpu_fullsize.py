@@ -10,8 +10,14 @@ keyed by global image index, 1-3 injected person boxes per image, synthetic weig
       bit-identical reruns and batch-permutation equivariance of the detector
   C4  D4 1024^2 (fp32, batch 2): finite, non-zero, bit-identical on rerun; drop connect active
 
-Tolerances as at 128^2: loss rel <= 1e-5, d scale rel <= 1e-5, d patch cosine >= 0.99999 and
-||d - d_ref|| / ||d_ref|| <= 1e-3; metric row per check_metric_row.
+Tolerances as at 128^2 (loss rel <= 1e-5, d scale rel <= 1e-5, d patch cosine >= 0.99999; metric row
+per check_metric_row) except ||d - d_ref|| / ||d_ref|| <= 5e-3 instead of 1e-3.  Reason (measured with
+scripts/diag_t5.py): at 512^2 batch 2 the P5 -> P6 max-pool of BiFPN cell 0 / node 6 sees a
+near-tie in image 0, channel 8 — two taps of one 3x3 window hold 2.01506268 and 2.01506146 in fp64
+(6e-7 apart), below fp32 resolution of the values, so the GPU routes that window's gradient to the
+other tap (TF's MaxPoolGrad picks the first maximum, as both implementations do; they only
+disagree on which value is larger).  That one routing moves 3.7e-3 of the d patch norm (every
+image receives it through the BN batch terms); the cosine stays >= 0.99999.
 """
 import numpy as np
 import pytest
@@ -48,7 +54,7 @@ def _step_vs_oracle(B):
     assert abs(met[_lib.M_LOSS] - ref["loss"]) <= 1e-5 * abs(ref["loss"])
     gp, rp = g[:-1], ref["grad"][:-1]
     assert _cos(gp, rp) >= 0.99999, _cos(gp, rp)
-    assert np.linalg.norm(gp - rp) / np.linalg.norm(rp) <= 1e-3
+    assert np.linalg.norm(gp - rp) / np.linalg.norm(rp) <= 5e-3
     assert abs(g[-1] - ref["grad"][-1]) <= 1e-5 * max(1.0, abs(ref["grad"][-1]))
     check_metric_row(met, ref, B)
     mt = torch.empty(B, device="cuda")
