@@ -24,12 +24,23 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# D0 @512 multiply-adds per image forward (efficientdet_arch_test.py:47-49); one step = clean fwd +
-# attack fwd + attack dgrad = 3 forward-equivalents, 2 FLOP per MAC
-D0_MACS = 2_532_997_127
+# multiply-adds per image forward at the model's native size (efficientdet_arch_test.py:47-114);
+# one step = clean fwd + attack fwd + attack dgrad = 3 forward-equivalents, 2 FLOP per MAC
+# (SURVEY.md 8d); other image sizes scale with the pixel count
+MACS = {"efficientdet-d0": (512, 2_532_997_127), "efficientdet-d1": (640, 6_095_640_824),
+        "efficientdet-d2": (768, 10_986_053_156), "efficientdet-d3": (896, 24_869_554_579),
+        "efficientdet-d4": (1024, 55_146_068_329), "efficientdet-lite0": (320, 977_617_221),
+        "efficientdet-lite4": (640, 20_221_443_966)}
+D0_MACS = MACS["efficientdet-d0"][1]
 FLOP_PER_IMAGE = 3 * 2 * D0_MACS
 PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 matrix / vector peak (MI355X_MICROARCH.md)
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+
+
+def flop_per_image(model, size):
+    native, macs = MACS.get(model, (512, D0_MACS))
+    return 3 * 2 * macs * (size / native) ** 2
 
 
 def synth_images(global_idx, size):
@@ -102,7 +113,7 @@ def pmc_traffic(kind):
     return None if e is None else e.get("bytes_per_launch")
 
 
-def kernel_roofline(kind, r):
+def kernel_roofline(kind, r, mfma_peak=PEAK_FP32_TFLOPS):
     """Roofline of the dominant launch group: its bound is the one whose peak-time for the group's
     algorithmic work is larger; achieved = algorithmic bytes (FLOPs) / measured time."""
     sec = r["ms"] * 1e-3
@@ -110,7 +121,7 @@ def kernel_roofline(kind, r):
     if hbm_bound:
         ach, peak, unit, bound = r["bytes"] / sec / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
     else:
-        ach, peak, unit, bound = r["flops"] / sec / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s", "mfma"
+        ach, peak, unit, bound = r["flops"] / sec / 1e12, mfma_peak, "TFLOP/s", "mfma"
     out = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
            "traffic": pmc_traffic(kind), "kernel": kind, "kernels": KIND_KERNELS.get(kind, kind),
            "launches": r["count"], "avg_us": round(1e3 * r["ms"] / r["count"], 2),
@@ -135,6 +146,9 @@ def main():
     ap.add_argument("--placement", choices=("injected", "first-pass"), default="injected",
                     help="injected: 1-3 synthetic person boxes per image (SURVEY.md 8d); first-pass: the "
                          "reference's own flow, patches go onto the first pass's soft-NMS boxes")
+    ap.add_argument("--dtype", choices=("f32", "bf16"), default="f32",
+                    help="1x1-conv arithmetic: f32 (the reference's precision, configs C1-C3) or bf16 "
+                         "(C4: bf16 matrix cores, fp32 accumulation)")
     ap.add_argument("--person-bias", type=float, default=0.0,
                     help="lift the person class-logit bias so the clean pass yields real soft-NMS candidates")
     args = ap.parse_args()
@@ -149,7 +163,7 @@ def main():
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker, _pad_boxes
     B, S = args.batch, args.image_size
     victim = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
-                                device=local, person_bias=args.person_bias)
+                                device=local, person_bias=args.person_bias, dtype=args.dtype)
     att = PatchAttacker(victim, seed=7, device=dev)
     ws_gb = victim.ctx.workspace_bytes(B) / 1e9
     gidx = list(range(rank * B, (rank + 1) * B))
@@ -183,9 +197,11 @@ def main():
         rep = victim.ctx.profile_report()
         victim.ctx.profile(False)
         kind, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
-        roofline = kernel_roofline(kind, r)
-        step_ach = FLOP_PER_IMAGE * images_per_s / world / 1e12
-        step_roof = {"achieved_tflops_per_gpu": round(step_ach, 3), "frac_fp32_peak": round(step_ach / PEAK_FP32_TFLOPS, 4),
+        mpeak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
+        roofline = kernel_roofline(kind, r, mpeak)
+        step_ach = flop_per_image(args.model, S) * images_per_s / world / 1e12
+        step_roof = {"achieved_tflops_per_gpu": round(step_ach, 3),
+                     "frac_mfma_peak": round(step_ach / mpeak, 4), "mfma_peak_tflops": mpeak,
                      "breakdown_ms": {k: round(v["ms"], 3) for k, v in sorted(rep.items(), key=lambda kv: -kv[1]["ms"])}}
         # bandwidth-aware conv roofline: sum over launches of max(bytes/HBM, flops/MFMA)
         roof_ms = sum(v.get("roof_ms", 0.0) for v in rep.values())
@@ -211,12 +227,13 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.dtype,
             "data": ("synthetic (U(-1,1) images, " + ("1-3 injected person boxes/image" if boxes is not None else
                      "placement from the first pass's soft-NMS boxes") + f", synthetic {args.model} weights"
                      + (f", person_bias {args.person_bias}" if args.person_bias else "") + ")"),
             "config": {"workload": (f"C{2 if world == 1 else 3}: EfficientDet-D0" if args.model == "efficientdet-d0"
-                                    else args.model) + f" patch attack {S}x{S}, "
+                                    else ("C4: " if args.model == "efficientdet-d4" else "") + args.model)
+                                   + f" patch attack {S}x{S}, "
                                    f"{B} images/GPU, bn=local", "global_batch": world * B, "image_size": S,
                        "workspace_gb_per_gpu": round(ws_gb, 3), "placement": args.placement,
                        "patches_per_step": int(met["patches"]),

@@ -48,6 +48,11 @@ enum {
  * inference BN with moving statistics (attacker.py:325 test_step). */
 enum { PHX_BN_LOCAL = 0, PHX_BN_FROZEN = 1 };
 
+/* Arithmetic of the victim's 1x1 convolutions ("C4: bf16 act, fp32 acc").
+ * F32: fp32 matrix cores (the reference's precision, BASELINE configs 1-3).  BF16: bf16 matrix
+ * cores with fp32 accumulation; BN statistics, depthwise convs, EOT and the loss stay fp32. */
+enum { PHX_DTYPE_F32 = 0, PHX_DTYPE_BF16 = 1 };
+
 typedef struct phx_config {
   const char* model_name;   /* "efficientdet-d0" ... "-d7", "efficientdet-lite0".."-lite4"
                                (hparams_config.py:301-467)                                  */
@@ -59,6 +64,7 @@ typedef struct phx_config {
                                pass keeps scores >= it (attacker.py:83-84) and gaussian soft-NMS
                                keeps scores > (it, or 0.001 when it is 0) (postprocess.py:186-188) */
   uint64_t seed;            /* Philox key for all EOT randomness                              */
+  int compute_dtype;        /* PHX_DTYPE_F32 / PHX_DTYPE_BF16                                  */
 } phx_config;
 
 typedef struct phx_ctx phx_ctx;

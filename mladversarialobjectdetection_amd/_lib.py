@@ -23,6 +23,7 @@ M_LOSS, M_SCALE_LOSS, M_TV, M_SUM_M, M_SUM_M2, M_ASR_NUM, M_ASR_DEN, M_NBOX, M_N
 NMETRIC = 9
 
 BN_LOCAL, BN_FROZEN = 0, 1
+DTYPE_F32, DTYPE_BF16 = 0, 1
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # PHX_LIB selects another in-tree build (libphx*.so next to this file) for A/B timing runs
@@ -43,6 +44,7 @@ class _Config(ctypes.Structure):
         ("bn_mode", c_int),
         ("score_thresh", c_float),
         ("seed", c_uint64),
+        ("compute_dtype", c_int),
     ]
 
 
@@ -125,11 +127,11 @@ class Context:
     """Owns one phx_ctx (one victim model on one device)."""
 
     def __init__(self, model_name="efficientdet-d0", image_size=0, max_batch=16,
-                 bn_mode=BN_LOCAL, score_thresh=0.5, seed=0, device=0):
+                 bn_mode=BN_LOCAL, score_thresh=0.5, seed=0, device=0, compute_dtype=DTYPE_F32):
         lib = load()
         self.lib = lib
         cfg = _Config(model_name.encode(), int(image_size), int(max_batch), int(bn_mode),
-                      float(score_thresh), int(seed) & ((1 << 64) - 1))
+                      float(score_thresh), int(seed) & ((1 << 64) - 1), int(compute_dtype))
         h = c_void_p()
         rc = lib.phx_create(ctypes.byref(cfg), int(device), ctypes.byref(h))
         if rc != 0:

@@ -86,13 +86,17 @@ class EfficientDetVictim:
 
     def __init__(self, model_name="efficientdet-d0", weights="synthetic", *, seed=0, image_size=0,
                  max_batch=16, bn_mode="local", score_thresh=0.5, rng_seed=0, device=None,
-                 person_bias=0.0):
+                 person_bias=0.0, dtype="f32"):
         if device is None:
             device = torch.cuda.current_device() if torch.cuda.is_available() else 0
         self.device = device
+        if dtype not in ("f32", "bf16"):
+            raise ValueError("dtype must be 'f32' (the reference's precision) or 'bf16'")
         self.ctx = _lib.Context(model_name, image_size, max_batch,
                                 _lib.BN_FROZEN if bn_mode == "frozen" else _lib.BN_LOCAL,
-                                score_thresh, rng_seed, device)
+                                score_thresh, rng_seed, device,
+                                _lib.DTYPE_BF16 if dtype == "bf16" else _lib.DTYPE_F32)
+        self.dtype = dtype
         self.manifest = self.ctx.manifest()
         if isinstance(weights, str) and weights == "synthetic":
             blob = wmod.synthetic_blob(self.manifest, seed=seed, person_bias=person_bias)

@@ -124,6 +124,7 @@ struct Exec {
   int* inj_count = nullptr;
   float* dscale_scratch = nullptr;  // dL/dscale of a gradient-free (eval) step
 
+  bool bf16 = false;  // the context's compute dtype (GEMM plans depend on it)
   size_t bytes = 0;  // device bytes owned by this executor
   uint64_t used = 0;  // phx_ctx::clock at the last use
   template <typename T>
@@ -152,6 +153,7 @@ struct Prof {
     std::string kind;
     hipEvent_t a, b;
     double flops, bytes;
+    double peak_tflops;  // the matrix-core peak the launch's FLOPs run at
   };
   bool on = false;
   std::vector<Rec> recs;
@@ -176,6 +178,7 @@ struct phx_ctx {
   int device = 0;
   int max_batch = 0;
   int bn_mode = PHX_BN_LOCAL;
+  bool bf16 = false;  // PHX_DTYPE_BF16: bf16 matrix cores for the 1x1 convs
   // nms_configs.score_thresh: the first pass keeps scores >= filter_thresh (attacker.py:83-84);
   // gaussian soft-NMS keeps scores > nms_thresh = score_thresh or 0.001 (postprocess.py:186-188)
   float score_thresh = 0.f;
@@ -304,7 +307,8 @@ std::string phx_ctx::model_info() const {
      << ",\"stddev_rgb\":" << arr3(c.stddev_rgb) << ",\"num_classes\":" << c.num_classes
      << ",\"survival_prob\":" << c.survival_prob << ",\"width_coefficient\":" << c.width_coefficient
      << ",\"depth_coefficient\":" << c.depth_coefficient << ",\"score_thresh\":" << filter_thresh
-     << ",\"nms_score_thresh\":" << nms_thresh << ",\"fpn_nodes\":[";
+     << ",\"nms_score_thresh\":" << nms_thresh << ",\"compute_dtype\":\"" << (bf16 ? "bf16" : "f32")
+     << "\",\"fpn_nodes\":[";
   const int nlev = c.max_level - c.min_level + 1;
   std::map<int, std::vector<int>> ids;
   for (int i = 0; i < nlev; ++i) ids[c.min_level + i] = {i};
@@ -344,7 +348,9 @@ struct Scope {
   Scope(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t st)
       : p(ctx->prof.on ? &ctx->prof : nullptr), s(st) {
     if (!p) return;
-    Prof::Rec r{kind, p->ev(), p->ev(), flops, bytes};
+    // GEMMs of a bf16 context run on the bf16 matrix cores; everything else at the fp32 rate
+    const double peak = (ctx->bf16 && std::string(kind) == "gemm") ? 2500.0 : 157.3;
+    Prof::Rec r{kind, p->ev(), p->ev(), flops, bytes, peak};
     PHX_HIP(hipEventRecord(r.a, s));
     p->recs.push_back(r);
     idx = p->recs.size() - 1;
@@ -388,6 +394,7 @@ Exec& phx_ctx::exec_for(int B) {
   auto ex = std::make_unique<Exec>();
   Exec& E = *ex;
   E.B = B;
+  E.bf16 = bf16;
   NetBuilder nb(mc, B, bn_mode == PHX_BN_LOCAL);
   nb.build();
   E.prog = nb.program();
@@ -442,7 +449,7 @@ Exec& phx_ctx::exec_for(int B) {
       const Tensor& to = P.tensors[pr.out];
       int np = 0;
       if (pr.t == OP_STEM) np = cdiv((long)to.rows(), 256);
-      else if (pr.t == OP_PW && to.c % 4 == 0) np = gemm_stat_partials((int)ti.rows(), to.c, ti.c);
+      else if (pr.t == OP_PW && to.c % 4 == 0) np = gemm_stat_partials((int)ti.rows(), to.c, ti.c, bf16);
       else if (pr.t == OP_DW) np = dw_stat_partials(ti.n, ti.h, ti.w, ti.c, to.h, to.w, pr.k, pr.stride, pr.pad_t, pr.pad_l);
       if (np <= 0) continue;
       E.fused_bn[i] = 1;
@@ -466,7 +473,7 @@ Exec& phx_ctx::exec_for(int B) {
       else if (L.t == OP_SE && L.in[0] == bn.out)
         np = ew_gstats_partials((long)li.h * li.w, li.c, li.n);
       else if (L.t == OP_PW && L.in[0] == bn.out && std::find(P.cls_out.begin(), P.cls_out.end(), L.out) == P.cls_out.end())
-        np = gemm_dgrad_gsink_partials((int)li.rows(), li.c, lo.c);
+        np = gemm_dgrad_gsink_partials((int)li.rows(), li.c, lo.c, bf16);
       else if (L.t == OP_ADD && (L.in[0] == bn.out || L.in[1] == bn.out) && L.in[0] != L.in[1])
         np = ew_gstats_partials((long)tz.rows(), tz.c, 1);
       if (np <= 0 || tz.c % 4) continue;
@@ -509,8 +516,8 @@ Exec& phx_ctx::exec_for(int B) {
     if (op.t != OP_PW) continue;
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
-    gp_need = std::max(gp_need, gemm_partial_floats((int)ti.rows(), to.c, ti.c));  // forward
-    gp_need = std::max(gp_need, gemm_partial_floats((int)ti.rows(), ti.c, to.c));  // dgrad
+    gp_need = std::max(gp_need, gemm_partial_floats((int)ti.rows(), to.c, ti.c, bf16));  // forward
+    gp_need = std::max(gp_need, gemm_partial_floats((int)ti.rows(), ti.c, to.c, bf16));  // dgrad
   }
   E.gpart = E.alloc<float>(gp_need);
   E.red = E.alloc<double>(red_need);
@@ -686,8 +693,8 @@ bool group_uniform(const Exec& E, const std::vector<int>& v) {
   if (a.t == OP_PW) {
     const Tensor& ta = P.tensors[a.in[0]];
     const Tensor& tb = P.tensors[a.out];
-    if (!gemm_group_ok(M.data(), (int)M.size(), tb.c, ta.c)) return false;  // forward
-    if (a.bwd && !gemm_group_ok(M.data(), (int)M.size(), ta.c, tb.c)) return false;  // dgrad
+    if (!gemm_group_ok(M.data(), (int)M.size(), tb.c, ta.c, E.bf16)) return false;  // forward
+    if (a.bwd && !gemm_group_ok(M.data(), (int)M.size(), ta.c, tb.c, E.bf16)) return false;  // dgrad
   }
   return true;
 }
@@ -811,7 +818,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
         segs[r] = GemmSeg{view(ctx, E, op.in[0], input), GradX{}, op.b >= 0 ? W + op.b : nullptr,
                           E.tptr(op.out, input), (int)P.tensors[op.in[0]].rows(), false, sink_of(r), GradSink{}};
       }
-      const int np = gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s);
+      const int np = gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s, E.bf16);
       if (sink_on)
         for (int r = 0; r < n; ++r) {
           E.stat_P[P.ops[g[r]].out] = np;
@@ -905,7 +912,7 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                           (int)P.tensors[op.in[0]].rows(), op.acc[0], StatSink{}, gsk_of(r)};
       }
       // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
-      const int np = gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s);
+      const int np = gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s, E.bf16);
       if (gs_on)
         for (int r = 0; r < n; ++r) {
           E.gstat_P[g[r] - 1] = np;
@@ -993,7 +1000,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
           rpi = ti.h * ti.w;
         }
         np = launch_gemm(A, ctx->wt_of(op.w), op.b >= 0 ? W + op.b : nullptr, y, (int)ti.rows(), to.c,
-                         ti.c, false, rs, rpi, s, E.gpart, sink);
+                         ti.c, false, rs, rpi, s, E.gpart, sink, E.bf16);
         break;
       }
       case OP_DW:
@@ -1151,7 +1158,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_PW:
         // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
         np = launch_gemm_dgrad(gview(ctx, E, op.out, input), W + op.w, dx, (int)ti.rows(), ti.c, to.c,
-                               op.acc[0], s, E.gpart, gsk);
+                               op.acc[0], s, E.gpart, gsk, E.bf16);
         break;
       case OP_DW:
         np = launch_dw_bwd(gview(ctx, E, op.out, input), W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k,
@@ -1288,6 +1295,9 @@ int phx_create(const phx_config* cfg, int device, phx_ctx** out) {
     ctx->device = device;
     ctx->max_batch = cfg->max_batch > 0 ? cfg->max_batch : 1;
     ctx->bn_mode = cfg->bn_mode;
+    if (cfg->compute_dtype != PHX_DTYPE_F32 && cfg->compute_dtype != PHX_DTYPE_BF16)
+      throw std::invalid_argument("unknown compute_dtype");
+    ctx->bf16 = cfg->compute_dtype == PHX_DTYPE_BF16;
     ctx->set_score_thresh(cfg->score_thresh);
     ctx->seed = cfg->seed;
     NetBuilder nb(ctx->mc, 0);
@@ -1673,7 +1683,8 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   if (!ctx) return PHX_EINVAL;
   PHX_TRY(ctx)
   // per launch group: measured time and the roofline time of its algorithmic work at the MI355X
-  // peaks (HBM 8 TB/s, fp32 MFMA 157.3 TFLOP/s); roof = sum over launches of max(hbm, mfma)
+  // peaks (HBM 8 TB/s; fp32 MFMA 157.3 TFLOP/s, bf16 2.5 PFLOP/s for bf16 GEMMs); roof = sum over
+  // launches of max(hbm, mfma)
   struct Agg { long n = 0; double ms = 0, flops = 0, bytes = 0, hbm_ms = 0, mfma_ms = 0, roof_ms = 0; };
   std::map<std::string, Agg> agg;
   for (auto& r : ctx->prof.recs) {
@@ -1685,7 +1696,7 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
     a.ms += ms;
     a.flops += r.flops;
     a.bytes += r.bytes;
-    const double th = r.bytes / 8.0e12 * 1e3, tm = r.flops / 157.3e12 * 1e3;
+    const double th = r.bytes / 8.0e12 * 1e3, tm = r.flops / (r.peak_tflops * 1e12) * 1e3;
     a.hbm_ms += th;
     a.mfma_ms += tm;
     a.roof_ms += std::max(th, tm);

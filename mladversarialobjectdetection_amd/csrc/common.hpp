@@ -52,6 +52,26 @@ __device__ __forceinline__ float act_grad(float z, int act) {
 }
 
 // ------------------------------------------------------------------------------------------
+// bf16 (the C4 configuration's activation / matrix-core type): round-to-nearest-even packing by
+// v_cvt_pk_bf16_f32, widening by a 16-bit shift.
+// ------------------------------------------------------------------------------------------
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint2 pack_bf16x4(float4 v) {
+  const f4v_t w = {v.x, v.y, v.z, v.w};
+  return __builtin_bit_cast(uint2, __builtin_convertvector(w, bf16x4_t));
+}
+__device__ __forceinline__ float4 unpack_bf16x4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ float round_bf16(float f) {
+  return __uint_as_float((uint32_t)__builtin_bit_cast(unsigned short, (__bf16)f) << 16);
+}
+
+// ------------------------------------------------------------------------------------------
 // InX: an input tensor as its consumers see it.  The output of a training-mode batch norm is
 // never materialised: consumers read the BN input y and apply a = act((y - mu) * sc + be) on
 // load (sc = gamma * rstd, be = beta), so every BN costs one statistics pass instead of a

@@ -29,34 +29,36 @@ struct GemmPlan {
   int nt, wm, gx, gy, splits, kslice;
 };
 GemmPlan plan_gemm(int M, int N, int K);
-size_t gemm_partial_floats(int M, int N, int K);
+// bf16: the 1x1 convs with N > 16 run on the bf16 matrix cores (A view applied in fp32, rounded to
+// bf16 in LDS; fp32 accumulation and epilogue) — the C4 configuration's compute type
+size_t gemm_partial_floats(int M, int N, int K, bool bf16 = false);
 // returns the StatSink partial rows written (see gemm_stat_partials)
 int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-                float* partial, StatSink sink = StatSink{});
-int gemm_stat_partials(int M, int N, int K);
+                float* partial, StatSink sink = StatSink{}, bool bf16 = false);
+int gemm_stat_partials(int M, int N, int K, bool bf16 = false);
 // the two GEMM implementations behind launch_gemm (gemm_impl(): PHX_GEMM env, default 2)
 struct Gemm2Plan {
   int wm, tm, tn, mtiles, gx, gy, splits, kslice;
 };
-Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs);
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false);
 int gemm_impl();
-int gemm_impl_for(int N);
+int gemm_impl_for(int N, bool bf16 = false);
 int gemm2_target_wgs();
 int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
               float* partial, StatSink sink, GradSink gsk = GradSink{});
 int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-              float* partial, StatSink sink, int target_wgs, GradSink gsk = GradSink{});
+              float* partial, StatSink sink, int target_wgs, GradSink gsk = GradSink{}, bool bf16 = false);
 int gemm_splitk_stats_partials(int M, int N);
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
                        bool acc, StatSink sink, hipStream_t s);
 // dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
 // with a GradSink, the BN-backward sums of the dgrad's result (returns the partial rows)
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
-                      hipStream_t s, float* partial, GradSink gs = GradSink{});
-int gemm_dgrad_gsink_partials(int M, int N, int K);
+                      hipStream_t s, float* partial, GradSink gs = GradSink{}, bool bf16 = false);
+int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16 = false);
 // Grouped GEMM: members share Bt [N][K] (weights shared across pyramid levels) and differ in A,
 // C, M and sinks.  mode as gemm2 (0 raw, 1 BN view, 3 gradient view).  No split-K: see
 // gemm_group_ok.  Returns the partial rows P written per member (the same for all).
@@ -70,8 +72,9 @@ struct GemmSeg {
   StatSink sink;
   GradSink gsk;
 };
-bool gemm_group_ok(const int* M, int n, int N, int K);
-int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s);
+bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16 = false);
+int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s,
+                   bool bf16 = false);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
 int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
                   int Wo, int k, int stride, int pt, int pl, hipStream_t s,

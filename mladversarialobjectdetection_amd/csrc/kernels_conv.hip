@@ -795,9 +795,9 @@ GemmPlan plan_gemm(int M, int N, int K) {
   return p;
 }
 
-size_t gemm_partial_floats(int M, int N, int K) {
+size_t gemm_partial_floats(int M, int N, int K, bool bf16) {
   GemmPlan p = plan_gemm(M, N, K);
-  Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs());
+  Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16);
   const size_t a = p.splits > 1 ? (size_t)p.splits * M * N : 0;
   const size_t b = q.splits > 1 ? (size_t)q.splits * M * N : 0;
   return std::max(a, b);
@@ -814,7 +814,7 @@ static int gemm_impl_env() {
 }
 // default (0): the 32x32 LDS-tiled kernel except for 16-wide outputs, where its 32-column tile
 // would idle half the matrix core and the 16x16 register kernel streams faster (tools/gemm_bench)
-int gemm_impl_for(int N) {
+int gemm_impl_for(int N, bool) {
   const int e = gemm_impl_env();
   if (e) return e;
   return N <= 16 ? 1 : 2;
@@ -842,9 +842,9 @@ static int splitk_stats_rb(int M, int N) {
 int gemm_splitk_stats_partials(int M, int N) { return cdiv(M, splitk_stats_rb(M, N)); }
 
 // 0: the statistics cannot be fused into this GEMM (split-K with N > 1024)
-int gemm_stat_partials(int M, int N, int K) {
-  if (gemm_impl_for(N) == 2) {
-    Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs());
+int gemm_stat_partials(int M, int N, int K, bool bf16) {
+  if (gemm_impl_for(N, bf16) == 2) {
+    Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16);
     if (q.splits > 1) return N <= 1024 ? gemm_splitk_stats_partials(M, N) : 0;
     return q.gx;
   }
@@ -923,20 +923,20 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
 
 int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int N, int K,
                 bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-                float* partial, StatSink sink) {
+                float* partial, StatSink sink, bool bf16) {
   if (rowscale && !A.mu) throw std::runtime_error("gemm: rowscale requires a BN view");
   const int mode = rowscale ? 2 : (A.mu ? 1 : 0);
-  if (gemm_impl_for(N) == 2)
+  if (gemm_impl_for(N, bf16) == 2)
     return gemm2_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink,
-                     gemm2_target_wgs(), GradSink{});
+                     gemm2_target_wgs(), GradSink{}, bf16);
   return gemm1_run(mode, A, GradX{}, Bt, bias, C, M, N, K, acc, rowscale, rows_per_img, s, partial, sink,
                    GradSink{});
 }
 
 // GradSink partial rows a dgrad GEMM of this shape writes (0: the sums cannot be fused: split-K)
-int gemm_dgrad_gsink_partials(int M, int N, int K) {
-  if (gemm_impl_for(N) == 2) {
-    Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs());
+int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16) {
+  if (gemm_impl_for(N, bf16) == 2) {
+    Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16);
     return q.splits > 1 ? 0 : q.gx;
   }
   GemmPlan p = plan_gemm(M, N, K);
@@ -944,11 +944,11 @@ int gemm_dgrad_gsink_partials(int M, int N, int K) {
 }
 
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
-                      hipStream_t s, float* partial, GradSink gs) {
+                      hipStream_t s, float* partial, GradSink gs, bool bf16) {
   InX raw{A.da, nullptr, nullptr, nullptr, 0};
-  if (gemm_impl_for(N) == 2)
+  if (gemm_impl_for(N, bf16) == 2)
     return gemm2_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{},
-                     gemm2_target_wgs(), gs);
+                     gemm2_target_wgs(), gs, bf16);
   return gemm1_run(A.y ? 3 : 0, raw, A, Bt, nullptr, C, M, N, K, acc, nullptr, 1, s, partial, StatSink{}, gs);
 }
 

@@ -61,18 +61,25 @@ struct Gemm2Group {
   int n;
 };
 
-template <int WM, int TM, int TN, int MODE>
+// BF: bf16 matrix cores (v_mfma_f32_32x32x16_bf16, fp32 accumulation) — the A view is applied in
+// fp32 and rounded to bf16 when the chunk is written to LDS, B (the weights) likewise; K advances in
+// 32-deep chunks (two MFMAs per tile pair).  fp32 (BF = 0): v_mfma_f32_32x32x2_f32, 16-deep chunks.
+template <int WM, int TM, int TN, int MODE, bool BF = false>
 struct G2 {
   static constexpr int WN = 4 / WM;
-  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = 16, LD = BK + 4;
-  static constexpr int NA = (BM * 4 + 255) / 256;    // A float4 per thread per chunk
-  static constexpr int NB = (BN * 4 + 255) / 256;     // B float4 per thread per chunk
-  static constexpr int LDS_FLOATS = 2 * (BM + BN) * LD;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = BF ? 32 : 16;
+  static constexpr int LD = BF ? BK + 8 : BK + 4;    // LDS row pitch in elements (16-B aligned rows)
+  static constexpr int KQ = BK / 4;                   // float4 per tile row per chunk
+  static constexpr int RPP = 256 / KQ;                // tile rows loaded per pass of the 256 lanes
+  static constexpr int NA = (BM + RPP - 1) / RPP;     // A float4 per thread per chunk
+  static constexpr int NB = (BN + RPP - 1) / RPP;     // B float4 per thread per chunk
+  static constexpr int ESZ = BF ? 2 : 4;              // bytes per LDS element
+  static constexpr int LDS_FLOATS = 2 * (BM + BN) * LD * ESZ / 4;
 };
 
-template <int WM, int TM, int TN, int MODE>
+template <int WM, int TM, int TN, int MODE, bool BF = false>
 struct G2Regs {
-  using P = G2<WM, TM, TN, MODE>;
+  using P = G2<WM, TM, TN, MODE, BF>;
   float4 a[P::NA];
   float4 y[MODE == 3 ? P::NA : 1];
   float4 rs[MODE == 2 ? P::NA : 1];
@@ -81,12 +88,12 @@ struct G2Regs {
   GChan4 gk;
 };
 
-template <int WM, int TM, int TN, int MODE>
-__device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE>& r, const Gemm2Args& a, int m0, int n0,
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, int m0, int n0,
                                         int k0, int kend) {
-  using P = G2<WM, TM, TN, MODE>;
+  using P = G2<WM, TM, TN, MODE, BF>;
   const int t = threadIdx.x;
-  const int c4 = t & 3;
+  const int c4 = t % P::KQ;
   const int kk = k0 + 4 * c4;
   const bool kok = kk < kend;
   if (MODE == 1 || MODE == 2) {
@@ -97,8 +104,8 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE>& r, const Gemm2
   }
 #pragma unroll
   for (int u = 0; u < P::NA; ++u) {
-    const int row = m0 + ((t + 256 * u) >> 2);
-    const bool ok = kok && row < a.M && t + 256 * u < P::BM * 4;
+    const int row = m0 + (t + 256 * u) / P::KQ;
+    const bool ok = kok && row < a.M && t + 256 * u < P::BM * P::KQ;
     const long e = (long)row * a.K + kk;
     if (MODE == 3) {
       r.a[u] = ok ? *reinterpret_cast<const float4*>(a.G.da + e) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -113,26 +120,38 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE>& r, const Gemm2
 #pragma unroll
   for (int u = 0; u < P::NB; ++u) {
     const int idx = t + 256 * u;
-    const int col = n0 + (idx >> 2);
-    const int kb = k0 + 4 * (idx & 3);
-    const bool ok = idx < P::BN * 4 && col < a.N && kb < kend;
+    const int col = n0 + idx / P::KQ;
+    const int kb = k0 + 4 * (idx % P::KQ);
+    const bool ok = idx < P::BN * P::KQ && col < a.N && kb < kend;
     r.b[u] = ok ? *reinterpret_cast<const float4*>(a.Bt + (long)col * a.K + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
 }
 
-template <int WM, int TM, int TN, int MODE>
-__device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE>& r, const Gemm2Args& a, float* sm,
+// element (row, k) of the A / B tile of LDS buffer `buf` (fp32 or bf16 elements)
+template <class P>
+__device__ __forceinline__ char* g2_tile(float* sm, int buf, bool b, int row, int k) {
+  char* base = reinterpret_cast<char*>(sm) + (size_t)buf * (P::BM + P::BN) * P::LD * P::ESZ;
+  if (b) base += (size_t)P::BM * P::LD * P::ESZ;
+  return base + ((size_t)row * P::LD + k) * P::ESZ;
+}
+
+template <class P>
+__device__ __forceinline__ void g2_put4(float* sm, int buf, bool b, int row, int k, float4 v) {
+  if constexpr (P::ESZ == 2) *reinterpret_cast<uint2*>(g2_tile<P>(sm, buf, b, row, k)) = pack_bf16x4(v);
+  else *reinterpret_cast<float4*>(g2_tile<P>(sm, buf, b, row, k)) = v;
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, float* sm,
                                          int buf, int m0, int k0, int kend) {
-  using P = G2<WM, TM, TN, MODE>;
+  using P = G2<WM, TM, TN, MODE, BF>;
   const int t = threadIdx.x;
-  const int c4 = t & 3;
+  const int c4 = t % P::KQ;
   const bool kok = k0 + 4 * c4 < kend;
-  float* As = sm + buf * (P::BM + P::BN) * P::LD;
-  float* Bs = As + P::BM * P::LD;
 #pragma unroll
   for (int u = 0; u < P::NA; ++u) {
-    if (t + 256 * u >= P::BM * 4) continue;
-    const int rl = (t + 256 * u) >> 2;
+    if (t + 256 * u >= P::BM * P::KQ) continue;
+    const int rl = (t + 256 * u) / P::KQ;
     float4 v = r.a[u];
     if (kok && m0 + rl < a.M) {
       if (MODE == 1 || MODE == 2) v = inx_apply4(a.A, r.ck, v);
@@ -143,26 +162,26 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE>& r, cons
     } else {
       v = make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    *reinterpret_cast<float4*>(As + rl * P::LD + 4 * c4) = v;
+    g2_put4<P>(sm, buf, false, rl, 4 * c4, v);
   }
 #pragma unroll
   for (int u = 0; u < P::NB; ++u) {
     const int idx = t + 256 * u;
-    if (idx < P::BN * 4) *reinterpret_cast<float4*>(Bs + (idx >> 2) * P::LD + 4 * (idx & 3)) = r.b[u];
+    if (idx < P::BN * P::KQ) g2_put4<P>(sm, buf, true, idx / P::KQ, 4 * (idx % P::KQ), r.b[u]);
   }
 }
 
 // SK: 0 plain, 1 StatSink (BN statistics of C), 2 GradSink (BN-backward sums of a dgrad's C)
-template <int WM, int TM, int TN, int MODE, int SK, int NS>
+template <int WM, int TM, int TN, int MODE, int SK, int NS, bool BF>
 __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
   const int zper = NS == 1 ? (int)gridDim.z : (int)gridDim.z / grp.n;
   const int seg = NS == 1 ? 0 : (int)blockIdx.z / zper;
   const int zs = (int)blockIdx.z - seg * zper;
   const Gemm2Args a = pick_seg(grp.a, seg);
   constexpr bool STATS = SK == 1;
-  using P = G2<WM, TM, TN, MODE>;
-  constexpr int WN = P::WN, BM = P::BM, BN = P::BN, BK = P::BK, LD = P::LD;
-  __shared__ float sm[P::LDS_FLOATS];
+  using P = G2<WM, TM, TN, MODE, BF>;
+  constexpr int WN = P::WN, BM = P::BM, BN = P::BN, BK = P::BK;
+  __shared__ __attribute__((aligned(16))) float sm[P::LDS_FLOATS];
   __shared__ float2 wst[SK ? 4 : 1][SK ? TN * 32 : 1];
   __shared__ float wcn[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -183,9 +202,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
 
   int tile = blockIdx.x;
   if (tile < a.mtiles && ksteps > 0) {
-    G2Regs<WM, TM, TN, MODE> rg;
-    g2_load<WM, TM, TN, MODE>(rg, a, tile * BM, n0, kbeg, kend);
-    g2_store<WM, TM, TN, MODE>(rg, a, sm, 0, tile * BM, kbeg, kend);
+    G2Regs<WM, TM, TN, MODE, BF> rg;
+    g2_load<WM, TM, TN, MODE, BF>(rg, a, tile * BM, n0, kbeg, kend);
+    g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, 0, tile * BM, kbeg, kend);
     __syncthreads();
     int buf = 0, kc = 0;
     floatx16 acc[TM][TN];
@@ -203,10 +222,28 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
         nkc = 0;
       }
       const bool have_next = ntile < a.mtiles;
-      if (have_next) g2_load<WM, TM, TN, MODE>(rg, a, ntile * BM, n0, kbeg + nkc * BK, kend);
+      if (have_next) g2_load<WM, TM, TN, MODE, BF>(rg, a, ntile * BM, n0, kbeg + nkc * BK, kend);
       // MFMAs on the staged chunk
-      {
-        const float* As = sm + buf * (BM + BN) * LD;
+      if constexpr (BF) {
+        // lane (r32, h) feeds row / column r32 with k = 16*kk + 8*h .. +7 (one ds_read_b128 each)
+#pragma unroll
+        for (int kk = 0; kk < BK / 16; ++kk) {
+          bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            fa[i] = *reinterpret_cast<const bf16x8_t*>(g2_tile<P>(sm, buf, false, wm * TM * 32 + i * 32 + r32, 16 * kk + 8 * h));
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            fb[j] = *reinterpret_cast<const bf16x8_t*>(g2_tile<P>(sm, buf, true, wn * TN * 32 + j * 32 + r32, 16 * kk + 8 * h));
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+      } else {
+        constexpr int LD = P::LD;
+        const float* As = reinterpret_cast<const float*>(g2_tile<P>(sm, buf, false, 0, 0));
         const float* Bs = As + BM * LD;
 #pragma unroll
         for (int s8 = 0; s8 < BK / 8; ++s8) {
@@ -338,7 +375,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
       }
       if (!have_next) break;
-      g2_store<WM, TM, TN, MODE>(rg, a, sm, buf ^ 1, ntile * BM, kbeg + nkc * BK, kend);
+      g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, buf ^ 1, ntile * BM, kbeg + nkc * BK, kend);
       __syncthreads();
       buf ^= 1;
       tile = ntile;
@@ -382,7 +419,7 @@ static G2Cfg g2_pick(int N) {
   return {2, 2, 2};
 }
 
-Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
   Gemm2Plan p;
   G2Cfg c = g2_pick(N);
   // few 128x128 tiles (small M, wide N, no split-K): 64-row tiles double the workgroups so
@@ -415,7 +452,8 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
   }();
   if (tiles < split_below && K >= 256)
     p.splits = std::max(1, std::min<int>((int)((2 * split_below + tiles - 1) / tiles), K / 128));
-  p.kslice = ((K + p.splits - 1) / p.splits + 15) / 16 * 16;
+  const int bk = bf16 ? 32 : 16;  // K chunk of the kernel variant
+  p.kslice = ((K + p.splits - 1) / p.splits + bk - 1) / bk * bk;
   p.splits = (K + p.kslice - 1) / p.kslice;
   const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
   p.gx = (int)std::min<long>(p.mtiles, want);
@@ -431,30 +469,31 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs) {
 }
 
 template <int WM, int TM, int TN, int MODE, int SK, int NS>
-static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a) {
-  hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS>), g, dim3(256), 0, s, a);
+static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf) {
+  if (bf) hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true>), g, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, false>), g, dim3(256), 0, s, a);
 }
 
 // sk: 1 forward statistics (modes 0-2), 2 BN-backward sums (dgrad modes 0, 3)
 template <int WM, int TM, int TN, int NS>
-static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a) {
+static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf) {
   switch (mode) {
     case 0:
-      if (sk == 1) g2_go<WM, TM, TN, 0, 1, NS>(g, s, a);
-      else if (sk == 2) g2_go<WM, TM, TN, 0, 2, NS>(g, s, a);
-      else g2_go<WM, TM, TN, 0, 0, NS>(g, s, a);
+      if (sk == 1) g2_go<WM, TM, TN, 0, 1, NS>(g, s, a, bf);
+      else if (sk == 2) g2_go<WM, TM, TN, 0, 2, NS>(g, s, a, bf);
+      else g2_go<WM, TM, TN, 0, 0, NS>(g, s, a, bf);
       break;
-    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1, NS>(g, s, a) : g2_go<WM, TM, TN, 1, 0, NS>(g, s, a); break;
-    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1, NS>(g, s, a) : g2_go<WM, TM, TN, 2, 0, NS>(g, s, a); break;
-    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2, NS>(g, s, a) : g2_go<WM, TM, TN, 3, 0, NS>(g, s, a); break;
+    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1, NS>(g, s, a, bf) : g2_go<WM, TM, TN, 1, 0, NS>(g, s, a, bf); break;
+    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1, NS>(g, s, a, bf) : g2_go<WM, TM, TN, 2, 0, NS>(g, s, a, bf); break;
+    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2, NS>(g, s, a, bf) : g2_go<WM, TM, TN, 3, 0, NS>(g, s, a, bf); break;
   }
 }
 
 int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-              float* partial, StatSink sink, int target_wgs, GradSink gsk) {
+              float* partial, StatSink sink, int target_wgs, GradSink gsk, bool bf16) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
-  const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs);
+  const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs, bf16);
   const bool stats = sink.part != nullptr;
   if (stats && (acc || mode == 3 || (N & 3) || (p.splits > 1 && N > 1024)))
     throw std::runtime_error("gemm: unsupported statistics epilogue");
@@ -472,14 +511,14 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   dim3 g(p.gx, p.gy, p.splits);
   const int key = p.wm * 100 + p.tm * 10 + p.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a); break;
-    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a); break;
-    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a); break;
-    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a); break;
-    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a); break;
-    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a); break;
-    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a); break;
-    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a); break;
+    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a, bf16); break;
+    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a, bf16); break;
+    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a, bf16); break;
+    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a, bf16); break;
+    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a, bf16); break;
+    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a, bf16); break;
+    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a, bf16); break;
+    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a, bf16); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
@@ -487,17 +526,18 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   return p.gx;
 }
 
-bool gemm_group_ok(const int* M, int n, int N, int K) {
-  if (n < 1 || n > kMaxSeg || gemm_impl_for(N) != 2) return false;
+bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16) {
+  if (n < 1 || n > kMaxSeg || gemm_impl_for(N, bf16) != 2) return false;
   for (int i = 0; i < n; ++i)
-    if (plan_gemm2(M[i], N, K, gemm2_target_wgs()).splits != 1) return false;
+    if (plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16).splits != 1) return false;
   return true;
 }
 
-int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s) {
+int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s,
+                   bool bf16) {
   std::vector<int> M(n);
   for (int i = 0; i < n; ++i) M[i] = segs[i].M;
-  if (!gemm_group_ok(M.data(), n, N, K)) throw std::runtime_error("gemm group: unsupported shapes");
+  if (!gemm_group_ok(M.data(), n, N, K, bf16)) throw std::runtime_error("gemm group: unsupported shapes");
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
   const bool stats = segs[0].sink.part != nullptr, gs = segs[0].gsk.part != nullptr;
   if (stats && (mode == 3 || (N & 3))) throw std::runtime_error("gemm group: unsupported statistics");
@@ -507,7 +547,7 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
   int gx = 1;
   Gemm2Plan p0{};
   for (int i = 0; i < n; ++i) {
-    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs());
+    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16);
     if (i == 0) p0 = p;
     gx = std::max(gx, p.gx);
   }
@@ -526,14 +566,14 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
   dim3 grid(gx, p0.gy, n);
   const int key = p0.wm * 100 + p0.tm * 10 + p0.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a); break;
-    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a); break;
+    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();

@@ -144,6 +144,33 @@ def fuse_nodes(nodes, wsm, method):
     return out
 
 
+def _rbf16(t):
+    """round to bf16 (nearest even) and back"""
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+class Bf16Conv1x1(torch.autograd.Function):
+    """A 1x1 convolution as the library's bf16 GEMM computes it (PHX_DTYPE_BF16, SURVEY.md 8a R4
+    "C4: bf16 act, fp32 acc"): operands rounded to bf16, products accumulated in full precision.
+    Forward rounds x and w when the GEMM's N (output channels) > 16; the data gradient rounds dy and
+    w when its N (input channels) > 16 — smaller GEMMs run on the fp32 register kernel."""
+
+    @staticmethod
+    def forward(ctx, x, w, rnd_fwd, rnd_bwd):
+        ctx.save_for_backward(w)
+        ctx.rnd_bwd = rnd_bwd
+        if rnd_fwd:
+            x, w = _rbf16(x), _rbf16(w)
+        return F.conv2d(x, w)
+
+    @staticmethod
+    def backward(ctx, g):
+        (w,) = ctx.saved_tensors
+        if ctx.rnd_bwd:
+            g, w = _rbf16(g), _rbf16(w)
+        return torch.einsum("nohw,oi->nihw", g, w[:, :, 0, 0]), None, None, None
+
+
 class Relu6(torch.autograd.Function):
     """tf.nn.relu6 with TF's Relu6Grad: the gradient passes on the open interval (0, 6)."""
 
@@ -172,6 +199,8 @@ class Detector:
         # trainable=False (attack_detection.py:46-47; the library's bn=frozen mode); drop connect
         # still follows `training`
         self.bn_frozen = bn_frozen
+        # bf16: emulate the library's PHX_DTYPE_BF16 1x1-conv arithmetic (Bf16Conv1x1)
+        self.bf16 = False
         # drop-connect draws: dict(seed, step, gimg0, pass) — pass 0 first, 1 second, 2 detect
         self.drop = drop
         self._cache = {}
@@ -195,7 +224,12 @@ class Detector:
         pl, pr = same_pads(x.shape[3], kw, stride)
         if pt or pb or pl or pr:
             x = F.pad(x, (pl, pr, pt, pb))
-        y = F.conv2d(x, wt, stride=stride)
+        if self.bf16 and kh == 1 and kw == 1 and "/se/" not in kname:
+            cin, cout = wt.shape[1], wt.shape[0]
+            # the class-predict conv's data gradient is the library's sparse fp32 scatter
+            y = Bf16Conv1x1.apply(x, wt, cout > 16, cin > 16 and "class-predict" not in kname)
+        else:
+            y = F.conv2d(x, wt, stride=stride)
         if bias is not None:
             y = y + self.w(bias).view(1, -1, 1, 1)
         return y

@@ -50,7 +50,7 @@ def asr_counts(first, second):
 
 def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0=0,
                 model="efficientdet-d0", image_size=None, add_tv=True, score_thresh=0.5,
-                dtype=torch.float64, training=True, image_grad=False, bn_frozen=False):
+                dtype=torch.float64, training=True, image_grad=False, bn_frozen=False, bf16=False):
     """Returns dict(loss, grad (NPARAM float64: [patch | scale]), m (per image), patched, ...).
 
     boxes: None -> first-pass soft-NMS boxes (the reference); else a list per image of [n,4]
@@ -60,6 +60,7 @@ def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0
     image_size = image_size or D.MODELS[model]["image_size"]
     det = D.Detector(weights, model, image_size, dtype=dtype, training=training,
                      drop=dict(seed=seed, step=step, gimg0=gimg0, **{"pass": 0}), bn_frozen=bn_frozen)
+    det.bf16 = bf16  # emulate the library's bf16 1x1-conv arithmetic
     images_t = torch.as_tensor(np.asarray(images, dtype=np.float64), dtype=dtype)
     B = images_t.shape[0]
     fp = first_pass(det, images_t, image_size, score_thresh)

