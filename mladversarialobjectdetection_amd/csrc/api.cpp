@@ -341,16 +341,39 @@ int fail(phx_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
+// PHX_PROF_DETAIL=1: launch groups are split by shape ("gemm fwd M=.. N=.. K=..") for tuning
+bool prof_detail() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_PROF_DETAIL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+std::string op_tag(const Program& P, const Op& op, bool bwd) {
+  const Tensor& ti = P.tensors[op.in[0]];
+  const Tensor& to = P.tensors[op.out];
+  char b[160];
+  if (op.t == OP_PW)
+    snprintf(b, sizeof b, " %s M=%zu N=%d K=%d", bwd ? "dgrad" : "fwd", ti.rows(), bwd ? ti.c : to.c,
+             bwd ? to.c : ti.c);
+  else if (op.t == OP_DW)
+    snprintf(b, sizeof b, " %dx%dx%d k%d s%d", ti.h, ti.w, ti.c, op.k, op.stride);
+  else
+    snprintf(b, sizeof b, " %dx%dx%dx%d", ti.n, ti.h, ti.w, ti.c);
+  return b;
+}
+
 struct Scope {
   Prof* p;
   size_t idx;
   hipStream_t s;
-  Scope(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t st)
+  Scope(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t st, const std::string& tag = "")
       : p(ctx->prof.on ? &ctx->prof : nullptr), s(st) {
     if (!p) return;
     // GEMMs of a bf16 context run on the bf16 matrix cores; everything else at the fp32 rate
     const double peak = (ctx->bf16 && std::string(kind) == "gemm") ? 2500.0 : 157.3;
-    Prof::Rec r{kind, p->ev(), p->ev(), flops, bytes, peak};
+    Prof::Rec r{std::string(kind) + (prof_detail() ? tag : std::string()), p->ev(), p->ev(), flops, bytes, peak};
     PHX_HIP(hipEventRecord(r.a, s));
     p->recs.push_back(r);
     idx = p->recs.size() - 1;
@@ -790,7 +813,8 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
     by += o0.t == OP_BN ? 8.0 * (double)E.stat_P[P.ops[i].in[0]] * ti.c : 4.0 * (double)(ti.numel() + to.numel());
   }
   if (o0.t == OP_PW) by += 4.0 * ti0.c * to0.c;
-  Scope scope(ctx, o0.t == OP_PW ? "gemm" : o0.t == OP_DW ? "dw_fwd" : "bn_stats", fl, by, s);
+  Scope scope(ctx, o0.t == OP_PW ? "gemm" : o0.t == OP_DW ? "dw_fwd" : "bn_stats", fl, by, s,
+              prof_detail() ? " group" + op_tag(P, o0, false) : std::string());
   switch (o0.t) {
     case OP_DW: {
       DwSeg segs[kMaxSeg];
@@ -881,7 +905,8 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
     }
   }
   if (o0.t == OP_PW) by += 4.0 * ti0.c * to0.c;
-  Scope scope(ctx, o0.t == OP_PW ? "gemm" : o0.t == OP_DW ? "dw_bwd" : "bn_bwd_reduce", fl, by, s);
+  Scope scope(ctx, o0.t == OP_PW ? "gemm" : o0.t == OP_DW ? "dw_bwd" : "bn_bwd_reduce", fl, by, s,
+              prof_detail() ? " group" + op_tag(P, o0, true) : std::string());
   switch (o0.t) {
     case OP_DW: {
       DwSeg segs[kMaxSeg];
@@ -982,7 +1007,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     const bool sink_on = !frozen && i + 1 < P.ops.size() && E.fused_bn[i + 1];
     const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0} : StatSink{};
     if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
-    Scope scope(ctx, kind, fl, by, s);
+    Scope scope(ctx, kind, fl, by, s, prof_detail() ? op_tag(P, op, false) : std::string());
     int np = 0;
     switch (op.t) {
       case OP_STEM:
@@ -1137,7 +1162,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       gsk_in = op.in[0] == bn.out ? 0 : 1;
     }
     if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
-    Scope scope(ctx, kind, fl, by, s);
+    Scope scope(ctx, kind, fl, by, s, prof_detail() ? op_tag(P, op, true) : std::string());
     int np = -1;
     switch (op.t) {
       case OP_STEM: {
