@@ -89,6 +89,8 @@ struct Exec {
   float *scores = nullptr, *boxes = nullptr;
   int* classes = nullptr;
   uint8_t* keep = nullptr;
+  int* cand_list = nullptr;   // soft-NMS candidates appended by pre_nms [B][A] + counts [B]
+  int* cand_count = nullptr;
   float* nms_ws = nullptr;
   int* nms_wi = nullptr;
   float *nms1_boxes = nullptr, *nms1_scores = nullptr;
@@ -581,6 +583,9 @@ Exec& phx_ctx::exec_for(int B) {
   E.classes = E.alloc<int>(BA);
   E.boxes = E.alloc<float>(BA * 4);
   E.keep = E.alloc<uint8_t>(BA);
+  E.cand_list = E.alloc<int>(BA);
+  E.cand_count = E.alloc<int>(B);
+  PHX_HIP(hipMemset(E.cand_count, 0, (size_t)B * sizeof(int)));
   E.nms_ws = E.alloc<float>(BA);
   E.nms_wi = E.alloc<int>(BA * 2);
   E.nms1_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
@@ -1255,7 +1260,10 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
   }
 }
 
-void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
+// cand_mask: the keep bits whose anchors (above the NMS threshold) pre_nms appends to the
+// soft-NMS candidate list (2: the first pass's person/valid/>=thresh, 1: the second pass's
+// person/valid for the ASR metric, 0: no list); the run_nms that follows consumes it
+void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0) {
   const Program& P = E.prog;
   Scope scope(ctx, "pre_nms", 0.0,
               (double)E.B * ctx->A * (ctx->mc.num_classes + 4 + 4 + 6) * 4.0, s);
@@ -1263,14 +1271,16 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s) {
   launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
                  ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->filter_thresh,
-                 E.scores, E.classes, E.boxes, E.keep, E.ntiles, s);
+                 E.scores, E.classes, E.boxes, E.keep, E.ntiles, s,
+                 cand_mask ? NmsCand{E.cand_list, E.cand_count, cand_mask, ctx->nms_thresh} : NmsCand{});
 }
 
 // postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25
 void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s) {
   Scope scope(ctx, "soft_nms", 0.0, (double)E.B * ctx->A * 5.0, s);
   launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->nms_thresh,
-                  0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s);
+                  0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s,
+                  NmsCand{E.cand_list, E.cand_count, keep_mask, ctx->nms_thresh});
 }
 
 // run `fn(side)` on the executor's side stream after the work enqueued on `s` so far; join_side
@@ -1471,7 +1481,7 @@ int phx_first_pass(phx_ctx* ctx, const float* images, int B, float* ob, float* o
   hipStream_t s = (hipStream_t)stream;
   Exec& E = ctx->exec_for(B);
   run_forward(ctx, E, images, s, 0, 0, 0);
-  run_pre_nms(ctx, E, s);
+  run_pre_nms(ctx, E, s, 2);
   run_nms(ctx, E, 2, ob, os, oc, s);
   return PHX_OK;
   PHX_CATCH(ctx)
@@ -1623,7 +1633,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
   // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
   run_forward(ctx, E, images, s, 0, step, gimg0);
-  run_pre_nms(ctx, E, s);
+  run_pre_nms(ctx, E, s, 2);
   // (a second HIP stream for the NMS passes that only feed the ASR metric was measured: any
   // multi-stream use slows the whole step by ~0.8 ms on this runtime, so everything stays on `s`)
   run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
@@ -1639,7 +1649,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_count(E.ed, E.place, metrics, s);
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);
-  run_pre_nms(ctx, E, s);
+  run_pre_nms(ctx, E, s, 1);
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, grad + PHX_NPATCH, metrics, s);
   // 4. victim data-gradient -> d(patched images)
@@ -1671,7 +1681,7 @@ int phx_eval_step(phx_ctx* ctx, const float* images, int B, const float* boxes, 
   ctx->last = &E;
   PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
   run_forward(ctx, E, images, s, 0, step, gimg0, false);
-  run_pre_nms(ctx, E, s);
+  run_pre_nms(ctx, E, s, 2);
   run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
   launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
   const bool inject = boxes != nullptr;
@@ -1683,7 +1693,7 @@ int phx_eval_step(phx_ctx* ctx, const float* images, int B, const float* boxes, 
               params, step, gimg0, s);
   launch_eot_count(E.ed, E.place, metrics, s);
   run_forward(ctx, E, E.patched, s, 1, step, gimg0, false);
-  run_pre_nms(ctx, E, s);
+  run_pre_nms(ctx, E, s, 1);
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, E.dscale_scratch, metrics, s);
   run_nms(ctx, E, 1, E.nms2_boxes, E.nms2_scores, E.nms2_count, s);

@@ -207,17 +207,27 @@ struct LevelDesc {
   int tile0;      // first pre_nms tile of this level
 };
 int pre_nms_tiles(int h, int w, int na);
+// soft-NMS candidates appended by pre_nms: list [B][A] anchor indices, count [B] (zero on entry,
+// reset to zero by the k_soft_nms that consumes them); mask selects keep bits (2: first pass,
+// 1: second pass), thresh = the NMS score threshold.  list == nullptr: no list.
+struct NmsCand {
+  int* list = nullptr;
+  int* count = nullptr;
+  int mask = 0;
+  float thresh = 0.f;
+};
 // pre_nms (postprocess.py:119-156) + person/validity filter (attacker.py:69-89, 105-113)
 // outputs per anchor: score, class, box; keep flag (bit0 = person&valid, bit1 = >= thresh)
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
-                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s);
+                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand = NmsCand{});
 // soft-NMS (NonMaxSuppressionV5, gaussian) per image over candidates selected by keep&mask
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,
                      int max_out, float clip_hi, float* out_boxes, float* out_scores,
-                     int* out_count, float* work_score, int* work_sb, hipStream_t s);
+                     int* out_count, float* work_score, int* work_sb, hipStream_t s,
+                     NmsCand cand = NmsCand{});
 // per-image m_b = max(max_{keep} score, 0), tie count, and loss-gradient coefficient
 void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m,
                       int* argmax, int* nties, int* scratch, hipStream_t s);

@@ -64,10 +64,16 @@ struct Gemm2Group {
 // BF: bf16 matrix cores (v_mfma_f32_32x32x16_bf16, fp32 accumulation) — the A view is applied in
 // fp32 and rounded to bf16 when the chunk is written to LDS, B (the weights) likewise; K advances in
 // 32-deep chunks (two MFMAs per tile pair).  fp32 (BF = 0): v_mfma_f32_32x32x2_f32, 16-deep chunks.
+#ifndef PHX_GEMM_BK_F32
+#define PHX_GEMM_BK_F32 16
+#endif
+#ifndef PHX_GEMM_BK_BF16
+#define PHX_GEMM_BK_BF16 32
+#endif
 template <int WM, int TM, int TN, int MODE, bool BF = false>
 struct G2 {
   static constexpr int WN = 4 / WM;
-  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = BF ? 32 : 16;
+  static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = BF ? PHX_GEMM_BK_BF16 : PHX_GEMM_BK_F32;
   static constexpr int LD = BF ? BK + 8 : BK + 4;    // LDS row pitch in elements (16-B aligned rows)
   static constexpr int KQ = BK / 4;                   // float4 per tile row per chunk
   static constexpr int RPP = 256 / KQ;                // tile rows loaded per pass of the 256 lanes
@@ -452,7 +458,7 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
   }();
   if (tiles < split_below && K >= 256)
     p.splits = std::max(1, std::min<int>((int)((2 * split_below + tiles - 1) / tiles), K / 128));
-  const int bk = bf16 ? 32 : 16;  // K chunk of the kernel variant
+  const int bk = bf16 ? PHX_GEMM_BK_BF16 : PHX_GEMM_BK_F32;  // K chunk of the kernel variant
   p.kslice = ((K + p.splits - 1) / p.splits + bk - 1) / bk * bk;
   p.splits = (K + p.kslice - 1) / p.kslice;
   const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));

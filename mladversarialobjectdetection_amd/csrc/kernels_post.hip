@@ -18,6 +18,35 @@ namespace phx {
 __device__ __forceinline__ float sigmoid_exact(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------------------------------
+// soft-NMS candidate lists, appended by pre_nms: every (image, anchor) with keep & mask and a
+// score above the NMS threshold (NonMaxSuppressionV5 drops the rest up front).  A workgroup counts
+// its tile's candidates, reserves a range of the image's list with one atomic, and writes the anchor
+// indices in anchor order; ranges of different tiles land in any order, so k_soft_nms breaks score
+// ties by anchor index (the order of the reference's ragged candidate list), which makes its
+// result independent of the list order.  k_soft_nms resets the count after reading it.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void nms_cand_append(const NmsCand& c, int b, int A, bool want, int a) {
+  __shared__ int wcount[4], wbase[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long bal = __ballot(want);
+  if (lane == 0) wcount[wave] = __popcll(bal);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    const int base = tot ? atomicAdd(c.count + b, tot) : 0;
+    wbase[0] = base;
+    wbase[1] = base + wcount[0];
+    wbase[2] = wbase[1] + wcount[1];
+    wbase[3] = wbase[2] + wcount[2];
+  }
+  __syncthreads();
+  if (want) {
+    const int pos = wbase[wave] + __popcll(bal & ((1ull << lane) - 1ull));
+    c.list[(long)b * A + pos] = a;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // pre_nms + masks.  A workgroup owns a tile of 128 consecutive anchors of one (image, level):
 // their 128 x 90 logits are one contiguous 46 KB run, staged into LDS with float4 loads, then
 // lane t reduces anchor t's 90 classes (max, first argmax) and decodes its box.
@@ -32,7 +61,7 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
                                                  float thresh, float* __restrict__ scores,
                                                  int* __restrict__ classes,
                                                  float* __restrict__ boxes,
-                                                 uint8_t* __restrict__ keep) {
+                                                 uint8_t* __restrict__ keep, NmsCand cand) {
   extern __shared__ float4 smem4[];
   float* lg_s = reinterpret_cast<float*>(smem4);
   const int b = blockIdx.y;
@@ -88,10 +117,18 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     ha_[t] = am;
   }
   __syncthreads();
-  if (half == 1 || t >= n) return;
-  if (c0 + hc < nclass && hm[t] > m) {
+  if (half == 1) {
+    if (cand.list) nms_cand_append(cand, b, A, false, 0);  // the tile's candidate append (collective)
+    return;
+  }
+  const bool live = t < n;
+  if (live && c0 + hc < nclass && hm[t] > m) {
     m = hm[t];
     am = ha_[t];
+  }
+  if (!live) {
+    if (cand.list) nms_cand_append(cand, b, A, false, 0);
+    return;
   }
   const int a = L.anchor0 + a0 + t;
   const long idx = (long)b * A + a;
@@ -120,15 +157,16 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     if (sc >= thresh) kf |= 2;
   }
   keep[idx] = kf;
+  if (cand.list) nms_cand_append(cand, b, A, (kf & cand.mask) != 0 && sc > cand.thresh, a);
 }
 
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
-                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s) {
+                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand) {
   size_t shm = (size_t)kPreTile * nclass * sizeof(float);
   hipLaunchKernelGGL(k_pre_nms, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,
-                     anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes, keep);
+                     anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes, keep, cand);
   PHX_LAUNCH_CHECK();
 }
 
@@ -161,7 +199,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     const uint8_t* __restrict__ keep, int keep_mask, const int* __restrict__ count, int N,
     float score_thresh, float scale, int max_out, float clip_hi, float* __restrict__ out_boxes,
     float* __restrict__ out_scores, int* __restrict__ out_count, float* __restrict__ wscore,
-    int* __restrict__ wsb, int* __restrict__ widx) {
+    int* __restrict__ wsb, int* __restrict__ widx, NmsCand cand) {
   const int b = blockIdx.x;
   const int t = threadIdx.x;
   const float* bb = boxes + (long)b * N * 4;
@@ -178,6 +216,20 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   __shared__ int red_i[kNmsThreads];
   __shared__ int s_done;
 
+  if (cand.list) {
+    // 1'. candidates appended by pre_nms (score > thresh and keep & mask already applied)
+    if (t == 0) s_n = cand.count[b];
+    __syncthreads();
+    const int* lst = cand.list + (long)b * N;
+    for (int i = t; i < s_n; i += kNmsThreads) {
+      const int a = lst[i];
+      wi[i] = a;
+      ws[i] = sb[a];
+      wb[i] = 0;
+    }
+    __syncthreads();
+    if (t == 0) cand.count[b] = 0;  // consumed: the next pre_nms appends from 0
+  } else {
   // 1. ordered compaction of candidates with score > thresh (and mask): every lane owns a
   //    contiguous segment, one workgroup scan of the segment counts places them
   auto ok_at = [&](int i) -> bool {
@@ -210,6 +262,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   }
   if (t == kNmsThreads - 1) s_n = red_i[t];
   __syncthreads();
+  }
   const int n = s_n;
   if (t == 0) { s_nsel = 0; s_done = 0; }
   __syncthreads();
@@ -219,15 +272,17 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   //    rescans.  The decay factors of the selections since the candidate's last visit are computed
   //    by one wave in parallel, then applied newest-first in order by one lane (same product, same
   //    early exit as the sequential rule).
-  auto better = [](float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); };
+  // order: score desc, then anchor index asc (the reference's candidate order); myi = position
+  auto better = [](float v, int a, float bv, int ba) { return v > bv || (v == bv && a < ba); };
   float myv = -INFINITY;
-  int myi = 0x7fffffff;
+  int myi = 0x7fffffff, mya = 0x7fffffff;
   for (int i = t; i < n; i += kNmsThreads) {
     const float v = ws[i];
-    if (better(v, i, myv, myi)) { myv = v; myi = i; }
+    const int a = wi[i];
+    if (better(v, a, myv, mya)) { myv = v; myi = i; mya = a; }
   }
   __shared__ float wv_s[kNmsThreads / 64];
-  __shared__ int wv_i[kNmsThreads / 64];
+  __shared__ int wv_i[kNmsThreads / 64], wv_a[kNmsThreads / 64];
   __shared__ float fac[PHX_MAX_OUT_DEV];
   __shared__ int s_c, s_from;
   __shared__ float s_orig;
@@ -235,19 +290,20 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   while (true) {
     if (s_nsel >= max_out) break;
     float v = myv;
-    int i = myi;
+    int i = myi, a = mya;
     for (int o = 32; o > 0; o >>= 1) {
       const float v2 = __shfl_xor(v, o);
       const int i2 = __shfl_xor(i, o);
-      if (better(v2, i2, v, i)) { v = v2; i = i2; }
+      const int a2 = __shfl_xor(a, o);
+      if (better(v2, a2, v, a)) { v = v2; i = i2; a = a2; }
     }
-    if (lane == 0) { wv_s[wave] = v; wv_i[wave] = i; }
+    if (lane == 0) { wv_s[wave] = v; wv_i[wave] = i; wv_a[wave] = a; }
     __syncthreads();
     if (t == 0) {
       float bv = wv_s[0];
-      int bi = wv_i[0];
+      int bi = wv_i[0], ba = wv_a[0];
       for (int w = 1; w < kNmsThreads / 64; ++w)
-        if (better(wv_s[w], wv_i[w], bv, bi)) { bv = wv_s[w]; bi = wv_i[w]; }
+        if (better(wv_s[w], wv_a[w], bv, ba)) { bv = wv_s[w]; bi = wv_i[w]; ba = wv_a[w]; }
       if (!(bv > score_thresh) || bi == 0x7fffffff) {
         s_done = 1;
       } else {
@@ -289,10 +345,11 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     __syncthreads();
     if (t == c % kNmsThreads) {
       myv = -INFINITY;
-      myi = 0x7fffffff;
+      myi = mya = 0x7fffffff;
       for (int k = t; k < n; k += kNmsThreads) {
         const float vv = ws[k];
-        if (better(vv, k, myv, myi)) { myv = vv; myi = k; }
+        const int ak = wi[k];
+        if (better(vv, ak, myv, mya)) { myv = vv; myi = k; mya = ak; }
       }
     }
   }
@@ -316,14 +373,14 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,
                      int max_out, float clip_hi, float* out_boxes, float* out_scores,
-                     int* out_count, float* work_score, int* work_sb, hipStream_t s) {
+                     int* out_count, float* work_score, int* work_sb, hipStream_t s, NmsCand cand) {
   if (max_out > PHX_MAX_OUT_DEV) throw std::runtime_error("soft_nms: max_out too large");
   // TF: scale = -0.5 / soft_nms_sigma (soft_nms_sigma = sigma / 2, postprocess.py:191-200)
   float scale = soft_sigma > 0.f ? -0.5f / soft_sigma : 0.f;
   int* widx = work_sb + (long)B * N;
   hipLaunchKernelGGL(k_soft_nms, dim3(B), dim3(kNmsThreads), 0, s, boxes, scores, keep, keep_mask,
                      count, N, score_thresh, scale, max_out, clip_hi, out_boxes, out_scores,
-                     out_count, work_score, work_sb, widx);
+                     out_count, work_score, work_sb, widx, cand);
   PHX_LAUNCH_CHECK();
 }
 
