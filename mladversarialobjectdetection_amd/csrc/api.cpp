@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <memory>
 #include <sstream>
@@ -366,12 +367,27 @@ std::string op_tag(const Program& P, const Op& op, bool bwd) {
   return b;
 }
 
+// PHX_DEBUG_SYNC=1: synchronise and check for a device error after every launch group, naming it
+// in the exception (fault localisation; never on the timed path)
+bool debug_sync() {
+  static const bool on = [] {
+    const char* e = std::getenv("PHX_DEBUG_SYNC");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 struct Scope {
   Prof* p;
   size_t idx;
   hipStream_t s;
+  std::string dbg;
   Scope(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t st, const std::string& tag = "")
       : p(ctx->prof.on ? &ctx->prof : nullptr), s(st) {
+    if (debug_sync()) {
+      dbg = std::string(kind) + tag;
+      PHX_HIP(hipStreamSynchronize(s));
+    }
     if (!p) return;
     // GEMMs of a bf16 context run on the bf16 matrix cores; everything else at the fp32 rate
     const double peak = (ctx->bf16 && std::string(kind) == "gemm") ? 2500.0 : 157.3;
@@ -380,8 +396,12 @@ struct Scope {
     p->recs.push_back(r);
     idx = p->recs.size() - 1;
   }
-  ~Scope() {
+  ~Scope() noexcept(false) {
     if (p) (void)hipEventRecord(p->recs[idx].b, s);
+    if (!dbg.empty() && std::uncaught_exceptions() == 0) {
+      const hipError_t e = hipStreamSynchronize(s);
+      if (e != hipSuccess) throw HipError(std::string("device error after ") + dbg + ": " + hipGetErrorString(e));
+    }
   }
 };
 
@@ -1012,7 +1032,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     const bool sink_on = !frozen && i + 1 < P.ops.size() && E.fused_bn[i + 1];
     const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0} : StatSink{};
     if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
-    Scope scope(ctx, kind, fl, by, s, prof_detail() ? op_tag(P, op, false) : std::string());
+    Scope scope(ctx, kind, fl, by, s, (prof_detail() || debug_sync()) ? op_tag(P, op, false) : std::string());
     int np = 0;
     switch (op.t) {
       case OP_STEM:
@@ -1167,7 +1187,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       gsk_in = op.in[0] == bn.out ? 0 : 1;
     }
     if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
-    Scope scope(ctx, kind, fl, by, s, prof_detail() ? op_tag(P, op, true) : std::string());
+    Scope scope(ctx, kind, fl, by, s, (prof_detail() || debug_sync()) ? op_tag(P, op, true) : std::string());
     int np = -1;
     switch (op.t) {
       case OP_STEM: {

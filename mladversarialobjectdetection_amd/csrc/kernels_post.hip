@@ -42,7 +42,7 @@ __device__ __forceinline__ void nms_cand_append(const NmsCand& c, int b, int A, 
   __syncthreads();
   if (want) {
     const int pos = wbase[wave] + __popcll(bal & ((1ull << lane) - 1ull));
-    c.list[(long)b * A + pos] = a;
+    if (pos < A) c.list[(long)b * A + pos] = a;  // a list never holds more than the image's anchors
   }
 }
 
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
 
   if (cand.list) {
     // 1'. candidates appended by pre_nms (score > thresh and keep & mask already applied)
-    if (t == 0) s_n = cand.count[b];
+    if (t == 0) s_n = min(cand.count[b], N);
     __syncthreads();
     const int* lst = cand.list + (long)b * N;
     for (int i = t; i < s_n; i += kNmsThreads) {
