@@ -117,20 +117,16 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     ha_[t] = am;
   }
   __syncthreads();
-  if (half == 1) {
-    if (cand.list) nms_cand_append(cand, b, A, false, 0);  // the tile's candidate append (collective)
-    return;
-  }
-  const bool live = t < n;
-  if (live && c0 + hc < nclass && hm[t] > m) {
+  // the candidate append below is a workgroup collective (ballots + barriers): every thread reaches
+  // it exactly once, at the same program point, so nothing returns early
+  const bool live = half == 0 && t < n;
+  bool want = false;
+  const int a = L.anchor0 + a0 + t;
+  if (live) {
+  if (c0 + hc < nclass && hm[t] > m) {
     m = hm[t];
     am = ha_[t];
   }
-  if (!live) {
-    if (cand.list) nms_cand_append(cand, b, A, false, 0);
-    return;
-  }
-  const int a = L.anchor0 + a0 + t;
   const long idx = (long)b * A + a;
   const float4 bx = *reinterpret_cast<const float4*>(box_base + L.box_off + ((long)b * nloc + a0 + t) * 4);
   const float4 an = *reinterpret_cast<const float4*>(anchors + (long)a * 4);
@@ -157,7 +153,9 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     if (sc >= thresh) kf |= 2;
   }
   keep[idx] = kf;
-  if (cand.list) nms_cand_append(cand, b, A, (kf & cand.mask) != 0 && sc > cand.thresh, a);
+  want = (kf & cand.mask) != 0 && sc > cand.thresh;
+  }
+  if (cand.list) nms_cand_append(cand, b, A, want, a);
 }
 
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
