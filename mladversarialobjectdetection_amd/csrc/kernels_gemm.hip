@@ -94,6 +94,11 @@ struct G2Regs {
   GChan4 gk;
 };
 
+// Branch-free: out-of-range rows / columns / k quads load from a clamped (valid) address and are
+// zeroed when g2_store writes the chunk to LDS (a select here would wait for each load at once).
+// A load under an exec-mask branch makes hipcc's wait counting conservative (vmcnt(0) right
+// after the first conditional load), which exposed a full HBM round trip per K step before the
+// MFMAs of the staged chunk could issue.
 template <int WM, int TM, int TN, int MODE, bool BF>
 __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, int m0, int n0,
                                         int k0, int kend) {
@@ -102,25 +107,20 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const G
   const int c4 = t % P::KQ;
   const int kk = k0 + 4 * c4;
   const bool kok = kk < kend;
-  if (MODE == 1 || MODE == 2) {
-    if (kok) r.ck = inx_chan4(a.A, kk);
-  }
-  if (MODE == 3) {
-    if (kok) r.gk = gx_chan4(a.G, kk);
-  }
+  const int kc = kok ? kk : kend - 4;  // kend >= 4, K % 4 == 0
+  if (MODE == 1 || MODE == 2) r.ck = inx_chan4(a.A, kc);
+  if (MODE == 3) r.gk = gx_chan4(a.G, kc);
 #pragma unroll
   for (int u = 0; u < P::NA; ++u) {
     const int row = m0 + (t + 256 * u) / P::KQ;
-    const bool ok = kok && row < a.M && t + 256 * u < P::BM * P::KQ;
-    const long e = (long)row * a.K + kk;
+    const long e = (long)min(row, a.M - 1) * a.K + kc;
     if (MODE == 3) {
-      r.a[u] = ok ? *reinterpret_cast<const float4*>(a.G.da + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-      r.y[u] = ok ? *reinterpret_cast<const float4*>(a.G.y + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
+      r.y[u] = *reinterpret_cast<const float4*>(a.G.y + e);
     } else {
-      r.a[u] = ok ? *reinterpret_cast<const float4*>(a.A.p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      r.a[u] = *reinterpret_cast<const float4*>(a.A.p + e);
       if (MODE == 2)
-        r.rs[u] = ok ? *reinterpret_cast<const float4*>(a.rowscale + (long)(row / a.rpi) * a.K + kk)
-                     : make_float4(0.f, 0.f, 0.f, 0.f);
+        r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(min(row, a.M - 1) / a.rpi) * a.K + kc);
     }
   }
 #pragma unroll
@@ -128,8 +128,7 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const G
     const int idx = t + 256 * u;
     const int col = n0 + idx / P::KQ;
     const int kb = k0 + 4 * (idx % P::KQ);
-    const bool ok = idx < P::BN * P::KQ && col < a.N && kb < kend;
-    r.b[u] = ok ? *reinterpret_cast<const float4*>(a.Bt + (long)col * a.K + kb) : make_float4(0.f, 0.f, 0.f, 0.f);
+    r.b[u] = *reinterpret_cast<const float4*>(a.Bt + (long)min(col, a.N - 1) * a.K + (kb < kend ? kb : kend - 4));
   }
 }
 
@@ -147,24 +146,30 @@ __device__ __forceinline__ void g2_put4(float* sm, int buf, bool b, int row, int
   else *reinterpret_cast<float4*>(g2_tile<P>(sm, buf, b, row, k)) = v;
 }
 
-template <int WM, int TM, int TN, int MODE, bool BF>
-__device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, float* sm,
-                                         int buf, int m0, int k0, int kend) {
+// The activation of the A view is a compile-time constant inside the store pass (one dispatch per
+// chunk instead of a branch tree per element).
+template <int WM, int TM, int TN, int MODE, bool BF, int ACT>
+__device__ __forceinline__ void g2_store_act(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a,
+                                             float* sm, int buf, int m0, int n0, int k0, int kend) {
   using P = G2<WM, TM, TN, MODE, BF>;
   const int t = threadIdx.x;
   const int c4 = t % P::KQ;
   const bool kok = k0 + 4 * c4 < kend;
+  InX ax = a.A;
+  ax.act = ACT;
+  GradX gx = a.G;
+  gx.act = ACT;
 #pragma unroll
   for (int u = 0; u < P::NA; ++u) {
     if (t + 256 * u >= P::BM * P::KQ) continue;
     const int rl = (t + 256 * u) / P::KQ;
     float4 v = r.a[u];
     if (kok && m0 + rl < a.M) {
-      if (MODE == 1 || MODE == 2) v = inx_apply4(a.A, r.ck, v);
+      if (MODE == 1 || MODE == 2) v = inx_apply4(ax, r.ck, v);
       if (MODE == 2) {
         v.x *= r.rs[u].x; v.y *= r.rs[u].y; v.z *= r.rs[u].z; v.w *= r.rs[u].w;
       }
-      if (MODE == 3) v = gx_apply4(a.G, r.gk, v, r.y[u]);
+      if (MODE == 3) v = gx_apply4(gx, r.gk, v, r.y[u]);
     } else {
       v = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -173,8 +178,20 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, 
 #pragma unroll
   for (int u = 0; u < P::NB; ++u) {
     const int idx = t + 256 * u;
-    if (idx < P::BN * P::KQ) g2_put4<P>(sm, buf, true, idx / P::KQ, 4 * (idx % P::KQ), r.b[u]);
+    if (idx < P::BN * P::KQ) {
+      const bool ok = n0 + idx / P::KQ < a.N && k0 + 4 * (idx % P::KQ) < kend;
+      g2_put4<P>(sm, buf, true, idx / P::KQ, 4 * (idx % P::KQ), ok ? r.b[u] : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
   }
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, float* sm,
+                                         int buf, int m0, int n0, int k0, int kend) {
+  const int act = MODE == 0 ? 0 : MODE == 3 ? a.G.act : a.A.act;
+  if (act == 1) g2_store_act<WM, TM, TN, MODE, BF, 1>(r, a, sm, buf, m0, n0, k0, kend);
+  else if (act == 2) g2_store_act<WM, TM, TN, MODE, BF, 2>(r, a, sm, buf, m0, n0, k0, kend);
+  else g2_store_act<WM, TM, TN, MODE, BF, 0>(r, a, sm, buf, m0, n0, k0, kend);
 }
 
 // SK: 0 plain, 1 StatSink (BN statistics of C), 2 GradSink (BN-backward sums of a dgrad's C)
@@ -206,11 +223,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) smean[j] = sm2[j] = 0.f;
 
+  // bias of this workgroup's columns, read once (a load in the epilogue would wait behind the
+  // prefetch of the next chunk: the wait counter is in order)
+  float bias[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    bias[j] = (!split && a.bias) ? a.bias[min(n0 + wn * TN * 32 + j * 32 + r32, a.N - 1)] : 0.f;
+
   int tile = blockIdx.x;
   if (tile < a.mtiles && ksteps > 0) {
     G2Regs<WM, TM, TN, MODE, BF> rg;
     g2_load<WM, TM, TN, MODE, BF>(rg, a, tile * BM, n0, kbeg, kend);
-    g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, 0, tile * BM, kbeg, kend);
+    g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, 0, tile * BM, n0, kbeg, kend);
     __syncthreads();
     int buf = 0, kc = 0;
     floatx16 acc[TM][TN];
@@ -228,7 +252,10 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
         nkc = 0;
       }
       const bool have_next = ntile < a.mtiles;
-      if (have_next) g2_load<WM, TM, TN, MODE, BF>(rg, a, ntile * BM, n0, kbeg + nkc * BK, kend);
+      // (issued unconditionally — the last step re-loads its own chunk — so no branch joins the
+      // loads and the MFMAs below do not wait for them)
+      g2_load<WM, TM, TN, MODE, BF>(rg, a, (have_next ? ntile : tile) * BM, n0, kbeg + (have_next ? nkc : kc) * BK, kend);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs
       // MFMAs on the staged chunk
       if constexpr (BF) {
         // lane (r32, h) feeds row / column r32 with k = 16*kk + 8*h .. +7 (one ds_read_b128 each)
@@ -273,26 +300,51 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       }
       if (kc == ksteps - 1) {
         // ---- epilogue of `tile` ----
+        // In the 32x32 C/D layout lane (r32, h) holds column r32, rows (e&3) + 8*(e>>2) + 4*h.
+        // A wave whose 32*TM x 32*TN block lies inside C (`full`, wave-uniform) runs without
+        // per-element bounds checks, and an accumulating store reads its 16 old values per tile
+        // before adding (a per-element conditional load waits vmcnt(0) each time).
         const int mrow0 = tile * BM + wm * TM * 32;
+        const int ncol0 = n0 + wn * TN * 32;
+        const bool full = mrow0 + TM * 32 <= a.M && ncol0 + TN * 32 <= a.N;
+        const bool accum = !split && a.acc;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const int col = n0 + wn * TN * 32 + j * 32 + r32;
+          const int col = ncol0 + j * 32 + r32;
           const bool cok = col < a.N;
-          const float bv = (!split && a.bias && cok) ? a.bias[col] : 0.f;
+          const float bv = bias[j];
 #pragma unroll
-          for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i) {
+            float* cbase = out + (long)(mrow0 + i * 32 + 4 * h) * a.N + col;
+            if (full) {
+              float old[16];
+              if (accum) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-              const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-              float v = acc[i][j][e] + bv;
-              acc[i][j][e] = v;
-              if (cok && row < a.M) {
-                float* cp = out + (long)row * a.N + col;
-                if (!split && a.acc) v += *cp;
-                *cp = v;
+                for (int e = 0; e < 16; ++e) old[e] = cbase[(long)((e & 3) + 8 * (e >> 2)) * a.N];
+              }
+#pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                float v = acc[i][j][e] + bv;
+                acc[i][j][e] = v;
+                if (accum) v += old[e];
+                cbase[(long)((e & 3) + 8 * (e >> 2)) * a.N] = v;
                 if (SK == 2) acc[i][j][e] = v;
               }
+            } else {
+#pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                float v = acc[i][j][e] + bv;
+                acc[i][j][e] = v;
+                if (cok && row < a.M) {
+                  float* cp = out + (long)row * a.N + col;
+                  if (accum) v += *cp;
+                  *cp = v;
+                  if (SK == 2) acc[i][j][e] = v;
+                }
+              }
             }
+          }
         }
         if constexpr (STATS) {
           // per-wave column statistics over its TM*32 rows, then merged across the WM waves
@@ -346,16 +398,24 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
           for (int j = 0; j < TN; ++j) {
             const int col = n0 + wn * TN * 32 + j * 32 + r32;
             float s1 = 0.f, s2 = 0.f;
-            if (col < a.N) {
-              const float mu = a.gsk.mu[col], rs = a.gsk.rstd[col], sc = a.gsk.sc[col], be = a.gsk.be[col];
+            {
+              // BN input y at the tile's elements, loaded unconditionally from clamped addresses
+              const int cc = min(col, a.N - 1);
+              const float mu = a.gsk.mu[cc], rs = a.gsk.rstd[cc], sc = a.gsk.sc[cc], be = a.gsk.be[cc];
 #pragma unroll
-              for (int i = 0; i < TM; ++i)
+              for (int i = 0; i < TM; ++i) {
+                float yv[16];
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                  const int row = min(mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h, a.M - 1);
+                  yv[e] = a.gsk.y[(long)row * a.N + cc];
+                }
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                   const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                  if (row < a.M)
-                    gs_one(acc[i][j][e], a.gsk.y[(long)row * a.N + col], mu, rs, sc, be, a.gsk.act, s1, s2);
+                  if (col < a.N && row < a.M) gs_one(acc[i][j][e], yv[e], mu, rs, sc, be, a.gsk.act, s1, s2);
                 }
+              }
             }
             s1 += __shfl_xor(s1, 32);
             s2 += __shfl_xor(s2, 32);
@@ -381,7 +441,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
       }
       if (!have_next) break;
-      g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, buf ^ 1, ntile * BM, kbeg + nkc * BK, kend);
+      g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, buf ^ 1, ntile * BM, n0, kbeg + nkc * BK, kend);
       __syncthreads();
       buf ^= 1;
       tile = ntile;
