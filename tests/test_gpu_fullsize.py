@@ -59,7 +59,9 @@ def _step_vs_oracle(B):
     check_metric_row(met, ref, B)
     mt = torch.empty(B, device="cuda")
     v.ctx.call("phx_debug_last_maxscores", mt.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
-    np.testing.assert_allclose(mt.cpu().numpy(), ref["m_raw"], rtol=1e-5, atol=1e-6)
+    # per-image max scores: |d| <= 2e-5 as for the first pass's scores (fp32 through ~100 BN layers
+    # at 512^2; measured up to 2.5e-6)
+    np.testing.assert_allclose(mt.cpu().numpy(), ref["m_raw"], rtol=0, atol=2e-5)
 
 
 def test_c1_512_batch2_matches_oracle():
