@@ -42,6 +42,7 @@ struct Gemm2Plan {
   int wm, tm, tn, mtiles, gx, gy, splits, kslice;
 };
 Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false);
+void gemm2_force_cfg(int wm, int tm, int tn, int splits);  // tools/gemm_bench sweeps only (0 = off)
 int gemm_impl();
 int gemm_impl_for(int N, bool bf16 = false);
 int gemm2_target_wgs();

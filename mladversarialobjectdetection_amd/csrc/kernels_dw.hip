@@ -101,6 +101,15 @@ struct StageInX {
   __device__ __forceinline__ float4 finish(const Raw& x) const {
     return f ? inx_apply4(v, k, x) : x;
   }
+  // the view's activation as a compile-time constant (dw_stage dispatches once per launch)
+  static constexpr bool kActT = true;
+  __device__ __forceinline__ int act() const { return v.act; }
+  template <int ACT>
+  __device__ __forceinline__ float4 finish_t(const Raw& x) const {
+    InX c = v;
+    c.act = ACT;
+    return f ? inx_apply4(c, k, x) : x;
+  }
 };
 
 struct StageFuse {
@@ -137,6 +146,10 @@ struct StageFuse {
                        fuse_combine(a[0].z, a[1].z, a[2].z, f.nin, f.method, wv, den, f.act),
                        fuse_combine(a[0].w, a[1].w, a[2].w, f.nin, f.method, wv, den, f.act));
   }
+  static constexpr bool kActT = false;
+  __device__ __forceinline__ int act() const { return 0; }
+  template <int ACT>
+  __device__ __forceinline__ float4 finish_t(const Raw& r) const { return finish(r); }
 };
 
 struct StageGradX {
@@ -160,6 +173,14 @@ struct StageGradX {
   }
   __device__ __forceinline__ float4 finish(const Raw& r) const {
     return g.y ? gx_apply4(g, k, r.d, r.y) : r.d;
+  }
+  static constexpr bool kActT = true;
+  __device__ __forceinline__ int act() const { return g.y ? g.act : 0; }
+  template <int ACT>
+  __device__ __forceinline__ float4 finish_t(const Raw& r) const {
+    GradX c = g;
+    c.act = ACT;
+    return g.y ? gx_apply4(c, k, r.d, r.y) : r.d;
   }
 };
 
@@ -204,10 +225,13 @@ struct Taps {
   }
 };
 
-// stage rows [r0, r0+rin) x cols [c0, c0+cin) of the NHWC source (sh x sw) into LDS
-template <class Src, int U = 4>
-__device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, int sh, int sw, int C,
-                                         int r0, int c0, int chan, const DwGeom& g) {
+// stage rows [r0, r0+rin) x cols [c0, c0+cin) of the NHWC source (sh x sw) into LDS.
+// Loads are unconditional from clamped (valid) addresses, the padding zeros are selected when the
+// values are written, and the source view's activation is a compile-time constant of the pass (a
+// per-element switch on it was a third of the instructions of the staging loop).
+template <int ACT, class Src, int U>
+__device__ __forceinline__ void dw_stage_t(float4* tile, const Src& src, int b, int sh, int sw, int C,
+                                           int r0, int c0, int chan, const DwGeom& g) {
   const int CG = 1 << g.lcg;
   const int npx = g.rin * g.cin;
   const int pstep = 256 >> g.lcg;
@@ -222,13 +246,28 @@ __device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, in
       const int prow = pp / g.cin, pcol = pp - prow * g.cin;
       const int iy = r0 + prow, ix = c0 + pcol;
       ok[u] = pp < npx && iy >= 0 && iy < sh && ix >= 0 && ix < sw;
-      v[u] = ok[u] ? src.load((((long)b * sh + iy) * sw + ix) * C + chan) : src.zero();
+      const int iyc = min(max(iy, 0), sh - 1), ixc = min(max(ix, 0), sw - 1);
+      v[u] = src.load((((long)b * sh + iyc) * sw + ixc) * C + chan);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int pp = p + u * pstep;
-      if (pp < npx) tile[(pp << g.lcg) + ecg] = ok[u] ? src.finish(v[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (pp < npx)
+        tile[(pp << g.lcg) + ecg] = ok[u] ? src.template finish_t<ACT>(v[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+  }
+}
+
+template <class Src, int U = 4>
+__device__ __forceinline__ void dw_stage(float4* tile, const Src& src, int b, int sh, int sw, int C,
+                                         int r0, int c0, int chan, const DwGeom& g) {
+  if constexpr (Src::kActT) {
+    const int act = src.act();
+    if (act == 1) dw_stage_t<1, Src, U>(tile, src, b, sh, sw, C, r0, c0, chan, g);
+    else if (act == 2) dw_stage_t<2, Src, U>(tile, src, b, sh, sw, C, r0, c0, chan, g);
+    else dw_stage_t<0, Src, U>(tile, src, b, sh, sw, C, r0, c0, chan, g);
+  } else {
+    dw_stage_t<0, Src, U>(tile, src, b, sh, sw, C, r0, c0, chan, g);
   }
 }
 
@@ -470,6 +509,16 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
   GSChan4 kk;
   if (GS && active) kk = gs_chan4(gsk, c);
+  // the rows' old values (acc) and BN inputs (GradSink) are read before any is used, from clamped
+  // addresses (a conditional load per row waited for each one in turn)
+  float4 old[RPT], yv[RPT];
+  const int ixc = min(ix, g.W - 1);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const long e = (((long)b * g.H + min(iy0 + row0 + r, g.H - 1)) * g.W + ixc) * g.C + c;
+    if (acc_flag) old[r] = *reinterpret_cast<const float4*>(dx + e);
+    if constexpr (GS) yv[r] = *reinterpret_cast<const float4*>(gsk.y + e);
+  }
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
     const int iy = iy0 + row0 + r;
@@ -478,11 +527,10 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
     float4* o = reinterpret_cast<float4*>(dx + e);
     float4 a = acc[r];
     if (acc_flag) {
-      const float4 p = *o;
-      a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+      a.x += old[r].x; a.y += old[r].y; a.z += old[r].z; a.w += old[r].w;
     }
     *o = a;
-    if constexpr (GS) gs_acc4(gsk, kk, a, *reinterpret_cast<const float4*>(gsk.y + e), s1, s2);
+    if constexpr (GS) gs_acc4(gsk, kk, a, yv[r], s1, s2);
   }
   if constexpr (GS) dw_gsums(s1, s2, g.lcg, c, (long)b * g.ntiles + tl, gsk);
 }

@@ -195,8 +195,14 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, 
 }
 
 // SK: 0 plain, 1 StatSink (BN statistics of C), 2 GradSink (BN-backward sums of a dgrad's C)
+#ifndef PHX_GEMM_PF2
+#define PHX_GEMM_PF2 0
+#endif
 template <int WM, int TM, int TN, int MODE, int SK, int NS, bool BF>
 __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
+  // two-deep prefetch for the fp32 forward GEMMs (the dgrad's gradient view and the bf16 chunks
+  // hold twice the staging registers: one set keeps them clear of spills)
+  constexpr bool PF2 = PHX_GEMM_PF2 && !BF && MODE != 3;
   const int zper = NS == 1 ? (int)gridDim.z : (int)gridDim.z / grp.n;
   const int seg = NS == 1 ? 0 : (int)blockIdx.z / zper;
   const int zs = (int)blockIdx.z - seg * zper;
@@ -232,11 +238,27 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
 
   int tile = blockIdx.x;
   if (tile < a.mtiles && ksteps > 0) {
-    G2Regs<WM, TM, TN, MODE, BF> rg;
-    g2_load<WM, TM, TN, MODE, BF>(rg, a, tile * BM, n0, kbeg, kend);
-    g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, 0, tile * BM, n0, kbeg, kend);
-    __syncthreads();
+    // PF2: two register sets, the loads of chunk s+2 are issued while chunk s is multiplied and
+    // written to LDS at the end of step s+1 (two steps of latency cover; the HBM bytes a
+    // workgroup keeps in flight double).  PF1: one set, loads one step ahead.
+    G2Regs<WM, TM, TN, MODE, BF> rgA, rgB;
+    g2_load<WM, TM, TN, MODE, BF>(rgA, a, tile * BM, n0, kbeg, kend);
+    g2_store<WM, TM, TN, MODE, BF>(rgA, a, sm, 0, tile * BM, n0, kbeg, kend);
     int buf = 0, kc = 0;
+    // the chunk after (tile, kc): the following chunk of this tile, or the first of the next
+    auto advance = [&](int t, int k, int& tn, int& kn) {
+      tn = t;
+      kn = k + 1;
+      if (kn == ksteps) {
+        tn = t + gridDim.x;
+        kn = 0;
+      }
+    };
+    int t1, k1;
+    advance(tile, 0, t1, k1);
+    bool h1 = t1 < a.mtiles;
+    if constexpr (PF2) g2_load<WM, TM, TN, MODE, BF>(rgB, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : 0) * BK, kend);
+    __syncthreads();
     floatx16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -244,17 +266,19 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    while (true) {
-      // next step of the pipeline: the following chunk of this tile, or the first of the next
-      int ntile = tile, nkc = kc + 1;
-      if (nkc == ksteps) {
-        ntile = tile + gridDim.x;
-        nkc = 0;
+    // one pipeline step: L receives the loads issued now, S holds the chunk stored at its end
+    auto step = [&](G2Regs<WM, TM, TN, MODE, BF>& L, G2Regs<WM, TM, TN, MODE, BF>& S) -> bool {
+      int t2 = 0, k2 = 0;
+      bool h2 = false;
+      // (issued unconditionally — past the end a step re-loads its own chunk — so no branch joins
+      // the loads and the MFMAs below do not wait for them)
+      if constexpr (PF2) {
+        advance(t1, k1, t2, k2);
+        h2 = h1 && t2 < a.mtiles;
+        g2_load<WM, TM, TN, MODE, BF>(L, a, (h2 ? t2 : tile) * BM, n0, kbeg + (h2 ? k2 : kc) * BK, kend);
+      } else {
+        g2_load<WM, TM, TN, MODE, BF>(L, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : kc) * BK, kend);
       }
-      const bool have_next = ntile < a.mtiles;
-      // (issued unconditionally — the last step re-loads its own chunk — so no branch joins the
-      // loads and the MFMAs below do not wait for them)
-      g2_load<WM, TM, TN, MODE, BF>(rg, a, (have_next ? ntile : tile) * BM, n0, kbeg + (have_next ? nkc : kc) * BK, kend);
       __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs
       // MFMAs on the staged chunk
       if constexpr (BF) {
@@ -440,12 +464,28 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
       }
-      if (!have_next) break;
-      g2_store<WM, TM, TN, MODE, BF>(rg, a, sm, buf ^ 1, ntile * BM, n0, kbeg + nkc * BK, kend);
+      if (!h1) return false;
+      g2_store<WM, TM, TN, MODE, BF>(PF2 ? S : L, a, sm, buf ^ 1, t1 * BM, n0, kbeg + k1 * BK, kend);
       __syncthreads();
       buf ^= 1;
-      tile = ntile;
-      kc = nkc;
+      tile = t1;
+      kc = k1;
+      if constexpr (PF2) {
+        t1 = t2;
+        k1 = k2;
+        h1 = h2;
+      } else {
+        advance(tile, kc, t1, k1);
+        h1 = t1 < a.mtiles;
+      }
+      return true;
+    };
+    if constexpr (PF2) {
+      while (step(rgA, rgB) && step(rgB, rgA)) {
+      }
+    } else {
+      while (step(rgA, rgA)) {
+      }
     }
   }
   if constexpr (STATS) {
@@ -485,9 +525,29 @@ static G2Cfg g2_pick(int N) {
   return {2, 2, 2};
 }
 
+// configuration forced by tools/gemm_bench sweeps (never set by the product)
+static int g_force[4] = {0, 0, 0, 0};
+void gemm2_force_cfg(int wm, int tm, int tn, int splits) {
+  g_force[0] = wm; g_force[1] = tm; g_force[2] = tn; g_force[3] = splits;
+}
+
 Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
   Gemm2Plan p;
   G2Cfg c = g2_pick(N);
+  if (g_force[0]) {
+    p.wm = g_force[0]; p.tm = g_force[1]; p.tn = g_force[2];
+    c = G2Cfg{p.wm, p.tm, p.tn};
+    p.mtiles = cdiv(M, c.bm());
+    p.gy = cdiv(N, c.bn());
+    const int bk = bf16 ? PHX_GEMM_BK_BF16 : PHX_GEMM_BK_F32;
+    p.splits = std::max(1, g_force[3]);
+    p.kslice = ((K + p.splits - 1) / p.splits + bk - 1) / bk * bk;
+    p.splits = (K + p.kslice - 1) / p.kslice;
+    const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
+    p.gx = (int)std::min<long>(p.mtiles, want);
+    if (p.gy > 1 && p.gx > 8) p.gx = p.gx / 8 * 8;
+    return p;
+  }
   // few 128x128 tiles (small M, wide N, no split-K): 64-row tiles double the workgroups so
   // every CU gets MFMA work
   static const bool half_rows = [] {

@@ -34,13 +34,25 @@ int main(int argc, char** argv) {
       {262144, 144, 24, false, true},  {262144, 24, 144, false, true},  {65536, 810, 64, true, false},
       {65536, 64, 64, true, true},     {16384, 672, 112, false, true},  {16384, 112, 672, false, true},
       {4096, 1152, 192, false, true},  {4096, 192, 1152, false, true},  {16384, 64, 64, true, true},
-      {4096, 64, 64, true, true},      {4096, 320, 1152, false, true}};
+      {4096, 64, 64, true, true},      {4096, 320, 1152, false, true},
+      // large, square-ish: the kernel's MFMA ceiling without shape effects
+      {65536, 512, 512, false, false}, {65536, 512, 512, false, true},  {16384, 1024, 1024, false, false}};
+  // GEMM_ONLY=i,j,...: run only those shape indices
+  if (const char* e = getenv("GEMM_ONLY")) {
+    std::vector<S> keep;
+    for (const char* q = e; *q;) {
+      keep.push_back(shapes[atoi(q)]);
+      while (*q && *q != ',') ++q;
+      if (*q) ++q;
+    }
+    shapes = keep;
+  }
   size_t maxA = 0, maxB = 0, maxC = 0, maxP = 0;
   for (auto& s : shapes) {
     maxA = std::max(maxA, (size_t)s.M * s.K);
     maxB = std::max(maxB, (size_t)s.N * s.K);
     maxC = std::max(maxC, (size_t)s.M * s.N);
-    maxP = std::max(maxP, gemm_partial_floats(s.M, s.N, s.K));
+    maxP = std::max(maxP, (size_t)8 * s.M * s.N);  // room for up to 8 split-K slabs (sweeps)
   }
   float *A, *Bt, *bias, *C, *R, *part;
   float2* sp;
@@ -66,7 +78,8 @@ int main(int argc, char** argv) {
         gemm2_run(0, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st, part, sink,
                   wgs);
     };
-    for (impl = 1; impl <= 2; ++impl) {
+    const int impl0 = getenv("GEMM_IMPL1") ? 1 : 2;
+    for (impl = impl0; impl <= 2; ++impl) {
     run();
     hipLaunchKernelGGL(k_ref, dim3(((long)s.M * s.N + 255) / 256), dim3(256), 0, st, A, Bt, s.bias ? bias : nullptr,
                        R, s.M, s.N, s.K);
@@ -102,5 +115,57 @@ int main(int argc, char** argv) {
   }
   printf("impl1 total %.1f us; impl2 total %.1f us, roofline %.1f us (%.0f%%)\n", tot1, tot_us, tot_roof,
          100 * tot_roof / tot_us);
+  // GEMM_SWEEP=1: every tile configuration x split count per shape (stats epilogue as listed)
+  if (getenv("GEMM_SWEEP")) {
+    // GEMM_MODE=1: A through a BN + swish view; 3: a BN-backward gradient view (dgrad, no stats)
+    // GEMM_BF16=1: bf16 matrix cores
+    const int mode = getenv("GEMM_MODE") ? atoi(getenv("GEMM_MODE")) : 0;
+    const bool bf = getenv("GEMM_BF16") != nullptr;
+    float *mu, *scl, *be, *ybuf, *m1, *m2;
+    hipMalloc(&mu, 4096 * 4); hipMalloc(&scl, 4096 * 4); hipMalloc(&be, 4096 * 4);
+    hipMalloc(&m1, 4096 * 4); hipMalloc(&m2, 4096 * 4);
+    hipMalloc(&ybuf, maxA * 4);
+    fill(mu, 4096, 4); fill(scl, 4096, 5); fill(be, 4096, 6); fill(m1, 4096, 7); fill(m2, 4096, 8);
+    fill(ybuf, maxA, 9);
+    printf("sweep mode %d bf16 %d\n", mode, (int)bf);
+    const int cfgs[8][3] = {{4, 1, 1}, {4, 1, 2}, {4, 1, 3}, {4, 1, 5}, {2, 2, 2}, {2, 1, 2}, {2, 1, 1}, {1, 1, 1}};
+    const int splits_opt[4] = {1, 2, 4, 8};
+    for (auto& s : shapes) {
+      InX ax{A, mode == 1 ? mu : nullptr, scl, be, mode == 1 ? 1 : 0};
+      GradX gx{A, ybuf, mu, scl, scl, be, m1, m2, 1};
+      StatSink sink = (s.stats && mode != 3) ? StatSink{sp, sc, s.N, 0} : StatSink{};
+      double best = 1e30;
+      int bc = -1, bs = 0;
+      for (int ci = 0; ci < 8; ++ci)
+        for (int si = 0; si < 4; ++si) {
+          const int sp_ = splits_opt[si];
+          if (sp_ > 1 && (s.K < 128 * sp_ || s.N > 1024)) continue;
+          gemm2_force_cfg(cfgs[ci][0], cfgs[ci][1], cfgs[ci][2], sp_);
+          if (gemm_partial_floats(s.M, s.N, s.K, bf) > std::max<size_t>(1, maxP)) continue;
+          auto go = [&]() {
+            if (mode == 3)
+              gemm2_run(3, InX{A, nullptr, nullptr, nullptr, 0}, gx, Bt, nullptr, C, s.M, s.N, s.K, false, nullptr,
+                        1, st, part, StatSink{}, wgs, GradSink{}, bf);
+            else
+              gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st,
+                        part, sink, wgs, GradSink{}, bf);
+          };
+          for (int i = 0; i < 3; ++i) go();
+          hipEventRecord(e0, st);
+          for (int i = 0; i < 20; ++i) go();
+          hipEventRecord(e1, st);
+          hipEventSynchronize(e1);
+          float ms;
+          hipEventElapsedTime(&ms, e0, e1);
+          const double us = ms * 1e3 / 20;
+          if (us < best) { best = us; bc = ci; bs = sp_; }
+          printf("sweep M=%8d N=%5d K=%5d cfg=%d%d%d splits=%d  %8.1f us\n", s.M, s.N, s.K, cfgs[ci][0],
+                 cfgs[ci][1], cfgs[ci][2], sp_, us);
+        }
+      gemm2_force_cfg(0, 0, 0, 0);
+      printf("best   M=%8d N=%5d K=%5d cfg=%d%d%d splits=%d  %8.1f us\n", s.M, s.N, s.K, cfgs[bc][0], cfgs[bc][1],
+             cfgs[bc][2], bs, best);
+    }
+  }
   return 0;
 }
