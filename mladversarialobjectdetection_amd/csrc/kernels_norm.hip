@@ -1072,11 +1072,101 @@ __global__ void k_maxpool_bwd(const uint8_t* __restrict__ amax, const float* __r
   dx[idx] = g;
 }
 
+// Channel-quad forms (C % 4 == 0, every resample in the model tables): a lane owns 4 channels of
+// one pixel — 16-B loads and stores, the BN view's parameters loaded once per lane, 32-bit index
+// math — instead of one lane per element with 4-B accesses and 64-bit divisions (the scalar
+// kernels above ran the D4 BiFPN resamples at a fraction of HBM bandwidth; they remain for C % 4).
+__device__ __forceinline__ void quad_pos(int idx, int C4, int Wd, int Hd, int& c4, int& x, int& y, int& b) {
+  c4 = idx % C4;
+  const int p = idx / C4;
+  x = p % Wd;
+  const int q = p / Wd;
+  y = q % Hd;
+  b = q / Hd;
+}
+
+// max-pool: TF MaxPool picks the first maximum of the window (strict > after the first element)
+__global__ __launch_bounds__(256) void k_maxpool_fwd4(InX x, float4* __restrict__ y, uint32_t* __restrict__ amax,
+                                                      int H, int W, int C4, int Ho, int Wo, int k, int st, int pt,
+                                                      int pl, int total4) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total4) return;
+  int c4, ox, oy, b;
+  quad_pos(idx, C4, Wo, Ho, c4, ox, oy, b);
+  const int C = C4 * 4;
+  Chan4 ck;
+  if (x.mu) ck = inx_chan4(x, c4 * 4);
+  float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int am[4] = {-1, -1, -1, -1};
+  for (int i = 0; i < k; ++i) {
+    const int iy = oy * st - pt + i;
+    if (iy < 0 || iy >= H) continue;
+    for (int j = 0; j < k; ++j) {
+      const int ix = ox * st - pl + j;
+      if (ix < 0 || ix >= W) continue;
+      float4 v4 = *reinterpret_cast<const float4*>(x.p + ((long)(b * H + iy) * W + ix) * C + c4 * 4);
+      if (x.mu) v4 = inx_apply4(x, ck, v4);
+      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (am[e] < 0 || v[e] > m[e]) {
+          m[e] = v[e];
+          am[e] = i * k + j;
+        }
+    }
+  }
+  y[idx] = make_float4(m[0], m[1], m[2], m[3]);
+  amax[idx] = (uint32_t)(am[0] & 255) | ((uint32_t)(am[1] & 255) << 8) | ((uint32_t)(am[2] & 255) << 16) |
+              ((uint32_t)(am[3] & 255) << 24);
+}
+
+__global__ __launch_bounds__(256) void k_maxpool_bwd4(const uint32_t* __restrict__ amax, const float4* __restrict__ dy,
+                                                      float4* __restrict__ dx, int H, int W, int C4, int Ho, int Wo,
+                                                      int k, int st, int pt, int pl, int acc_flag, int total4) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total4) return;
+  int c4, ix, iy, b;
+  quad_pos(idx, C4, W, H, c4, ix, iy, b);
+  float g[4] = {0.f, 0.f, 0.f, 0.f};
+  const int oyl = max(0, (iy + pt - k + st) / st), oyh = min(Ho - 1, (iy + pt) / st);
+  const int oxl = max(0, (ix + pl - k + st) / st), oxh = min(Wo - 1, (ix + pl) / st);
+  for (int oy = oyl; oy <= oyh; ++oy) {
+    const int i = iy - (oy * st - pt);
+    if (i < 0 || i >= k) continue;
+    for (int ox = oxl; ox <= oxh; ++ox) {
+      const int j = ix - (ox * st - pl);
+      if (j < 0 || j >= k) continue;
+      const int o = ((b * Ho + oy) * Wo + ox) * C4 + c4;
+      const uint32_t a = amax[o];
+      const float4 d = dy[o];
+      const float dv[4] = {d.x, d.y, d.z, d.w};
+      const uint32_t want = (uint32_t)(i * k + j);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (((a >> (8 * e)) & 255u) == want) g[e] += dv[e];
+    }
+  }
+  float4 r = make_float4(g[0], g[1], g[2], g[3]);
+  if (acc_flag) {
+    const float4 p = dx[idx];
+    r.x += p.x; r.y += p.y; r.z += p.z; r.w += p.w;
+  }
+  dx[idx] = r;
+}
+
+static bool quad_ok(long total, int C) { return C % 4 == 0 && total / 4 < (1L << 31); }
+
 void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int C, int Ho, int Wo,
                         int k, int stride, int pt, int pl, hipStream_t s) {
   long total = (long)B * Ho * Wo * C;
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, amax, B, H, W, C, Ho,
-                     Wo, k, stride, pt, pl);
+  if (quad_ok(total, C)) {
+    const int t4 = (int)(total / 4);
+    hipLaunchKernelGGL(k_maxpool_fwd4, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, (float4*)y, (uint32_t*)amax, H, W,
+                       C / 4, Ho, Wo, k, stride, pt, pl, t4);
+  } else {
+    hipLaunchKernelGGL(k_maxpool_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, amax, B, H, W, C, Ho,
+                       Wo, k, stride, pt, pl);
+  }
   PHX_LAUNCH_CHECK();
 }
 
@@ -1084,8 +1174,14 @@ void launch_maxpool_bwd(const uint8_t* amax, const float* dy, float* dx, int B, 
                         int Ho, int Wo, int k, int stride, int pt, int pl, bool acc,
                         hipStream_t s) {
   long total = (long)B * H * W * C;
-  hipLaunchKernelGGL(k_maxpool_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, amax, dy, dx, B, H, W, C,
-                     Ho, Wo, k, stride, pt, pl, acc ? 1 : 0);
+  if (quad_ok(total, C) && quad_ok((long)B * Ho * Wo * C, C)) {
+    const int t4 = (int)(total / 4);
+    hipLaunchKernelGGL(k_maxpool_bwd4, dim3(cdiv(t4, 256)), dim3(256), 0, s, (const uint32_t*)amax,
+                       (const float4*)dy, (float4*)dx, H, W, C / 4, Ho, Wo, k, stride, pt, pl, acc ? 1 : 0, t4);
+  } else {
+    hipLaunchKernelGGL(k_maxpool_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, amax, dy, dx, B, H, W, C,
+                       Ho, Wo, k, stride, pt, pl, acc ? 1 : 0);
+  }
   PHX_LAUNCH_CHECK();
 }
 
@@ -1140,19 +1236,67 @@ __global__ void k_upsample_bwd(const float* __restrict__ dy, float* __restrict__
   dx[idx] = g;
 }
 
+__global__ __launch_bounds__(256) void k_upsample_fwd4(InX x, float4* __restrict__ y, int H, int W, int C4, int Ho,
+                                                       int Wo, int total4) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total4) return;
+  int c4, ox, oy, b;
+  quad_pos(idx, C4, Wo, Ho, c4, ox, oy, b);
+  const int sy = nn_src(oy, (float)H / (float)Ho, H);
+  const int sx = nn_src(ox, (float)W / (float)Wo, W);
+  y[idx] = inx_load4(x, ((long)(b * H + sy) * W + sx) * (C4 * 4) + c4 * 4, c4 * 4);
+}
+
+__global__ __launch_bounds__(256) void k_upsample_bwd4(const float4* __restrict__ dy, float4* __restrict__ dx, int H,
+                                                       int W, int C4, int Ho, int Wo, int acc_flag, int total4) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total4) return;
+  int c4, ix, iy, b;
+  quad_pos(idx, C4, W, H, c4, ix, iy, b);
+  const float sy = (float)H / (float)Ho, sx = (float)W / (float)Wo;
+  int oy0 = (int)floorf((float)iy / sy) - 1, oy1 = (int)ceilf((float)(iy + 1) / sy) + 1;
+  int ox0 = (int)floorf((float)ix / sx) - 1, ox1 = (int)ceilf((float)(ix + 1) / sx) + 1;
+  oy0 = max(oy0, 0); ox0 = max(ox0, 0); oy1 = min(oy1, Ho - 1); ox1 = min(ox1, Wo - 1);
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int oy = oy0; oy <= oy1; ++oy) {
+    if (nn_src(oy, sy, H) != iy) continue;
+    for (int ox = ox0; ox <= ox1; ++ox) {
+      if (nn_src(ox, sx, W) != ix) continue;
+      const float4 d = dy[((b * Ho + oy) * Wo + ox) * C4 + c4];
+      g.x += d.x; g.y += d.y; g.z += d.z; g.w += d.w;
+    }
+  }
+  if (acc_flag) {
+    const float4 p = dx[idx];
+    g.x += p.x; g.y += p.y; g.z += p.z; g.w += p.w;
+  }
+  dx[idx] = g;
+}
+
 void launch_upsample_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, int Wo,
                          hipStream_t s) {
   long total = (long)B * Ho * Wo * C;
-  hipLaunchKernelGGL(k_upsample_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho,
-                     Wo);
+  if (quad_ok(total, C)) {
+    const int t4 = (int)(total / 4);
+    hipLaunchKernelGGL(k_upsample_fwd4, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, (float4*)y, H, W, C / 4, Ho, Wo, t4);
+  } else {
+    hipLaunchKernelGGL(k_upsample_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho,
+                       Wo);
+  }
   PHX_LAUNCH_CHECK();
 }
 
 void launch_upsample_bwd(const float* dy, float* dx, int B, int H, int W, int C, int Ho, int Wo,
                          bool acc, hipStream_t s) {
   long total = (long)B * H * W * C;
-  hipLaunchKernelGGL(k_upsample_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, dx, B, H, W, C, Ho,
-                     Wo, acc ? 1 : 0);
+  if (quad_ok(total, C) && quad_ok((long)B * Ho * Wo * C, C)) {
+    const int t4 = (int)(total / 4);
+    hipLaunchKernelGGL(k_upsample_bwd4, dim3(cdiv(t4, 256)), dim3(256), 0, s, (const float4*)dy, (float4*)dx, H, W,
+                       C / 4, Ho, Wo, acc ? 1 : 0, t4);
+  } else {
+    hipLaunchKernelGGL(k_upsample_bwd, dim3(cdiv(total, 256)), dim3(256), 0, s, dy, dx, B, H, W, C, Ho,
+                       Wo, acc ? 1 : 0);
+  }
   PHX_LAUNCH_CHECK();
 }
 
@@ -1207,6 +1351,50 @@ __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
   }
 }
 
+// channel-quad form of k_fuse_bwd (C % 4 == 0): identical per-element arithmetic, 16-B accesses
+__global__ __launch_bounds__(256) void k_fuse_bwd4(FuseArgs fa, int nin, const float* __restrict__ w0,
+                                                   const float* __restrict__ w1, const float* __restrict__ w2,
+                                                   int method, int act, const float4* __restrict__ dy, long n4,
+                                                   int C) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float wv[3], den;
+  fuse_weights(w0, w1, w2, nin, method, wv, &den);
+  const int c = (int)((i * 4) % C);
+  const float4 a0 = inx_load4(fa.x[0], i * 4, c), a1 = inx_load4(fa.x[1], i * 4, c);
+  const float4 a2 = nin > 2 ? inx_load4(fa.x[2], i * 4, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 d4 = dy[i];
+  const float x0[4] = {a0.x, a0.y, a0.z, a0.w}, x1[4] = {a1.x, a1.y, a1.z, a1.w}, x2[4] = {a2.x, a2.y, a2.z, a2.w};
+  const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+  float dv[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float v;
+    if (method == 0) {
+      v = x0[e] * wv[0] / den;
+      v = v + x1[e] * wv[1] / den;
+      if (nin > 2) v = v + x2[e] * wv[2] / den;
+    } else {
+      v = x0[e] + x1[e];
+      if (nin > 2) v = v + x2[e];
+    }
+    dv[e] = dd[e] * act_grad(v, act);
+  }
+  for (int k = 0; k < nin; ++k) {
+    if (!fa.dx[k]) continue;
+    float g[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) g[e] = method == 0 ? (dv[e] / den) * wv[k] : dv[e];
+    float4* o = reinterpret_cast<float4*>(fa.dx[k]) + i;
+    float4 r = make_float4(g[0], g[1], g[2], g[3]);
+    if (fa.acc[k]) {
+      const float4 p = *o;
+      r.x += p.x; r.y += p.y; r.z += p.z; r.w += p.w;
+    }
+    *o = r;
+  }
+}
+
 void launch_fuse_fwd(const InX* xs, int nin, const float* wsm0, const float* wsm1,
                      const float* wsm2, int method, int act, float* y, long n, int C,
                      hipStream_t s) {
@@ -1226,8 +1414,12 @@ void launch_fuse_bwd(const InX* xs, int nin, const float* wsm0, const float* wsm
     fa.dx[i] = dxs[i];
     fa.acc[i] = acc[i] ? 1 : 0;
   }
-  hipLaunchKernelGGL(k_fuse_bwd, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
-                     method, act, dy, n, C);
+  if (C % 4 == 0)
+    hipLaunchKernelGGL(k_fuse_bwd4, dim3(cdiv(n / 4, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+                       method, act, (const float4*)dy, n / 4, C);
+  else
+    hipLaunchKernelGGL(k_fuse_bwd, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+                       method, act, dy, n, C);
   PHX_LAUNCH_CHECK();
 }
 
