@@ -191,12 +191,17 @@ __device__ __forceinline__ void fma4(float4& a, const float4& x, const float4& w
   a.w = fmaf(x.w, w.w, a.w);
 }
 
-// filter taps: K=3 kernels hold their 9 taps in registers; K=5 kernels read the 25 taps of
-// their 4 channels from LDS (all lanes of one channel group hit the same address, so the read
-// is a broadcast) — 100 VGPRs of taps would halve occupancy.
+// filter taps: read from LDS (all lanes of one channel group hit the same address, so the read is
+// a broadcast).  25 float4 taps of a 5x5 kernel held in registers cost 100 VGPRs and halved
+// occupancy (measured: the 5x5 forwards and data gradients 25 % faster from LDS, -2 % per step on
+// D0 and D4); for 3x3 the LDS form is equal or slightly faster.
+#ifndef PHX_DW_LDS_TAPS
+#define PHX_DW_LDS_TAPS 2
+#endif
 template <int K>
 struct Taps {
-  static constexpr bool kLds = false;
+  // 1: 5x5 taps in LDS (25 float4 in registers halved occupancy), 2: every kernel size
+  static constexpr bool kLds = PHX_DW_LDS_TAPS == 2 || (PHX_DW_LDS_TAPS == 1 && K > 3);
   float4 r[kLds ? 1 : K * K];
   const float4* l;
   int cg, CG;
@@ -609,7 +614,8 @@ static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k
 }
 
 static size_t dw_lds(const DwGeom& g, int k) {
-  return ((size_t)g.rin * g.cin + (k > 3 ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
+  const bool lds_taps = PHX_DW_LDS_TAPS == 2 || (PHX_DW_LDS_TAPS == 1 && k > 3);
+  return ((size_t)g.rin * g.cin + (lds_taps ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
 }
 
 template <int K, int S, int RPT, int NS, class XV>
