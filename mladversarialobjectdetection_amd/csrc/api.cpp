@@ -93,7 +93,6 @@ struct Exec {
   int* cand_list = nullptr;   // soft-NMS candidates appended by pre_nms [B][A] + counts [B]
   int* cand_count = nullptr;
   float* nms_ws = nullptr;
-  int* nms_wi = nullptr;
   float *nms1_boxes = nullptr, *nms1_scores = nullptr;
   int* nms1_count = nullptr;
   float *nms2_boxes = nullptr, *nms2_scores = nullptr;
@@ -200,7 +199,7 @@ struct phx_ctx {
   Exec* last = nullptr;
   std::string err;
   // scratch for phx_soft_nms standalone
-  DPtr sn_ws, sn_wi;
+  DPtr sn_ws;
   size_t sn_cap = 0;
   // scratch for phx_augment (per-image channel-sum partials)
   DPtr aug_ws;
@@ -606,8 +605,7 @@ Exec& phx_ctx::exec_for(int B) {
   E.cand_list = E.alloc<int>(BA);
   E.cand_count = E.alloc<int>(B);
   PHX_HIP(hipMemset(E.cand_count, 0, (size_t)B * sizeof(int)));
-  E.nms_ws = E.alloc<float>(BA);
-  E.nms_wi = E.alloc<int>(BA * 2);
+  E.nms_ws = E.alloc<float>(soft_nms_work_floats(B, A));
   E.nms1_boxes = E.alloc<float>((size_t)B * PHX_MAX_OUT * 4);
   E.nms1_scores = E.alloc<float>((size_t)B * PHX_MAX_OUT);
   E.nms1_count = E.alloc<int>(B);
@@ -1299,7 +1297,7 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0) {
 void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s) {
   Scope scope(ctx, "soft_nms", 0.0, (double)E.B * ctx->A * 5.0, s);
   launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->nms_thresh,
-                  0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, E.nms_wi, s,
+                  0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, s,
                   NmsCand{E.cand_list, E.cand_count, keep_mask, ctx->nms_thresh});
 }
 
@@ -1512,16 +1510,14 @@ int phx_soft_nms(phx_ctx* ctx, const float* boxes, const float* scores, const in
   if (!ctx || !boxes || !scores || B <= 0 || N <= 0) return PHX_EINVAL;
   PHX_TRY(ctx)
   hipStream_t s = (hipStream_t)stream;
-  size_t need = (size_t)B * N;
+  const size_t need = soft_nms_work_floats(B, N);
   if (need > ctx->sn_cap) {
     PHX_HIP(hipStreamSynchronize(s));
     ctx->sn_ws.reset(dalloc<float>(need));
-    ctx->sn_wi.reset(dalloc<int>(need * 2));
     ctx->sn_cap = need;
   }
   launch_soft_nms(boxes, scores, nullptr, 0, count, B, N, ctx->nms_thresh, 0.25f, PHX_MAX_OUT,
-                  (float)ctx->mc.image_size, ob, os, oc, (float*)ctx->sn_ws.get(),
-                  (int*)ctx->sn_wi.get(), s);
+                  (float)ctx->mc.image_size, ob, os, oc, (float*)ctx->sn_ws.get(), s);
   return PHX_OK;
   PHX_CATCH(ctx)
 }

@@ -227,8 +227,9 @@ void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDes
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,
                      int max_out, float clip_hi, float* out_boxes, float* out_scores,
-                     int* out_count, float* work_score, int* work_sb, hipStream_t s,
-                     NmsCand cand = NmsCand{});
+                     int* out_count, float* work, hipStream_t s, NmsCand cand = NmsCand{});
+// work floats of launch_soft_nms (compacted candidate boxes, spilled queue keys, anchors, visits)
+size_t soft_nms_work_floats(int B, int N);
 // per-image m_b = max(max_{keep} score, 0), tie count, and loss-gradient coefficient
 void launch_image_max(const float* scores, const uint8_t* keep, int B, int A, float* m,
                       int* argmax, int* nties, int* scratch, hipStream_t s);

@@ -7,6 +7,8 @@
 //   loss               attacker.py:189-193 and its gradient (ragged reduce_max, maximum(.,0))
 // Arithmetic that decides discrete outcomes (masks, thresholds, argmax) is kept in TF's fp32
 // operation order with FMA contraction disabled.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "post.hpp"
@@ -172,9 +174,20 @@ int pre_nms_tiles(int h, int w, int na) { return (h * w * na + kPreTile - 1) / k
 
 // ------------------------------------------------------------------------------------------
 // soft-NMS: one workgroup per image.  Exact restatement of NonMaxSuppressionV5's lazy
-// priority queue: pop the (score desc, index asc) maximum, decay it by every box selected
-// since its last visit (newest first, early exit at <= thresh), select if unchanged, else
-// re-queue while > thresh.  Candidate order = ragged (anchor) order.
+// priority queue: pop the (score desc, candidate order asc) maximum, decay it by every box
+// selected since its last visit (newest first, early exit at <= thresh), select if unchanged,
+// else re-queue while > thresh.  Candidate order = ragged (anchor) order.
+//
+// Layout (one image, dynamic LDS up to 160 KB):
+//  * candidates are compacted in anchor order (a bitmap of the candidate anchors, then a
+//    workgroup scan), so the candidate position IS the tie order and the queue key of position
+//    c is the 64-bit (score bits << 32 | ~c): scores are positive floats, so an unsigned max
+//    picks the higher score and, among equals, the lower position.  Removed = key 0.
+//  * the candidates' boxes are copied to a compacted global array (one load per pop);
+//  * score bits and last-visit counts live in LDS for the first `cap` positions, in global
+//    memory beyond; per-chunk maxima (chunks of 64*m positions) and per-group maxima (groups of
+//    64 chunks) in LDS, so a pop is one group scan, and a re-queue one chunk + one group rescan.
+//  * the pop loop runs in wave 0 alone (no workgroup barriers); its state is wave-uniform.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float tf_iou(const float* bi, const float* bj) {
   const float ymin_i = fminf(bi[0], bi[2]), xmin_i = fminf(bi[1], bi[3]);
@@ -191,175 +204,297 @@ __device__ __forceinline__ float tf_iou(const float* bi, const float* bj) {
 }
 
 constexpr int kNmsThreads = 256;
+constexpr int kNmsLdsBytes = 160 * 1024;
+constexpr int kNmsGroups = 64;  // group maxima (<= 64 groups of 64 chunks)
+
+struct NmsPlan {
+  int m;        // chunk = 64*m positions
+  int nchunk;   // chunks for N positions
+  int ck_bytes; // chunk-key region (also the bitmap of N bits during compaction)
+  int cap;      // positions whose key / visit count live in LDS
+  int lds;      // dynamic LDS bytes
+};
+
+static NmsPlan nms_plan(int N) {
+  NmsPlan p;
+  p.m = std::max(1, cdiv(N, 64L * 64 * kNmsGroups));
+  p.nchunk = cdiv(N, 64L * p.m);
+  const int bitmap = cdiv(N, 64) * 8;
+  p.ck_bytes = (std::max(p.nchunk * 8, bitmap) + 15) / 16 * 16;
+  const int fixed = kNmsGroups * 8 + PHX_MAX_OUT_DEV * 16 + PHX_MAX_OUT_DEV * 4 + kNmsThreads * 4 + 64;
+  int cap = (kNmsLdsBytes - fixed - p.ck_bytes) / 5 / 64 * 64;
+  p.cap = std::max(0, std::min(cap, (N + 63) / 64 * 64));
+  p.lds = fixed + p.ck_bytes + p.cap * 5;
+  p.lds = (p.lds + 15) / 16 * 16;
+  return p;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
+    const uint64_t w = ((uint64_t)hi << 32) | lo;
+    v = w > v ? w : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint64_t nms_key(uint32_t sbits, int pos) {
+  return sbits ? (((uint64_t)sbits << 32) | (uint32_t)~(uint32_t)pos) : 0ull;
+}
 
 __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     const float* __restrict__ boxes, const float* __restrict__ scores,
     const uint8_t* __restrict__ keep, int keep_mask, const int* __restrict__ count, int N,
     float score_thresh, float scale, int max_out, float clip_hi, float* __restrict__ out_boxes,
-    float* __restrict__ out_scores, int* __restrict__ out_count, float* __restrict__ wscore,
-    int* __restrict__ wsb, int* __restrict__ widx, NmsCand cand) {
+    float* __restrict__ out_scores, int* __restrict__ out_count, float4* __restrict__ cbox_all,
+    uint32_t* __restrict__ gkey_all, int* __restrict__ gwi_all, uint8_t* __restrict__ gwb_all,
+    NmsCand cand, NmsPlan pl) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char nms_smem[];
   const int b = blockIdx.x;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   const float* bb = boxes + (long)b * N * 4;
   const float* sb = scores + (long)b * N;
-  float* ws = wscore + (long)b * N;
-  int* wb = wsb + (long)b * N;
-  int* wi = widx + (long)b * N;
-  const int n_in = count ? count[b] : N;
+  float4* cbox = cbox_all + (long)b * N;
+  uint32_t* gkey = gkey_all + (long)b * N;
+  int* gwi = gwi_all + (long)b * N;
+  uint8_t* gwb = gwb_all + (long)b * N;
 
-  __shared__ int s_n;
-  __shared__ float sel_box[PHX_MAX_OUT_DEV][4];
-  __shared__ float sel_score[PHX_MAX_OUT_DEV];
-  __shared__ int s_nsel;
-  __shared__ int red_i[kNmsThreads];
-  __shared__ int s_done;
+  uint64_t* s_ck = reinterpret_cast<uint64_t*>(nms_smem);       // chunk maxima (or the bitmap)
+  uint32_t* s_bm = reinterpret_cast<uint32_t*>(nms_smem);
+  uint64_t* s_gk = reinterpret_cast<uint64_t*>(nms_smem + pl.ck_bytes);
+  float4* s_sel = reinterpret_cast<float4*>(s_gk + kNmsGroups);
+  float* s_sels = reinterpret_cast<float*>(s_sel + PHX_MAX_OUT_DEV);
+  int* s_scan = reinterpret_cast<int*>(s_sels + PHX_MAX_OUT_DEV);
+  int* s_misc = s_scan + kNmsThreads;
+  uint32_t* s_key = reinterpret_cast<uint32_t*>(s_misc + 16);
+  uint8_t* s_wb = reinterpret_cast<uint8_t*>(s_key + pl.cap);
+  const int cap = pl.cap;
 
+  // 1. bitmap of the candidate anchors (or count-prefix positions)
+  const int nbits = N;
+  const int nwords = (nbits + 63) / 64 * 2;
+  for (int w = t; w < nwords; w += kNmsThreads) s_bm[w] = 0u;
+  if (cand.list && t == 0) s_misc[0] = min(cand.count[b], N);
+  __syncthreads();
   if (cand.list) {
-    // 1'. candidates appended by pre_nms (score > thresh and keep & mask already applied)
-    if (t == 0) s_n = min(cand.count[b], N);
-    __syncthreads();
+    // candidates appended by pre_nms (score > thresh and keep & mask already applied)
+    const int nl = s_misc[0];
     const int* lst = cand.list + (long)b * N;
-    for (int i = t; i < s_n; i += kNmsThreads) {
+    for (int i = t; i < nl; i += kNmsThreads) {
       const int a = lst[i];
-      wi[i] = a;
-      ws[i] = sb[a];
-      wb[i] = 0;
+      atomicOr(&s_bm[a >> 5], 1u << (a & 31));
     }
     __syncthreads();
     if (t == 0) cand.count[b] = 0;  // consumed: the next pre_nms appends from 0
   } else {
-  // 1. ordered compaction of candidates with score > thresh (and mask): every lane owns a
-  //    contiguous segment, one workgroup scan of the segment counts places them
-  auto ok_at = [&](int i) -> bool {
-    bool ok = sb[i] > score_thresh;
-    if (keep) ok = ok && ((keep[(long)b * N + i] & keep_mask) != 0);
-    return ok;
-  };
-  const int per = (n_in + kNmsThreads - 1) / kNmsThreads;
-  const int lo = min(n_in, t * per), hi = min(n_in, lo + per);
+    const int n_in = count ? min(count[b], N) : N;
+    for (int base = 0; base < n_in; base += 4 * kNmsThreads) {
+      bool ok[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * kNmsThreads + t;
+        const int ic = min(i, N - 1);
+        bool o = sb[ic] > score_thresh;
+        if (keep) o = o && ((keep[(long)b * N + ic] & keep_mask) != 0);
+        ok[u] = o && i < n_in;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const unsigned long long bal = __ballot(ok[u]);
+        const int w0 = (base + u * kNmsThreads + wave * 64) >> 5;
+        if (lane == 0 && w0 < nwords) {
+          s_bm[w0] = (uint32_t)bal;
+          s_bm[w0 + 1] = (uint32_t)(bal >> 32);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // 2. ordered compaction: thread t owns words [t*per, (t+1)*per); a workgroup scan of their
+  //    popcounts places the anchors in order (written to gwi)
+  const int per = (nwords + kNmsThreads - 1) / kNmsThreads;
+  const int w_lo = min(nwords, t * per), w_hi = min(nwords, w_lo + per);
   int cnt = 0;
-  for (int i = lo; i < hi; ++i) cnt += ok_at(i) ? 1 : 0;
-  red_i[t] = cnt;
+  for (int w = w_lo; w < w_hi; ++w) cnt += __popc(s_bm[w]);
+  s_scan[t] = cnt;
   __syncthreads();
   for (int off = 1; off < kNmsThreads; off <<= 1) {
-    int v = (t >= off) ? red_i[t - off] : 0;
+    const int v = t >= off ? s_scan[t - off] : 0;
     __syncthreads();
-    red_i[t] += v;
+    s_scan[t] += v;
     __syncthreads();
   }
   {
-    int pos = red_i[t] - cnt;
-    for (int i = lo; i < hi; ++i) {
-      if (ok_at(i)) {
-        wi[pos] = i;
-        ws[pos] = sb[i];
-        wb[pos] = 0;
-        ++pos;
+    int pos = s_scan[t] - cnt;
+    for (int w = w_lo; w < w_hi; ++w) {
+      uint32_t bits = s_bm[w];
+      while (bits) {
+        const int bit = __ffs(bits) - 1;
+        bits &= bits - 1;
+        gwi[pos++] = w * 32 + bit;
       }
     }
   }
-  if (t == kNmsThreads - 1) s_n = red_i[t];
-  __syncthreads();
+  const int n = s_scan[kNmsThreads - 1];
+  __syncthreads();  // gwi complete (global writes of this workgroup, visible after the barrier)
+
+  // 3. gather keys and boxes in candidate order (coalesced over positions)
+  for (int p0 = 0; p0 < n; p0 += 4 * kNmsThreads) {
+    int a[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[u] = gwi[min(p0 + u * kNmsThreads + t, n - 1)];
+    float sc[4];
+    float4 bx[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      sc[u] = sb[a[u]];
+      bx[u] = *reinterpret_cast<const float4*>(bb + (long)a[u] * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + u * kNmsThreads + t;
+      if (p < n) {
+        cbox[p] = bx[u];
+        const uint32_t k = __float_as_uint(sc[u]);
+        if (p < cap) {
+          s_key[p] = k;
+          s_wb[p] = 0;
+        } else {
+          gkey[p] = k;
+          gwb[p] = 0;
+        }
+      }
+    }
   }
-  const int n = s_n;
-  if (t == 0) { s_nsel = 0; s_done = 0; }
   __syncthreads();
 
-  // 2. lazy priority-queue loop.  Lane t owns candidates t, t+256, ... and caches the best
-  //    (score desc, index asc) of its subset; only the owner of the candidate an iteration changed
-  //    rescans.  The decay factors of the selections since the candidate's last visit are computed
-  //    by one wave in parallel, then applied newest-first in order by one lane (same product, same
-  //    early exit as the sequential rule).
-  // order: score desc, then anchor index asc (the reference's candidate order); myi = position
-  auto better = [](float v, int a, float bv, int ba) { return v > bv || (v == bv && a < ba); };
-  float myv = -INFINITY;
-  int myi = 0x7fffffff, mya = 0x7fffffff;
-  for (int i = t; i < n; i += kNmsThreads) {
-    const float v = ws[i];
-    const int a = wi[i];
-    if (better(v, a, myv, mya)) { myv = v; myi = i; mya = a; }
-  }
-  __shared__ float wv_s[kNmsThreads / 64];
-  __shared__ int wv_i[kNmsThreads / 64], wv_a[kNmsThreads / 64];
-  __shared__ float fac[PHX_MAX_OUT_DEV];
-  __shared__ int s_c, s_from;
-  __shared__ float s_orig;
-  const int lane = t & 63, wave = t >> 6;
-  while (true) {
-    if (s_nsel >= max_out) break;
-    float v = myv;
-    int i = myi, a = mya;
-    for (int o = 32; o > 0; o >>= 1) {
-      const float v2 = __shfl_xor(v, o);
-      const int i2 = __shfl_xor(i, o);
-      const int a2 = __shfl_xor(a, o);
-      if (better(v2, a2, v, a)) { v = v2; i = i2; a = a2; }
-    }
-    if (lane == 0) { wv_s[wave] = v; wv_i[wave] = i; wv_a[wave] = a; }
-    __syncthreads();
-    if (t == 0) {
-      float bv = wv_s[0];
-      int bi = wv_i[0], ba = wv_a[0];
-      for (int w = 1; w < kNmsThreads / 64; ++w)
-        if (better(wv_s[w], wv_a[w], bv, ba)) { bv = wv_s[w]; bi = wv_i[w]; ba = wv_a[w]; }
-      if (!(bv > score_thresh) || bi == 0x7fffffff) {
-        s_done = 1;
-      } else {
-        s_c = bi;
-        s_orig = bv;
-        s_from = wb[bi];
+  // 4. chunk and group maxima
+  const int CH = 64 * pl.m;
+  const int nch = (n + CH - 1) / CH;
+  const int ngr = (nch + 63) / 64;
+  // spilled keys / visit counts are re-read after wave 0 rewrote them: volatile (L1-bypassing) loads
+  volatile const uint32_t* vgkey = gkey;
+  volatile const uint8_t* vgwb = gwb;
+  auto key_at = [&](int p) -> uint32_t { return p < cap ? s_key[p] : vgkey[p]; };
+  auto chunk_max = [&](int ch) -> uint64_t {
+    uint64_t v = 0;
+    for (int j = 0; j < pl.m; ++j) {
+      const int p = ch * CH + j * 64 + lane;
+      if (p < n) {
+        const uint64_t k = nms_key(key_at(p), p);
+        v = k > v ? k : v;
       }
     }
-    __syncthreads();
-    if (s_done) break;
-    const int c = s_c, from = s_from, nsel = s_nsel;
-    const float* cb = bb + (long)wi[c] * 4;
-    if (wave == 0)
-      for (int j = from + lane; j < nsel; j += 64) {
-        const float sim = tf_iou(cb, sel_box[j]);
-        fac[j] = expf(scale * sim * sim);
-      }
-    __syncthreads();
-    if (t == 0) {
-      const float orig = s_orig;
-      float sc = orig;
-      for (int j = nsel - 1; j >= from; --j) {
-        sc *= fac[j];
-        if (sc <= score_thresh) break;
-      }
-      wb[c] = nsel;
-      if (sc == orig) {
-        sel_box[nsel][0] = cb[0]; sel_box[nsel][1] = cb[1];
-        sel_box[nsel][2] = cb[2]; sel_box[nsel][3] = cb[3];
-        sel_score[nsel] = sc;
-        s_nsel = nsel + 1;
-        ws[c] = -INFINITY;
-      } else if (sc > score_thresh) {
-        ws[c] = sc;
-      } else {
-        ws[c] = -INFINITY;
-      }
-    }
-    __syncthreads();
-    if (t == c % kNmsThreads) {
-      myv = -INFINITY;
-      myi = mya = 0x7fffffff;
-      for (int k = t; k < n; k += kNmsThreads) {
-        const float vv = ws[k];
-        const int ak = wi[k];
-        if (better(vv, ak, myv, mya)) { myv = vv; myi = k; mya = ak; }
-      }
-    }
+    return wave_max_u64(v);
+  };
+  for (int ch = wave; ch < nch; ch += kNmsThreads / 64) {
+    const uint64_t v = chunk_max(ch);
+    if (lane == 0) s_ck[ch] = v;
   }
   __syncthreads();
-  // 3. outputs: padded to max_out, boxes clipped to [0, image_size] (postprocess.py:61-64)
-  const int nsel = s_nsel;
+  for (int g = wave; g < ngr; g += kNmsThreads / 64) {
+    const int ch = g * 64 + lane;
+    const uint64_t v = wave_max_u64(ch < nch ? s_ck[ch] : 0ull);
+    if (lane == 0) s_gk[g] = v;
+  }
+  __syncthreads();
+
+  // 5. the lazy priority queue, wave 0 only
+  if (wave == 0) {
+    const uint32_t tbits = __float_as_uint(score_thresh);
+    int nsel = 0;
+    while (nsel < max_out) {
+      const uint64_t top = wave_max_u64(lane < ngr ? s_gk[lane] : 0ull);
+      if (top == 0ull) break;
+      const uint32_t vbits = (uint32_t)(top >> 32);
+      if (!(__uint_as_float(vbits) > score_thresh)) break;
+      (void)tbits;
+      const int c = (int)~(uint32_t)top;
+      const float orig = __uint_as_float(vbits);
+      const int from = c < cap ? (int)s_wb[c] : (int)vgwb[c];
+      const float4 cb4 = cbox[c];
+      const float cb[4] = {cb4.x, cb4.y, cb4.z, cb4.w};
+      // decay factors of the selections since the last visit, newest first: lane l holds
+      // selection nsel-1-l (and nsel-65-l)
+      const int nf = nsel - from;
+      float f0 = 1.f, f1 = 1.f;
+      if (lane < nf) {
+        const float4 s4 = s_sel[nsel - 1 - lane];
+        const float sbx[4] = {s4.x, s4.y, s4.z, s4.w};
+        const float sim = tf_iou(cb, sbx);
+        f0 = expf(scale * sim * sim);
+      }
+      if (lane + 64 < nf) {
+        const float4 s4 = s_sel[nsel - 65 - lane];
+        const float sbx[4] = {s4.x, s4.y, s4.z, s4.w};
+        const float sim = tf_iou(cb, sbx);
+        f1 = expf(scale * sim * sim);
+      }
+      float sc = orig;
+      for (int k = 0; k < nf; ++k) {
+        const float f = __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
+            (int)__float_as_uint(k < 64 ? f0 : f1), k & 63));
+        sc *= f;
+        if (sc <= score_thresh) break;
+      }
+      uint32_t nk;
+      if (sc == orig) {
+        if (lane == 0) {
+          s_sel[nsel] = cb4;
+          s_sels[nsel] = sc;
+        }
+        ++nsel;
+        nk = 0u;
+      } else {
+        nk = sc > score_thresh ? __float_as_uint(sc) : 0u;
+      }
+      // the candidate's new key and visit count (wb = selections at this visit)
+      const int wbnew = (sc == orig) ? nsel - 1 : nsel;
+      if (lane == 0) {
+        if (c < cap) {
+          s_key[c] = nk;
+          s_wb[c] = (uint8_t)wbnew;
+        } else {
+          gkey[c] = nk;
+          gwb[c] = (uint8_t)wbnew;
+        }
+      }
+      // rescan c's chunk (c's own value from registers) and its group
+      const int ch = c / CH;
+      uint64_t v = 0;
+      for (int j = 0; j < pl.m; ++j) {
+        const int p = ch * CH + j * 64 + lane;
+        if (p < n) {
+          const uint64_t k = p == c ? nms_key(nk, p) : nms_key(key_at(p), p);
+          v = k > v ? k : v;
+        }
+      }
+      const uint64_t cmax = wave_max_u64(v);
+      const int g = ch >> 6;
+      const int chl = g * 64 + lane;
+      uint64_t gv = chl == ch ? cmax : (chl < nch ? s_ck[chl] : 0ull);
+      gv = wave_max_u64(gv);
+      if (lane == 0) {
+        s_ck[ch] = cmax;
+        s_gk[g] = gv;
+      }
+    }
+    if (lane == 0) s_misc[1] = nsel;
+  }
+  __syncthreads();
+  // 6. outputs: padded to max_out, boxes clipped to [0, image_size] (postprocess.py:61-64)
+  const int nsel = s_misc[1];
   for (int k = t; k < max_out; k += kNmsThreads) {
     float* ob = out_boxes + ((long)b * max_out + k) * 4;
     if (k < nsel) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) ob[j] = fminf(fmaxf(sel_box[k][j], 0.0f), clip_hi);
-      out_scores[(long)b * max_out + k] = sel_score[k];
+      const float4 s4 = s_sel[k];
+      ob[0] = fminf(fmaxf(s4.x, 0.0f), clip_hi);
+      ob[1] = fminf(fmaxf(s4.y, 0.0f), clip_hi);
+      ob[2] = fminf(fmaxf(s4.z, 0.0f), clip_hi);
+      ob[3] = fminf(fmaxf(s4.w, 0.0f), clip_hi);
+      out_scores[(long)b * max_out + k] = s_sels[k];
     } else {
       ob[0] = ob[1] = ob[2] = ob[3] = 0.f;
       out_scores[(long)b * max_out + k] = 0.f;
@@ -368,17 +503,32 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   if (t == 0) out_count[b] = nsel;
 }
 
+size_t soft_nms_work_floats(int B, int N) { return (size_t)B * N * 7; }
+
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,
                      int max_out, float clip_hi, float* out_boxes, float* out_scores,
-                     int* out_count, float* work_score, int* work_sb, hipStream_t s, NmsCand cand) {
-  if (max_out > PHX_MAX_OUT_DEV) throw std::runtime_error("soft_nms: max_out too large");
+                     int* out_count, float* work, hipStream_t s, NmsCand cand) {
+  if (max_out > PHX_MAX_OUT_DEV || max_out > 128) throw std::runtime_error("soft_nms: max_out too large");
+  const NmsPlan pl = nms_plan(N);
+  if (pl.lds > kNmsLdsBytes || pl.nchunk > 64 * kNmsGroups) throw std::runtime_error("soft_nms: too many candidates");
   // TF: scale = -0.5 / soft_nms_sigma (soft_nms_sigma = sigma / 2, postprocess.py:191-200)
   float scale = soft_sigma > 0.f ? -0.5f / soft_sigma : 0.f;
-  int* widx = work_sb + (long)B * N;
-  hipLaunchKernelGGL(k_soft_nms, dim3(B), dim3(kNmsThreads), 0, s, boxes, scores, keep, keep_mask,
-                     count, N, score_thresh, scale, max_out, clip_hi, out_boxes, out_scores,
-                     out_count, work_score, work_sb, widx, cand);
+  // work (soft_nms_work_floats): compacted boxes [B][N] float4 | keys [B][N] | anchors [B][N] |
+  // visit counts [B][N] bytes
+  const long BN = (long)B * N;
+  float4* cbox = reinterpret_cast<float4*>(work);
+  uint32_t* gkey = reinterpret_cast<uint32_t*>(work + 4 * BN);
+  int* gwi = reinterpret_cast<int*>(work + 5 * BN);
+  uint8_t* gwb = reinterpret_cast<uint8_t*>(work + 6 * BN);
+  static bool attr = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_soft_nms),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kNmsLdsBytes) == hipSuccess;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL(k_soft_nms, dim3(B), dim3(kNmsThreads), pl.lds, s, boxes, scores, keep, keep_mask,
+                     count, N, score_thresh, scale, max_out, clip_hi, out_boxes, out_scores, out_count,
+                     cbox, gkey, gwi, gwb, cand, pl);
   PHX_LAUNCH_CHECK();
 }
 

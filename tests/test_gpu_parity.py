@@ -80,6 +80,31 @@ def test_soft_nms_exact(victim):
         np.testing.assert_array_equal(ob[b, :n], rb[:n])
 
 
+def test_soft_nms_dense_exact(victim):
+    """Every anchor of a D0 512^2 image a candidate (the person-prior stress case: thousands of
+    re-queues per image, candidates beyond the kernel's LDS capacity spill to global memory) and
+    quantised scores (score ties broken by candidate order)."""
+    from oracle import postprocess as pp
+    from oracle.detector import anchors
+    rng = np.random.default_rng(11)
+    A = anchors(512).reshape(-1, 4).astype(np.float32)
+    N = A.shape[0]
+    bx = np.stack([A + rng.normal(0, 2, A.shape).astype(np.float32) for _ in range(2)])
+    sc = (1 / (1 + np.exp(-(rng.normal(0, 1, (2, N)) + 4.6)))).astype(np.float32)
+    sc[1] = np.round(sc[1] * 64) / 64  # ties
+    sc[1] = np.minimum(sc[1], np.float32(0.999))
+    cnt = np.array([N, 40000], np.int32)
+    ob, os_, oc = victim.soft_nms(torch.as_tensor(bx).cuda(), torch.as_tensor(sc).cuda(),
+                                  torch.as_tensor(cnt).cuda())
+    ob, os_, oc = ob.cpu().numpy(), os_.cpu().numpy(), oc.cpu().numpy()
+    for b in range(2):
+        rb, rs, n = pp.nms_padded(bx[b, :cnt[b]], sc[b, :cnt[b]], S, 100, 0.5)
+        assert oc[b] == n == 100
+        # decayed scores: the device expf and numpy's exp may differ by an ulp (as above)
+        np.testing.assert_allclose(os_[b, :n], rs[:n], rtol=2e-6, atol=0)
+        np.testing.assert_array_equal(ob[b, :n], rb[:n])
+
+
 def test_brightness_matcher(victim):
     from mladversarialobjectdetection_amd.attacker import BrightnessMatcher
     from oracle import eot
