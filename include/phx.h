@@ -224,6 +224,42 @@ int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream);
  * nfloats floats (device->device).  PHX_EINVAL if the name or size is wrong, or no gradient exists. */
 int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size_t nfloats, void* stream);
 
+/* ---- defender step (BASELINE C5) ------------------------------------------
+ * attack_detection.PatchAttackDefender (attack_detection.py:31-206, training) over a frozen
+ * victim ctx: first pass (inference BN, person anchors, soft-NMS, filter_valid_boxes), Masker
+ * (self-supervised patches, attack_detection.py:321-498), 2 * PatchNeutralizer(images)
+ * (generator.py:17-277: attention U-Net, n_filters 8, dropout 0.2, batch norm) and
+ * loss = sum_b mean((targets - updates)^2) with its gradient w.r.t. the U-Net variables.
+ * The variables are one flat float buffer in phx_def_manifest order (Keras shapes and layouts:
+ * conv kernels [k,k,in,out], transposed-conv kernels [k,k,out,in]); the library owns the BN moving
+ * statistics (updated by every step, as Keras training-mode BN).  Replaces generator.define_model
+ * + PatchAttackDefender.__init__ (attack_detection.py:34-71). */
+typedef struct phx_def phx_def;
+/* the U-Net at the victim's image size (a multiple of 16, >= 240); seed keys the Masker's and
+ * Dropout's Philox draws */
+int phx_def_create(phx_ctx* victim, int max_batch, uint64_t seed, phx_def** out);
+void phx_def_destroy(phx_def* d);
+const char* phx_def_last_error(phx_def* d);
+int64_t phx_def_num_params(phx_def* d);
+int64_t phx_def_num_moving(phx_def* d);
+/* JSON {n_params, n_moving, params: [{name, shape, offset}], bn: [{name, channels, moving_mean,
+ * moving_variance}]} (offsets in floats) */
+int phx_def_manifest(phx_def* d, char* buf, size_t cap, size_t* needed);
+/* BN moving statistics: src != NULL loads them, dst != NULL copies them out (any memory) */
+int phx_def_moving(phx_def* d, float* dst, const float* src, void* stream);
+int phx_def_workspace_bytes(phx_def* d, int B, size_t* bytes);
+/* PatchAttackDefender.call(images, training=True) + tape.gradient (attack_detection.py:168-206).
+ * boxes [B,100,4] + count [B] (device) place the patches; NULL = the victim's first pass.
+ * grad: num_params floats followed by the metric row [loss] (SUM-all-reducible). */
+int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,
+                      const float* params, float* grad, int64_t step, int32_t global_image_offset, void* stream);
+/* debug copies of the last step (device->device): patched images / targets / updates [B,H,W,3],
+ * first-pass boxes [B,100,4], counts [B] (int32 bits) */
+enum { PHX_DEF_PATCHED = 0, PHX_DEF_TARGETS = 1, PHX_DEF_UPDATES = 2, PHX_DEF_BOXES = 3, PHX_DEF_COUNTS = 4 };
+int phx_def_debug(phx_def* d, int what, float* dst, size_t nfloats, void* stream);
+/* Keras Adam without constraints (the defender's optimizer, defender_train.py:35) */
+int phx_adam(float* params, const float* grad, float* m, float* v, int64_t n, float lr, int64_t t, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

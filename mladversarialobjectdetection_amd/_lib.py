@@ -88,7 +88,23 @@ _SIGS = [
     ("phx_debug_last_maxscores", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_image_grad", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_tap", c_int, [c_void_p, c_char_p, c_int, c_void_p, c_size_t, c_void_p]),
+    # defender step
+    ("phx_def_create", c_int, [c_void_p, c_int, c_uint64, POINTER(c_void_p)]),
+    ("phx_def_destroy", None, [c_void_p]),
+    ("phx_def_last_error", c_char_p, [c_void_p]),
+    ("phx_def_num_params", c_int64, [c_void_p]),
+    ("phx_def_num_moving", c_int64, [c_void_p]),
+    ("phx_def_manifest", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
+    ("phx_def_moving", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("phx_def_workspace_bytes", c_int, [c_void_p, c_int, POINTER(c_size_t)]),
+    ("phx_def_step_grad", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    ("phx_def_debug", c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
+    ("phx_adam", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_int64, c_void_p]),
 ]
+
+# phx_def_debug tensors
+DEF_PATCHED, DEF_TARGETS, DEF_UPDATES, DEF_BOXES, DEF_COUNTS = range(5)
 
 EXPORTED = [s[0] for s in _SIGS]
 
@@ -189,3 +205,38 @@ class Context:
     def call(self, name: str, *args):
         rc = getattr(self.lib, name)(self.h, *args)
         check(self.h, rc, name)
+
+
+class Defender:
+    """Owns one phx_def (the defender's U-Net + Masker) over a victim Context."""
+
+    def __init__(self, ctx: Context, max_batch: int, seed: int = 0):
+        self.lib = ctx.lib
+        self.ctx = ctx  # keeps the victim alive
+        h = c_void_p()
+        rc = self.lib.phx_def_create(ctx.h, int(max_batch), int(seed) & ((1 << 64) - 1), ctypes.byref(h))
+        if rc != 0:
+            raise PhxError(f"phx_def_create failed ({rc})")
+        self.h = h
+        self.max_batch = int(max_batch)
+        self.num_params = int(self.lib.phx_def_num_params(h))
+        self.num_moving = int(self.lib.phx_def_num_moving(h))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            self.lib.phx_def_destroy(h)
+            self.h = None
+
+    def manifest(self) -> dict:
+        need = c_size_t()
+        self.call("phx_def_manifest", None, 0, ctypes.byref(need))
+        buf = ctypes.create_string_buffer(need.value)
+        self.call("phx_def_manifest", buf, need.value, ctypes.byref(need))
+        return json.loads(buf.value.decode())
+
+    def call(self, name: str, *args):
+        rc = getattr(self.lib, name)(self.h, *args)
+        if rc != 0:
+            msg = self.lib.phx_def_last_error(self.h)
+            raise PhxError(f"{name} failed ({rc}): {msg.decode() if msg else ''}")

@@ -19,6 +19,7 @@
 #include "model.hpp"
 #include "phx.h"
 #include "post.hpp"
+#include "unet.hpp"
 
 using namespace phx;
 
@@ -998,11 +999,13 @@ DropView drop_view(const Exec& E, int op) {
 
 // train = false: Keras training=False (test_step, attacker.py:325) — inference BN from the moving
 // statistics (not updated) and no drop connect, whatever the context's BN mode
+// force_frozen: inference BN in a training pass (a victim whose layers are not trainable, as the
+// defender's protege, attack_detection.py:46-47); drop connect still follows `train`
 void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int pass, int64_t step,
-                 int gimg0, bool train = true) {
+                 int gimg0, bool train = true, bool force_frozen = false) {
   const Program& P = E.prog;
   float* W = ctx->w();
-  const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train;
+  const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train || force_frozen;
   if (E.ndrop && train)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   for (size_t i = 0; i < P.ops.size(); ++i) {
@@ -1301,6 +1304,27 @@ void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc
                   NmsCand{E.cand_list, E.cand_count, keep_mask, ctx->nms_thresh});
 }
 
+}  // namespace
+
+int phx::ctx_image_size(const phx_ctx* ctx) { return ctx->mc.image_size; }
+uint64_t phx::ctx_seed(const phx_ctx* ctx) { return ctx->seed; }
+int phx::ctx_device(const phx_ctx* ctx) { return ctx->device; }
+
+void phx::def_first_pass(phx_ctx* ctx, const float* images, int B, int64_t step, int gimg0, float* boxes, int* count,
+                    hipStream_t s) {
+  if (!ctx->weights_loaded) throw std::logic_error("weights not loaded");
+  if (B <= 0 || B > ctx->max_batch) throw std::out_of_range("batch exceeds max_batch");
+  Exec& E = ctx->exec_for(B);
+  // the protege's layers are frozen (inference BN); the call's training flag still reaches its
+  // drop connect (attack_detection.py:46-47, 183)
+  run_forward(ctx, E, images, s, 0, step, gimg0, true, true);
+  run_pre_nms(ctx, E, s, 4);  // person anchors only (attack_detection.py:116-121)
+  run_nms(ctx, E, 4, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
+  const float S = (float)ctx->mc.image_size;
+  def_filter(E.nms1_boxes, E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, S, S, ctx->filter_thresh, boxes, count, s);
+}
+
+namespace {
 // run `fn(side)` on the executor's side stream after the work enqueued on `s` so far; join_side
 // makes `s` wait for it
 void check_ready(phx_ctx* ctx, int B) {

@@ -358,6 +358,9 @@ enum RngStream : uint32_t {
   RNG_DROP = 5,       // per (MBConv block, pass, image): drop-connect uniform (utils.py:336-339)
   RNG_AUG = 6,        // input pipeline: per image flips, per batch contrast / brightness
                       // (train_data_generator.py:201-204, 222-225)
+  RNG_DSHUF = 7,      // defender Masker: per image shuffle key (attack_detection.py:487)
+  RNG_DFLIP = 8,      // defender Masker: per image left-right / up-down flips (:488-489)
+  RNG_DROPOUT = 9,    // defender U-Net: per (layer, image, element) Dropout(0.2) uniform
 };
 
 }  // namespace phx

@@ -59,9 +59,10 @@ __global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __res
                                                    uint64_t seed, int64_t step, int gimg0,
                                                    ImgParams* __restrict__ img,
                                                    BoxPlace* __restrict__ place,
-                                                   int* __restrict__ lists, int* __restrict__ err) {
+                                                   int* __restrict__ lists, int* __restrict__ err,
+                                                   PlaceRule rule) {
   const int t = threadIdx.x;
-  const float scale = params[PHX_NPATCH_DEV];
+  const float scale = params ? params[PHX_NPATCH_DEV] : 0.f;
   const float Hf = (float)d.H, Wf = (float)d.W;
   for (int b = t; b < d.B; b += blockDim.x) {
     u32x4 r = rng(seed, 0, 0, (uint32_t)(gimg0 + b), step, RNG_PRINT);
@@ -86,10 +87,11 @@ __global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __res
       const float ymin = bx[0], xmin = bx[1], ymax = bx[2], xmax = bx[3];
       const float h = ymax - ymin, w = xmax - xmin;
       const float longer = fmaxf(h, w);
-      const float psf = floorf(longer * scale);
-      const float diag = fminf(1.41421354f * psf, Wf);
       u32x4 r = rng(seed, 0, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_PLACE);
-      const float tol = 0.2f;
+      const float bscale = rule.random_scale ? runif(r.z, rule.scale_lo, rule.scale_hi) : scale;
+      const float psf = floorf(longer * bscale);
+      const float diag = fminf(1.41421354f * psf, Wf);
+      const float tol = rule.tol;
       const float oy = (ymin + h / 2.0f) + runif(r.x, (-tol * h) / 2.0f, (tol * h) / 2.0f);
       const float ox = (xmin + w / 2.0f) + runif(r.y, (-tol * w) / 2.0f, (tol * w) / 2.0f);
       float yp = fmaxf(oy - diag / 2.0f, 0.0f);
@@ -238,10 +240,10 @@ __global__ __launch_bounds__(256) void k_eot_spans(EotDims d, const BoxPlace* __
 
 void launch_eot_place(const EotDims& d, const float* boxes, const int* count, const float* params,
                       uint64_t seed, int64_t step, int gimg0, ImgParams* img, BoxPlace* place,
-                      SpanEntry* spans, int* err, hipStream_t s) {
+                      SpanEntry* spans, int* err, hipStream_t s, PlaceRule rule) {
   int* lists = reinterpret_cast<int*>(place + (long)d.B * d.maxb);
   hipLaunchKernelGGL(k_eot_place, dim3(1), dim3(256), 0, s, d, boxes, count, params, seed, step,
-                     gimg0, img, place, lists, err);
+                     gimg0, img, place, lists, err, rule);
   PHX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_eot_spans, dim3(2, d.B * d.maxb), dim3(256), 0, s, d, place, spans);
   PHX_LAUNCH_CHECK();
@@ -364,6 +366,18 @@ void launch_eot_match(const EotDims& d, const float* patch, const ImgParams* img
   PHX_LAUNCH_CHECK();
 }
 
+void launch_eot_match_batch(const EotDims& d, const float* src, const ImgParams* img, const float* tgt,
+                            float* matched, double* ysum, float* ymean, hipStream_t s) {
+  const long stride = (long)d.P * d.P * 3;
+  hipLaunchKernelGGL(k_eot_ysum, dim3(kYChunks, d.B, 2), dim3(256), 0, s, d, src, stride, img, tgt, 1, ysum);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_ymean, dim3(cdiv(d.B * 2, 64)), dim3(64), 0, s, d, ysum, kYChunks, ymean);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_eot_match, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d, src, stride, img,
+                     ymean, 1, matched);
+  PHX_LAUNCH_CHECK();
+}
+
 // ------------------------------------------------------------------------------------------
 // per-box kernels walk (valid box, 256-pixel chunk) work items
 // ------------------------------------------------------------------------------------------
@@ -412,7 +426,7 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
                                                     const BoxPlace* __restrict__ place,
                                                     const SpanEntry* __restrict__ spans,
                                                     uint64_t seed, int64_t step, int gimg0,
-                                                    float* __restrict__ rstore) {
+                                                    float* __restrict__ rstore, float amp) {
   extern __shared__ float V[];  // [kResizeRT][nx][3]
   const ListView L = lists_of(d, place);
   const int nv = *L.nvalid, total = L.tprefix[nv];
@@ -459,9 +473,9 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
       const int px = (i0 + ii) * P.ps + j;
       u32x4 r = rng(seed, (uint32_t)px, (uint32_t)k, (uint32_t)(gimg0 + b), step, RNG_NOISE);
       float* o = rstore + P.roff + (long)px * 3;
-      o[0] = (a0 + runif(r.x, -0.01f, 0.01f)) + P.delta;
-      o[1] = (a1 + runif(r.y, -0.01f, 0.01f)) + P.delta;
-      o[2] = (a2 + runif(r.z, -0.01f, 0.01f)) + P.delta;
+      o[0] = (a0 + runif(r.x, -amp, amp)) + P.delta;
+      o[1] = (a1 + runif(r.y, -amp, amp)) + P.delta;
+      o[2] = (a2 + runif(r.z, -amp, amp)) + P.delta;
     }
     __syncthreads();
   }
@@ -469,10 +483,10 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
 
 void launch_eot_resize(const EotDims& d, const float* matched, const BoxPlace* place,
                        const SpanEntry* spans, uint64_t seed, int64_t step, int gimg0,
-                       float* rstore, hipStream_t s) {
+                       float* rstore, hipStream_t s, float noise_amp) {
   const size_t shm = (size_t)kResizeRT * d.P * 3 * sizeof(float);
   hipLaunchKernelGGL(k_eot_resize, dim3(kResizeGrid), dim3(256), shm, s, d, matched, place, spans,
-                     seed, step, gimg0, rstore);
+                     seed, step, gimg0, rstore, noise_amp);
   PHX_LAUNCH_CHECK();
 }
 
@@ -500,7 +514,8 @@ __global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* _
                                                        const BoxPlace* __restrict__ place,
                                                        const float* __restrict__ rstore,
                                                        float* __restrict__ img_out,
-                                                       int16_t* __restrict__ owner) {
+                                                       int16_t* __restrict__ owner,
+                                                       float* __restrict__ mask) {
   const long npx = (long)d.H * d.W;
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (long)d.B * npx) return;
@@ -511,12 +526,14 @@ __global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* _
   const float* ip = img_in + idx * 3;
   float v[3] = {ip[0], ip[1], ip[2]};
   int16_t own[3] = {-1, -1, -1};
+  bool covered = false;
   const int n = L.img_n[b], f = L.img_first[b];
   for (int q = 0; q < n; ++q) {
     const int sl = L.vlist[f + q];
     const BoxPlace& P = place[sl];
     const int qy = y - P.ymin, qx = x - P.xmin;
     if (qy < 0 || qy >= P.diag || qx < 0 || qx >= P.diag) continue;
+    covered = true;
     const float ox = (float)qx, oy = (float)qy;
     const float proj = 0.0f * ox + 0.0f * oy + 1.0f;
     const float inx = (P.fwd[0] * ox + P.fwd[1] * oy + P.fwd[2]) / proj;
@@ -534,6 +551,12 @@ __global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* _
     }
   }
   float* op = img_out + idx * 3;
+  if (mask) {
+    float* mp = mask + idx * 3;
+    mp[0] = covered ? ip[0] - v[0] : 0.f;
+    mp[1] = covered ? ip[1] - v[1] : 0.f;
+    mp[2] = covered ? ip[2] - v[2] : 0.f;
+  }
   op[0] = v[0]; op[1] = v[1]; op[2] = v[2];
   if (owner) {
     owner[idx * 3 + 0] = own[0];
@@ -543,10 +566,11 @@ __global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* _
 }
 
 void launch_eot_composite(const EotDims& d, const float* img_in, const BoxPlace* place,
-                          const float* rstore, float* img_out, int16_t* owner, hipStream_t s) {
+                          const float* rstore, float* img_out, int16_t* owner, hipStream_t s,
+                          float* mask) {
   long n = (long)d.B * d.H * d.W;
   hipLaunchKernelGGL(k_eot_composite, dim3(cdiv(n, 256)), dim3(256), 0, s, d, img_in, place, rstore,
-                     img_out, owner);
+                     img_out, owner, mask);
   PHX_LAUNCH_CHECK();
 }
 
@@ -903,10 +927,12 @@ __global__ __launch_bounds__(256) void k_adam(float* __restrict__ params,
   m[i] = mi;
   v[i] = vi;
   float x = params[i] - (mi * alpha) / (sqrtf(vi) + eps);
-  if (i < npatch)
-    x = fminf(fmaxf(x, -1.0f), 1.0f);
-  else
-    x = fminf(fmaxf(x, 0.0f), 1.0f);
+  if (npatch >= 0) {  // the attacker's constraints (npatch < 0: plain Adam, the defender's U-Net)
+    if (i < npatch)
+      x = fminf(fmaxf(x, -1.0f), 1.0f);
+    else
+      x = fminf(fmaxf(x, 0.0f), 1.0f);
+  }
   params[i] = x;
 }
 
@@ -917,6 +943,13 @@ void launch_adam_clip(float* params, const float* grad, float* m, float* v, long
   const float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
   hipLaunchKernelGGL(k_adam, dim3(cdiv(n, 256)), dim3(256), 0, s, params, grad, m, v, n, alpha,
                      (long)PHX_NPATCH_DEV);
+  PHX_LAUNCH_CHECK();
+}
+
+void launch_adam(float* params, const float* grad, float* m, float* v, long n, float lr, int64_t t, hipStream_t s) {
+  const float b1p = powf(0.9f, (float)t), b2p = powf(0.999f, (float)t);
+  const float alpha = lr * sqrtf(1.0f - b2p) / (1.0f - b1p);
+  hipLaunchKernelGGL(k_adam, dim3(cdiv(n, 256)), dim3(256), 0, s, params, grad, m, v, n, alpha, -1L);
   PHX_LAUNCH_CHECK();
 }
 

@@ -154,6 +154,7 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     kf = 1;
     if (sc >= thresh) kf |= 2;
   }
+  if (am == 0) kf |= 4;  // person, before the validity filter (the defender's odet_model)
   keep[idx] = kf;
   want = (kf & cand.mask) != 0 && sc > cand.thresh;
   }

@@ -1,0 +1,759 @@
+// kernels_unet.hip — the defender step's attention U-Net (generator.py:17-277) forward and weight
+// gradient, its Masker extras (attack_detection.py:321-498) and its loss (attack_detection.py:194-198).
+//
+// Design (MI355X): every 3x3 convolution is a gather into a K-contiguous column matrix (im2col,
+// K = 9*Cin padded to a multiple of 4) followed by the library's persistent MFMA GEMM
+// (kernels_gemm.hip); the data gradient of a stride-1 conv is the same gather of dY against the
+// flipped kernel, the transposed conv's forward is a parity gather (out[2i + k] += x[i] w[k]) and
+// its data gradient a stride-2 gather.  Weight gradients reduce over the M = B*H*W rows: a
+// workgroup owns a 64x64 (output channel, K) tile and a slice of rows, the slices' partials are
+// folded in a fixed order (bit-reproducible).  BN statistics and BN-backward sums are fp64 column
+// reductions over row blocks, folded in a fixed order.
+#include <algorithm>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "post.hpp"
+#include "unet.hpp"
+
+namespace phx {
+
+__device__ __forceinline__ float leaky(float x) { return x > 0.f ? x : 0.2f * x; }
+__device__ __forceinline__ float leaky_grad(float z) { return z > 0.f ? 1.f : 0.2f; }
+
+// ------------------------------------------------------------------------------------------
+// gathers
+// ------------------------------------------------------------------------------------------
+// mode 0: conv, out (oy, ox) tap (ky, kx) reads x[oy*s + ky - pt, ox*s + kx - pl]
+// mode 1: transposed conv (stride 2, TF 'same' = pads (0, 1) of the equivalent forward conv):
+//         out (oy, ox) tap (ky, kx) reads x[(oy - ky) / 2, (ox - kx) / 2] when both are even
+// col[m][k], k = (ky*3 + kx)*C + c, zero beyond 9C (K padded to Kp)
+__global__ __launch_bounds__(256) void k_im2col(const float* __restrict__ x, float* __restrict__ col, int B,
+                                                int H, int W, int C, int Ho, int Wo, int Kp, int mode,
+                                                int s, int pt, int pl) {
+  const long n = (long)B * Ho * Wo * Kp;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % Kp);
+    const long m = i / Kp;
+    float v = 0.f;
+    if (k < 9 * C) {
+      const int tap = k / C, c = k - tap * C;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      const int ox = (int)(m % Wo);
+      const long r = m / Wo;
+      const int oy = (int)(r % Ho);
+      const int b = (int)(r / Ho);
+      int iy, ix;
+      bool ok;
+      if (mode == 0) {
+        iy = oy * s + ky - pt;
+        ix = ox * s + kx - pl;
+        ok = true;
+      } else {
+        const int dy = oy - ky, dx = ox - kx;
+        ok = dy >= 0 && dx >= 0 && !(dy & 1) && !(dx & 1);
+        iy = dy >> 1;
+        ix = dx >> 1;
+      }
+      if (ok && iy >= 0 && iy < H && ix >= 0 && ix < W) v = x[(((long)b * H + iy) * W + ix) * C + c];
+    }
+    col[i] = v;
+  }
+}
+
+// derived weight matrices of the GEMMs (B operand [N][K]) from the Keras kernels
+//  kind 0: conv fwd      Bt[co][(ky,kx,ci)] = W[ky][kx][ci][co]
+//  kind 1: conv dgrad    Bt[ci][(ky,kx,co)] = W[2-ky][2-kx][ci][co]
+//  kind 2: tconv fwd     Bt[co][(ky,kx,ci)] = Wt[ky][kx][co][ci]
+//  kind 3: tconv dgrad   Bt[ci][(ky,kx,co)] = Wt[ky][kx][co][ci]
+//  kind 4: 1x1 fwd       Bt[co][ci] = W[ci][co];  kind 5: 1x1 dgrad Bt[ci][co] = W[ci][co]
+__global__ __launch_bounds__(256) void k_wprep(const float* __restrict__ w, float* __restrict__ bt, int kind,
+                                               int ci, int co, int Kp) {
+  const bool dg = kind == 1 || kind == 3 || kind == 5;
+  const int N = dg ? ci : co;
+  const int Kin = dg ? co : ci;  // channels along K
+  const int taps = kind >= 4 ? 1 : 9;
+  const long n = (long)N * Kp;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int nn = (int)(i / Kp), k = (int)(i % Kp);
+    float v = 0.f;
+    if (k < taps * Kin) {
+      const int tap = k / Kin, c = k - tap * Kin;
+      const int ky = tap / 3, kx = tap - ky * 3;
+      long src;
+      switch (kind) {
+        case 0: src = (((long)ky * 3 + kx) * ci + c) * co + nn; break;
+        case 1: src = (((long)(2 - ky) * 3 + (2 - kx)) * ci + nn) * co + c; break;
+        case 2: src = (((long)ky * 3 + kx) * co + nn) * ci + c; break;
+        case 3: src = (((long)ky * 3 + kx) * co + c) * ci + nn; break;
+        case 4: src = (long)c * co + nn; break;
+        default: src = (long)nn * co + c; break;
+      }
+      v = w[src];
+    }
+    bt[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight gradient: part[z][co][k] = sum over rows of slice z of dy[m][co] * col[m][k]
+// 64 x 64 tile per workgroup, 16 x 16 threads with 4 x 4 outputs each, 32-row chunks in LDS
+// ------------------------------------------------------------------------------------------
+constexpr int kWgT = 64, kWgR = 32;
+
+__global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dy, int ldy, const float* __restrict__ col,
+                                               int ldc, long M, int Co, int Kp, long rows_per_slice,
+                                               float* __restrict__ part) {
+  __shared__ float sd[kWgR][kWgT + 4], sc[kWgR][kWgT + 4];
+  const int co0 = blockIdx.x * kWgT, k0 = blockIdx.y * kWgT;
+  const long r0 = (long)blockIdx.z * rows_per_slice, r1 = min(M, r0 + rows_per_slice);
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+  float acc[4][4] = {};
+  for (long rb = r0; rb < r1; rb += kWgR) {
+    for (int e = threadIdx.x; e < kWgR * kWgT; e += 256) {
+      const int rr = e / kWgT, cc = e - rr * kWgT;
+      const long row = rb + rr;
+      const bool rok = row < r1;
+      sd[rr][cc] = (rok && co0 + cc < Co) ? dy[row * ldy + co0 + cc] : 0.f;
+      sc[rr][cc] = (rok && k0 + cc < Kp) ? col[row * ldc + k0 + cc] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int rr = 0; rr < kWgR; ++rr) {
+      float a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = sd[rr][ty * 4 + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = sc[rr][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  float* out = part + (long)blockIdx.z * Co * Kp;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + ty * 4 + i;
+    if (co >= Co) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + tx * 4 + j;
+      if (k < Kp) out[(long)co * Kp + k] = acc[i][j];
+    }
+  }
+}
+
+// fold the slices (fixed order) and scatter into the Keras kernel layout of the gradient
+//  kind 0: conv  [ky][kx][ci][co] from (co, (ky,kx,ci));  kind 2: tconv [ky][kx][co][ci];
+//  kind 4: 1x1 [ci][co]
+__global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ part, int nslice, int Co, int Kp,
+                                                    int Kin, int taps, int kind, float* __restrict__ g) {
+  const long n = (long)Co * taps * Kin;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i / ((long)taps * Kin));
+    const int k = (int)(i % ((long)taps * Kin));
+    float s = 0.f;
+    for (int z = 0; z < nslice; ++z) s += part[((long)z * Co + co) * Kp + k];
+    const int tap = k / Kin, c = k - tap * Kin;
+    long dst;
+    if (kind == 2) dst = ((long)tap * Co + co) * Kin + c;
+    else dst = ((long)tap * Kin + c) * Co + co;
+    g[dst] = s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fp64 column reductions over [M, C] (C <= 256): block z reduces its row range; thread t owns
+// channel t % C (threads past the last whole group of C idle), then thread c folds its group.  Modes:
+//   0 BN statistics: s0 = sum(y - y[0]), s1 = sum((y - y[0])^2)
+//   1 BN backward:   dz = da * act'(z), z = (y - mu) * sc + be; s0 = sum dz, s1 = sum dz * xhat
+//   2 column sums:   s0 = sum v
+// ------------------------------------------------------------------------------------------
+struct ColRed {
+  const float* y;   // BN input (modes 0, 1) or values (mode 2)
+  const float* da;  // mode 1: gradient of the activation output
+  const float* mu;
+  const float* rstd;
+  const float* sc;
+  const float* be;
+  int act;          // 1 leaky, 0 identity
+  int ld;           // row stride (floats)
+};
+
+__global__ __launch_bounds__(256) void k_colred64(ColRed r, long M, int C, long rows_per_block, int mode,
+                                                  double* __restrict__ part) {
+  __shared__ double s0s[256], s1s[256];
+  const int t = threadIdx.x, lane_rows = 256 / C, c = t % C, r_off = t / C;
+  const bool active = r_off < lane_rows;
+  const long r0 = (long)blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  const double shift = mode == 0 ? (double)r.y[c] : 0.0;
+  float mu = 0.f, rs = 0.f, scv = 0.f, be = 0.f;
+  if (mode == 1) {
+    mu = r.mu[c]; rs = r.rstd[c]; scv = r.sc[c]; be = r.be[c];
+  }
+  double a0 = 0.0, a1 = 0.0;
+  for (long row = r0 + r_off; active && row < r1; row += lane_rows) {
+    const float v = r.y[row * r.ld + c];
+    if (mode == 0) {
+      const double d = (double)v - shift;
+      a0 += d;
+      a1 += d * d;
+    } else if (mode == 1) {
+      const float yc = v - mu;
+      float dz = r.da[row * r.ld + c];
+      if (r.act) dz *= leaky_grad(yc * scv + be);
+      a0 += (double)dz;
+      a1 += (double)dz * (double)(yc * rs);
+    } else {
+      a0 += (double)v;
+    }
+  }
+  s0s[t] = a0;
+  s1s[t] = a1;
+  __syncthreads();
+  if (t < C) {
+    double b0 = 0.0, b1 = 0.0;
+    for (int j = 0; j < lane_rows; ++j) {
+      b0 += s0s[t + j * C];
+      b1 += s1s[t + j * C];
+    }
+    part[((long)blockIdx.x * C + t) * 2 + 0] = b0;
+    part[((long)blockIdx.x * C + t) * 2 + 1] = b1;
+  }
+}
+
+// BN statistics: mean / rstd / sc = gamma * rstd, moving statistics (momentum 0.99, Bessel)
+__global__ void k_un_bn_final(const double* __restrict__ part, int nblk, long M, int C,
+                              const float* __restrict__ y0, const float* __restrict__ gamma,
+                              float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ sc,
+                              float* __restrict__ mmean, float* __restrict__ mvar) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int z = 0; z < nblk; ++z) {
+    s0 += part[((long)z * C + c) * 2];
+    s1 += part[((long)z * C + c) * 2 + 1];
+  }
+  const double dm = s0 / (double)M;
+  double var = s1 / (double)M - dm * dm;
+  if (var < 0.0) var = 0.0;
+  const double mu = (double)y0[c] + dm;
+  const double rs = 1.0 / sqrt(var + 1e-3);
+  mean[c] = (float)mu;
+  rstd[c] = (float)rs;
+  sc[c] = (float)(rs * (double)gamma[c]);
+  if (mmean) {
+    const double uvar = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    mmean[c] = (float)(mmean[c] - (mmean[c] - mu) * 0.01);
+    mvar[c] = (float)(mvar[c] - (mvar[c] - uvar) * 0.01);
+  }
+}
+
+// BN backward: mean(dz), mean(dz*xhat); d gamma = sum dz*xhat, d beta = sum dz
+__global__ void k_un_bnb_final(const double* __restrict__ part, int nblk, long M, int C, float* __restrict__ mdz,
+                               float* __restrict__ mdzx, float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int z = 0; z < nblk; ++z) {
+    s0 += part[((long)z * C + c) * 2];
+    s1 += part[((long)z * C + c) * 2 + 1];
+  }
+  mdz[c] = (float)(s0 / (double)M);
+  mdzx[c] = (float)(s1 / (double)M);
+  dgamma[c] = (float)s1;
+  dbeta[c] = (float)s0;
+}
+
+// column sums (bias gradients)
+__global__ void k_un_colsum_final(const double* __restrict__ part, int nblk, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s0 = 0.0;
+  for (int z = 0; z < nblk; ++z) s0 += part[((long)z * C + c) * 2];
+  out[c] = (float)s0;
+}
+
+// ------------------------------------------------------------------------------------------
+// elementwise
+// ------------------------------------------------------------------------------------------
+// a = act((y - mu) * sc + be), act 1 = leaky
+__global__ __launch_bounds__(256) void k_un_bnact(const float* __restrict__ y, const float* __restrict__ mu,
+                                                  const float* __restrict__ sc, const float* __restrict__ be,
+                                                  float* __restrict__ a, long n, int C, int act) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float z = (y[i] - mu[c]) * sc[c] + be[c];
+    a[i] = act ? leaky(z) : z;
+  }
+}
+
+// dy = sc * (dz - mean dz - xhat * mean(dz xhat)), dz = da * act'(z)
+__global__ __launch_bounds__(256) void k_un_bnb_apply(const float* __restrict__ da, const float* __restrict__ y,
+                                                      const float* __restrict__ mu, const float* __restrict__ rstd,
+                                                      const float* __restrict__ sc, const float* __restrict__ be,
+                                                      const float* __restrict__ mdz, const float* __restrict__ mdzx,
+                                                      float* __restrict__ dy, long n, int C, int act) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float yc = y[i] - mu[c];
+    float dz = da[i];
+    if (act) dz *= leaky_grad(yc * sc[c] + be[c]);
+    dy[i] = sc[c] * (dz - mdz[c] - (yc * rstd[c]) * mdzx[c]);
+  }
+}
+
+// 2x2 max-pool (valid) + the winning tap (first maximum in row-major window order), then Dropout
+__global__ __launch_bounds__(256) void k_un_pool_drop(const float* __restrict__ x, float* __restrict__ out,
+                                                      uint8_t* __restrict__ arg, int B, int H, int W, int C,
+                                                      uint64_t seed, int64_t step, int gimg0, int layer) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long n = (long)B * Ho * Wo * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long p = i / C;
+    const int ox = (int)(p % Wo);
+    const long r = p / Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    const float* base = x + (((long)b * H + 2 * oy) * W + 2 * ox) * C + c;
+    float m = base[0];
+    int am = 0;
+    const float v1 = base[C], v2 = base[(long)W * C], v3 = base[(long)W * C + C];
+    if (v1 > m) { m = v1; am = 1; }
+    if (v2 > m) { m = v2; am = 2; }
+    if (v3 > m) { m = v3; am = 3; }
+    arg[i] = (uint8_t)am;
+    const long e = i - (long)b * Ho * Wo * C;  // element index within the image
+    const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
+                                        (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+    out[i] = u01(q.x) >= 0.2f ? (m * 1.25f) : 0.f;
+  }
+}
+
+// backward of pool + dropout: dx (the whole input, zeros off the winning taps) [+= when acc]
+__global__ __launch_bounds__(256) void k_un_pool_drop_bwd(const float* __restrict__ dout,
+                                                          const uint8_t* __restrict__ arg, float* __restrict__ dx,
+                                                          int B, int H, int W, int C, uint64_t seed, int64_t step,
+                                                          int gimg0, int layer, int acc) {
+  const int Ho = H / 2, Wo = W / 2;
+  const long n = (long)B * Ho * Wo * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long p = i / C;
+    const int ox = (int)(p % Wo);
+    const long r = p / Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    const long e = i - (long)b * Ho * Wo * C;
+    const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
+                                        (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+    const float g = u01(q.x) >= 0.2f ? dout[i] * 1.25f : 0.f;
+    const int am = arg[i];
+    float* base = dx + (((long)b * H + 2 * oy) * W + 2 * ox) * C + c;
+    const long off[4] = {0, C, (long)W * C, (long)W * C + C};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float v = k == am ? g : 0.f;
+      if (acc) base[off[k]] += v;
+      else base[off[k]] = v;
+    }
+  }
+}
+
+// attention, forward part 1: s = leaky(bn1(g) + bn2(x))  (the BN outputs are never stored)
+__global__ __launch_bounds__(256) void k_att_s(const float* __restrict__ g, const float* __restrict__ x,
+                                               const float* __restrict__ mu1, const float* __restrict__ sc1,
+                                               const float* __restrict__ be1, const float* __restrict__ mu2,
+                                               const float* __restrict__ sc2, const float* __restrict__ be2,
+                                               float* __restrict__ s, long n, int C) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float zg = (g[i] - mu1[c]) * sc1[c] + be1[c];
+    const float zx = (x[i] - mu2[c]) * sc2[c] + be2[c];
+    s[i] = leaky(zg + zx);
+  }
+}
+
+// t[m] = sum_c s[m][c] * w[c] + b  (the attention's 1-channel 1x1 conv)
+__global__ __launch_bounds__(256) void k_att_t(const float* __restrict__ s, const float* __restrict__ w,
+                                               const float* __restrict__ b, float* __restrict__ t, long M, int C) {
+  for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) acc = fmaf(s[m * C + c], w[c], acc);
+    t[m] = acc + b[0];
+  }
+}
+
+// attention, forward part 2 + concat + Dropout: a = sigmoid(bn3(t)); cat = [up, skip * a] (2C
+// channels) times the Dropout mask of layer `layer`
+__global__ __launch_bounds__(256) void k_att_cat(const float* __restrict__ up, const float* __restrict__ skip,
+                                                 const float* __restrict__ t, const float* __restrict__ mu3,
+                                                 const float* __restrict__ sc3, const float* __restrict__ be3,
+                                                 float* __restrict__ cat, int B, long HW, int C, uint64_t seed,
+                                                 int64_t step, int gimg0, int layer) {
+  const long n = (long)B * HW * 2 * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c2 = (int)(i % (2 * C));
+    const long m = i / (2 * C);
+    float v;
+    if (c2 < C) {
+      v = up[m * C + c2];
+    } else {
+      const float z = (t[m] - mu3[0]) * sc3[0] + be3[0];
+      const float a = 1.0f / (1.0f + expf(-z));
+      v = skip[m * C + c2 - C] * a;
+    }
+    const int b = (int)(m / HW);
+    const long e = i - (long)b * HW * 2 * C;
+    const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
+                                        (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+    cat[i] = u01(q.x) >= 0.2f ? v * 1.25f : 0.f;
+  }
+}
+
+// backward of k_att_cat: dup = dcat[:, :C] (masked), dskip_direct = dcat[:, C:] * a, and per row
+// dz3 = (sum_c dcat[:, C + c] * skip) * a (1 - a)  (the gradient of bn3's output)
+__global__ __launch_bounds__(256) void k_att_cat_bwd(const float* __restrict__ dcat, const float* __restrict__ skip,
+                                                     const float* __restrict__ t, const float* __restrict__ mu3,
+                                                     const float* __restrict__ sc3, const float* __restrict__ be3,
+                                                     float* __restrict__ dup, float* __restrict__ dskip,
+                                                     float* __restrict__ dz3, int B, long HW, int C, uint64_t seed,
+                                                     int64_t step, int gimg0, int layer) {
+  const long M = (long)B * HW;
+  for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(m / HW);
+    const float z = (t[m] - mu3[0]) * sc3[0] + be3[0];
+    const float a = 1.0f / (1.0f + expf(-z));
+    float da = 0.f;
+    for (int c2 = 0; c2 < 2 * C; ++c2) {
+      const long i = m * 2 * C + c2;
+      const long e = i - (long)b * HW * 2 * C;
+      const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
+                                          (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
+                                    (uint32_t)seed, (uint32_t)(seed >> 32));
+      const float g = u01(q.x) >= 0.2f ? dcat[i] * 1.25f : 0.f;
+      if (c2 < C) {
+        dup[m * C + c2] = g;
+      } else {
+        const float sk = skip[m * C + c2 - C];
+        dskip[m * C + c2 - C] = g * a;
+        da = fmaf(g, sk, da);
+      }
+    }
+    dz3[m] = da * (a * (1.0f - a));
+  }
+}
+
+// d(pre-leaky sum) of the attention: ds[m][c] = dt[m] * w3[c] * leaky'(bn1(g) + bn2(x))
+__global__ __launch_bounds__(256) void k_att_s_bwd(const float* __restrict__ dt, const float* __restrict__ w3,
+                                                   const float* __restrict__ g, const float* __restrict__ x,
+                                                   const float* __restrict__ mu1, const float* __restrict__ sc1,
+                                                   const float* __restrict__ be1, const float* __restrict__ mu2,
+                                                   const float* __restrict__ sc2, const float* __restrict__ be2,
+                                                   float* __restrict__ dsum, long n, int C) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long m = i / C;
+    const float zg = (g[i] - mu1[c]) * sc1[c] + be1[c];
+    const float zx = (x[i] - mu2[c]) * sc2[c] + be2[c];
+    dsum[i] = dt[m] * w3[c] * leaky_grad(zg + zx);
+  }
+}
+
+// output layer + loss: o = tanh(x W + b) (1x1, C -> 3), u = 2 o, per image mean((t - u)^2);
+// dz = d loss / d(x W + b) = -2 (t - u) / (HW*3) * 2 * (1 - o^2); partial loss per block (fp64)
+__global__ __launch_bounds__(256) void k_un_out_loss(const float* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ bias, const float* __restrict__ tgt,
+                                                     float* __restrict__ upd, float* __restrict__ dz,
+                                                     double* __restrict__ lpart, long M, long HW, int C) {
+  __shared__ double sh[256];
+  double acc = 0.0;
+  const float inv = 1.0f / (float)(HW * 3);
+  for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float z = bias[o];
+      for (int c = 0; c < C; ++c) z = fmaf(x[m * C + c], w[c * 3 + o], z);
+      const float th = tanhf(z);
+      const float u = 2.0f * th;
+      const float d = tgt[m * 3 + o] - u;
+      acc += (double)d * (double)d;
+      upd[m * 3 + o] = u;
+      dz[m * 3 + o] = (-2.0f * d * inv) * 2.0f * (1.0f - th * th);
+    }
+  }
+  sh[threadIdx.x] = acc / (double)(HW * 3);
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) lpart[blockIdx.x] = sh[0];
+}
+
+__global__ void k_un_loss_final(const double* __restrict__ lpart, int n, float* __restrict__ out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) s += lpart[i];
+  out[0] = (float)s;
+}
+
+// dx[m][c] = sum_o dz[m][o] * w[c][o]  (+= when acc): the data gradient of a 1x1 conv with few outputs
+__global__ __launch_bounds__(256) void k_un_small_dgrad(const float* __restrict__ dz, const float* __restrict__ w,
+                                                        float* __restrict__ dx, long M, int C, int O, int acc) {
+  const long n = M * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long m = i / C;
+    float v = 0.f;
+    for (int o = 0; o < O; ++o) v = fmaf(dz[m * O + o], w[c * O + o], v);
+    if (acc) dx[i] += v;
+    else dx[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_un_add(float* __restrict__ a, const float* __restrict__ b, long n) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) a[i] += b[i];
+}
+
+// ------------------------------------------------------------------------------------------
+// Masker extras
+// ------------------------------------------------------------------------------------------
+// per target image b: source image perm[b] (tf.random.shuffle: ranks of one Philox key per image,
+// ties by index) and its left-right / up-down flips (flip when u01 >= 0.5); one workgroup
+__global__ void k_def_perm(int B, uint64_t seed, int64_t step, int gimg0, int* __restrict__ info) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    // the image whose key has rank b
+    int src = 0;
+    for (int j = 0; j < B; ++j) {
+      const uint32_t kj = philox4x32_10(u32x4{0u, 0u, (uint32_t)(gimg0 + j), (uint32_t)((uint64_t)step << 8) | RNG_DSHUF},
+                                        (uint32_t)seed, (uint32_t)(seed >> 32)).x;
+      int rank = 0;
+      for (int i = 0; i < B; ++i) {
+        const uint32_t ki = philox4x32_10(u32x4{0u, 0u, (uint32_t)(gimg0 + i), (uint32_t)((uint64_t)step << 8) | RNG_DSHUF},
+                                          (uint32_t)seed, (uint32_t)(seed >> 32)).x;
+        rank += (ki < kj || (ki == kj && i < j)) ? 1 : 0;
+      }
+      if (rank == b) src = j;
+    }
+    const u32x4 f = philox4x32_10(u32x4{0u, 0u, (uint32_t)(gimg0 + b), (uint32_t)((uint64_t)step << 8) | RNG_DFLIP},
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+    info[b * 3 + 0] = src;
+    info[b * 3 + 1] = u01(f.x) >= 0.5f ? 1 : 0;
+    info[b * 3 + 2] = u01(f.y) >= 0.5f ? 1 : 0;
+  }
+}
+
+// patches[b] = flips(images[perm[b], :P, :P])
+__global__ __launch_bounds__(256) void k_def_crops(const float* __restrict__ images, const int* __restrict__ info,
+                                                   float* __restrict__ out, int B, int H, int W, int P) {
+  const long n = (long)B * P * P;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int x = (int)(i % P);
+    const long r = i / P;
+    const int y = (int)(r % P);
+    const int b = (int)(r / P);
+    const int src = info[b * 3], lr = info[b * 3 + 1], ud = info[b * 3 + 2];
+    const int sy = ud ? P - 1 - y : y, sx = lr ? P - 1 - x : x;
+    const float* s = images + (((long)src * H + sy) * W + sx) * 3;
+    float* o = out + i * 3;
+    o[0] = s[0];
+    o[1] = s[1];
+    o[2] = s[2];
+  }
+}
+
+// odet_model's filter_valid_boxes after NMS (attack_detection.py:79-94, 121-125): keep boxes with
+// w / W <= 1, h / H <= 1, area > 100 and score >= thresh, in order
+__global__ void k_def_filter(const float* __restrict__ nb, const float* __restrict__ ns, const int* __restrict__ nc,
+                             int B, int maxo, float Hf, float Wf, float thresh, float* __restrict__ ob,
+                             int* __restrict__ oc) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  int k = 0;
+  for (int i = 0; i < nc[b]; ++i) {
+    const float* bx = nb + ((long)b * maxo + i) * 4;
+    const float h = bx[2] - bx[0], w = bx[3] - bx[1];
+    const bool ok = (w / Wf <= 1.0f) && (h / Hf <= 1.0f) && (h * w > 100.0f) && ns[(long)b * maxo + i] >= thresh;
+    if (ok) {
+      float* o = ob + ((long)b * maxo + k) * 4;
+      o[0] = bx[0]; o[1] = bx[1]; o[2] = bx[2]; o[3] = bx[3];
+      ++k;
+    }
+  }
+  oc[b] = k;
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+static dim3 grid_for(long n) { return dim3((unsigned)std::min<long>(std::max<long>(cdiv(n, 256), 1), 8192)); }
+
+void un_im2col(const float* x, float* col, int B, int H, int W, int C, int Ho, int Wo, int Kp, int mode, int s,
+               int pt, int pl, hipStream_t st) {
+  hipLaunchKernelGGL(k_im2col, grid_for((long)B * Ho * Wo * Kp), dim3(256), 0, st, x, col, B, H, W, C, Ho, Wo, Kp,
+                     mode, s, pt, pl);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_wprep(const float* w, float* bt, int kind, int ci, int co, int Kp, hipStream_t st) {
+  const bool dg = kind == 1 || kind == 3 || kind == 5;
+  hipLaunchKernelGGL(k_wprep, grid_for((long)(dg ? ci : co) * Kp), dim3(256), 0, st, w, bt, kind, ci, co, Kp);
+  PHX_LAUNCH_CHECK();
+}
+
+int un_wgrad_slices(long M) { return (int)std::min<long>(std::max<long>(cdiv(M, 2048), 1), 256); }
+
+void un_wgrad(const float* dy, int ldy, const float* col, int ldc, long M, int Co, int Kp, int Kin, int taps,
+              int kind, float* part, float* g, hipStream_t st) {
+  const int ns = un_wgrad_slices(M);
+  const long rps = (M + ns - 1) / ns;
+  hipLaunchKernelGGL(k_wgrad, dim3(cdiv(Co, kWgT), cdiv(Kp, kWgT), ns), dim3(256), 0, st, dy, ldy, col, ldc, M, Co,
+                     Kp, rps, part);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_wgrad_fold, grid_for((long)Co * taps * Kin), dim3(256), 0, st, part, ns, Co, Kp, Kin, taps,
+                     kind, g);
+  PHX_LAUNCH_CHECK();
+}
+
+int un_colred_blocks(long M) { return (int)std::min<long>(std::max<long>(cdiv(M, 1024), 1), 1024); }
+
+static void colred(const ColRed& r, long M, int C, int mode, double* part, int* nblk, hipStream_t st) {
+  if (C < 1 || C > 256) throw std::runtime_error("unet column reduction: C must be in [1, 256]");
+  const int nb = un_colred_blocks(M);
+  const long rpb = (M + nb - 1) / nb;
+  hipLaunchKernelGGL(k_colred64, dim3(nb), dim3(256), 0, st, r, M, C, rpb, mode, part);
+  PHX_LAUNCH_CHECK();
+  *nblk = nb;
+}
+
+void un_bn_stats(const float* y, long M, int C, const float* gamma, float* mean, float* rstd, float* sc,
+                 float* mmean, float* mvar, double* part, hipStream_t st) {
+  ColRed r{y, nullptr, nullptr, nullptr, nullptr, nullptr, 0, C};
+  int nb;
+  colred(r, M, C, 0, part, &nb, st);
+  hipLaunchKernelGGL(k_un_bn_final, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nb, M, C, y, gamma, mean, rstd, sc,
+                     mmean, mvar);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_bn_bwd(const float* da, const float* y, long M, int C, const float* mu, const float* rstd, const float* sc,
+               const float* be, int act, float* mdz, float* mdzx, float* dgamma, float* dbeta, float* dy,
+               double* part, hipStream_t st) {
+  ColRed r{y, da, mu, rstd, sc, be, act, C};
+  int nb;
+  colred(r, M, C, 1, part, &nb, st);
+  hipLaunchKernelGGL(k_un_bnb_final, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nb, M, C, mdz, mdzx, dgamma, dbeta);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_un_bnb_apply, grid_for(M * C), dim3(256), 0, st, da, y, mu, rstd, sc, be, mdz, mdzx, dy, M * C,
+                     C, act);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_colsum(const float* v, long M, int C, float* out, double* part, hipStream_t st) {
+  ColRed r{v, nullptr, nullptr, nullptr, nullptr, nullptr, 0, C};
+  int nb;
+  colred(r, M, C, 2, part, &nb, st);
+  hipLaunchKernelGGL(k_un_colsum_final, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nb, C, out);
+  PHX_LAUNCH_CHECK();
+}
+
+size_t un_colred_doubles(long M, int C) { return (size_t)un_colred_blocks(M) * C * 2; }
+
+void un_bnact(const float* y, const float* mu, const float* sc, const float* be, float* a, long M, int C, int act,
+              hipStream_t st) {
+  hipLaunchKernelGGL(k_un_bnact, grid_for(M * C), dim3(256), 0, st, y, mu, sc, be, a, M * C, C, act);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_pool_drop(const float* x, float* out, uint8_t* arg, int B, int H, int W, int C, uint64_t seed, int64_t step,
+                  int gimg0, int layer, hipStream_t st) {
+  hipLaunchKernelGGL(k_un_pool_drop, grid_for((long)B * (H / 2) * (W / 2) * C), dim3(256), 0, st, x, out, arg, B, H, W,
+                     C, seed, step, gimg0, layer);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_pool_drop_bwd(const float* dout, const uint8_t* arg, float* dx, int B, int H, int W, int C, uint64_t seed,
+                      int64_t step, int gimg0, int layer, bool acc, hipStream_t st) {
+  hipLaunchKernelGGL(k_un_pool_drop_bwd, grid_for((long)B * (H / 2) * (W / 2) * C), dim3(256), 0, st, dout, arg, dx, B,
+                     H, W, C, seed, step, gimg0, layer, acc ? 1 : 0);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_att_s(const float* g, const float* x, const float* mu1, const float* sc1, const float* be1, const float* mu2,
+              const float* sc2, const float* be2, float* s, long M, int C, hipStream_t st) {
+  hipLaunchKernelGGL(k_att_s, grid_for(M * C), dim3(256), 0, st, g, x, mu1, sc1, be1, mu2, sc2, be2, s, M * C, C);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_att_t(const float* s, const float* w, const float* b, float* t, long M, int C, hipStream_t st) {
+  hipLaunchKernelGGL(k_att_t, grid_for(M), dim3(256), 0, st, s, w, b, t, M, C);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_att_cat(const float* up, const float* skip, const float* t, const float* mu3, const float* sc3,
+                const float* be3, float* cat, int B, long HW, int C, uint64_t seed, int64_t step, int gimg0, int layer,
+                hipStream_t st) {
+  hipLaunchKernelGGL(k_att_cat, grid_for((long)B * HW * 2 * C), dim3(256), 0, st, up, skip, t, mu3, sc3, be3, cat, B,
+                     HW, C, seed, step, gimg0, layer);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_att_cat_bwd(const float* dcat, const float* skip, const float* t, const float* mu3, const float* sc3,
+                    const float* be3, float* dup, float* dskip, float* dz3, int B, long HW, int C, uint64_t seed,
+                    int64_t step, int gimg0, int layer, hipStream_t st) {
+  hipLaunchKernelGGL(k_att_cat_bwd, grid_for((long)B * HW), dim3(256), 0, st, dcat, skip, t, mu3, sc3, be3, dup, dskip,
+                     dz3, B, HW, C, seed, step, gimg0, layer);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_att_s_bwd(const float* dt, const float* w3, const float* g, const float* x, const float* mu1,
+                  const float* sc1, const float* be1, const float* mu2, const float* sc2, const float* be2,
+                  float* dsum, long M, int C, hipStream_t st) {
+  hipLaunchKernelGGL(k_att_s_bwd, grid_for(M * C), dim3(256), 0, st, dt, w3, g, x, mu1, sc1, be1, mu2, sc2, be2, dsum,
+                     M * C, C);
+  PHX_LAUNCH_CHECK();
+}
+
+int un_loss_blocks(long M) { return (int)std::min<long>(cdiv(M, 256), 1024); }
+
+void un_out_loss(const float* x, const float* w, const float* b, const float* tgt, float* upd, float* dz,
+                 double* lpart, float* loss, long M, long HW, int C, hipStream_t st) {
+  const int nb = un_loss_blocks(M);
+  hipLaunchKernelGGL(k_un_out_loss, dim3(nb), dim3(256), 0, st, x, w, b, tgt, upd, dz, lpart, M, HW, C);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_un_loss_final, dim3(1), dim3(64), 0, st, lpart, nb, loss);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_small_dgrad(const float* dz, const float* w, float* dx, long M, int C, int O, bool acc, hipStream_t st) {
+  hipLaunchKernelGGL(k_un_small_dgrad, grid_for(M * C), dim3(256), 0, st, dz, w, dx, M, C, O, acc ? 1 : 0);
+  PHX_LAUNCH_CHECK();
+}
+
+void un_add(float* a, const float* b, long n, hipStream_t st) {
+  hipLaunchKernelGGL(k_un_add, grid_for(n), dim3(256), 0, st, a, b, n);
+  PHX_LAUNCH_CHECK();
+}
+
+void def_perm_crops(const float* images, int* info, float* crops, int B, int H, int W, int P, uint64_t seed,
+                    int64_t step, int gimg0, hipStream_t st) {
+  hipLaunchKernelGGL(k_def_perm, dim3(1), dim3(256), 0, st, B, seed, step, gimg0, info);
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_def_crops, grid_for((long)B * P * P), dim3(256), 0, st, images, info, crops, B, H, W, P);
+  PHX_LAUNCH_CHECK();
+}
+
+void def_filter(const float* nb, const float* ns, const int* nc, int B, int maxo, float H, float W, float thresh,
+                float* ob, int* oc, hipStream_t st) {
+  hipLaunchKernelGGL(k_def_filter, dim3(cdiv(B, 64)), dim3(64), 0, st, nb, ns, nc, B, maxo, H, W, thresh, ob, oc);
+  PHX_LAUNCH_CHECK();
+}
+
+}  // namespace phx

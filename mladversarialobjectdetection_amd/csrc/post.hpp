@@ -54,21 +54,34 @@ struct EotDims {
   long rcap;          // R storage capacity (floats)
 };
 
+// placement rule: the attacker's Patcher.create (attacker.py:448-488: centre tolerance 0.2, the
+// trained scale params[NPATCH]) or the defender's Masker.create in training (attack_detection.py:
+// 450-483: tolerance 0.5, scale U(0.3, 0.5) per box)
+struct PlaceRule {
+  float tol = 0.2f;
+  int random_scale = 0;
+  float scale_lo = 0.f, scale_hi = 0.f;
+};
 // placement + per-image print parameters (+ R offsets).  boxes [B,maxb,4], count [B].
 void launch_eot_place(const EotDims& d, const float* boxes, const int* count, const float* params,
                       uint64_t seed, int64_t step, int gimg0, ImgParams* img, BoxPlace* place,
-                      SpanEntry* spans, int* err, hipStream_t s);
+                      SpanEntry* spans, int* err, hipStream_t s, PlaceRule rule = PlaceRule{});
 // brightness matcher: out[b] = match(print(patch, img[b]), tgt[b]); mean scratch doubles [B*2*64]
 void launch_eot_match(const EotDims& d, const float* patch, const ImgParams* img, const float* tgt,
                       float* matched, double* ysum, float* ymean, bool apply_print,
                       hipStream_t s);
-// per box: pre = resize(matched[b]) + noise + delta  (pre-clip values)
+// brightness matcher over one printed source per image (the defender's Masker: src [B,P,P,3])
+void launch_eot_match_batch(const EotDims& d, const float* src, const ImgParams* img, const float* tgt,
+                            float* matched, double* ysum, float* ymean, hipStream_t s);
+// per box: pre = resize(matched[b]) + U(-amp, amp) noise + delta  (pre-clip values)
 void launch_eot_resize(const EotDims& d, const float* matched, const BoxPlace* place,
                        const SpanEntry* spans, uint64_t seed, int64_t step, int gimg0,
-                       float* rstore, hipStream_t s);
-// composite: out = paste of every valid box, owner map for the gradient
+                       float* rstore, hipStream_t s, float noise_amp = 0.01f);
+// composite: out = paste of every valid box, owner map for the gradient; mask (optional, the
+// defender's target): img_in - out on every pixel some box's region covers, 0 elsewhere
 void launch_eot_composite(const EotDims& d, const float* img_in, const BoxPlace* place,
-                          const float* rstore, float* img_out, int16_t* owner, hipStream_t s);
+                          const float* rstore, float* img_out, int16_t* owner, hipStream_t s,
+                          float* mask = nullptr);
 // backward: dR (pre-clip) per box from dimg via TF's inverse-warp rotation gradient
 void launch_eot_rot_bwd(const EotDims& d, const float* dimg, const int16_t* owner,
                         const BoxPlace* place, const float* rstore, float* dstore,
@@ -89,5 +102,7 @@ void launch_eot_count(const EotDims& d, const BoxPlace* place, float* metrics, h
 // Adam + clip constraints
 void launch_adam_clip(float* params, const float* grad, float* m, float* v, long n, float lr,
                       int64_t t, hipStream_t s);
+// plain Keras Adam (no constraints): the defender's U-Net variables
+void launch_adam(float* params, const float* grad, float* m, float* v, long n, float lr, int64_t t, hipStream_t s);
 
 }  // namespace phx

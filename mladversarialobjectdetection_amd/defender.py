@@ -1,0 +1,174 @@
+"""Mirror of the reference's defender (attack_detection.PatchAttackDefender + generator.PatchNeutralizer)
+over libphx: the U-Net variables and Adam state are caller-owned device tensors, every step runs in
+the HIP library (phx_def_step_grad), and data parallelism is one SUM all-reduce of
+[d variables | loss] per step (torch.distributed, RCCL on ROCm).
+
+  PatchAttackDefender.__init__  attack_detection.py:34-71 (U-Net built at the protege's image size)
+  PatchAttackDefender.call      attack_detection.py:168-206 (training=True)
+  PatchAttackDefender.train_step attack_detection.py:327-336
+  generator.define_model        generator.py:269-281 (Keras initialisers restated in numpy)
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import distributed as ddp
+from .attacker import EfficientDetVictim, _pad_boxes, _stream
+
+
+def _fans(shape, transpose=False):
+    """keras compute_fans for a conv kernel [k, k, a, b]: fan_in = k*k*a, fan_out = k*k*b."""
+    rf = int(np.prod(shape[:-2])) if len(shape) > 2 else 1
+    return shape[-2] * rf, shape[-1] * rf
+
+
+def init_unet_params(manifest: dict, seed: int = 0) -> np.ndarray:
+    """generator.py initialisers: he_normal (truncated normal, stddev sqrt(2 / fan_in) / .87962566)
+    for the encoder / decoder 3x3 convs, the transposed convs and the output conv; glorot_uniform for
+    the attention 1x1 convs (Keras default); zero biases; BN gamma 1, beta 0."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros(manifest["n_params"], np.float32)
+    for p in manifest["params"]:
+        name, shape, off = p["name"], tuple(p["shape"]), p["offset"]
+        n = int(np.prod(shape))
+        if name.endswith("/kernel"):
+            fan_in, fan_out = _fans(shape)
+            if "/attention/" in name:
+                lim = np.sqrt(6.0 / (fan_in + fan_out))
+                v = rng.uniform(-lim, lim, n)
+            else:
+                sd = np.sqrt(2.0 / fan_in) / 0.87962566103423978
+                v = rng.standard_normal(n)
+                bad = np.abs(v) > 2.0
+                while bad.any():
+                    v[bad] = rng.standard_normal(int(bad.sum()))
+                    bad = np.abs(v) > 2.0
+                v = v * sd
+            out[off:off + n] = v.astype(np.float32)
+        elif name.endswith("/gamma"):
+            out[off:off + n] = 1.0
+    return out
+
+
+class PatchAttackDefender:
+    """attack_detection.PatchAttackDefender (training path): the protege is frozen (inference BN),
+    the trainable variables are the U-Net's."""
+
+    def __init__(self, protege_model: EfficientDetVictim, initial_weights=None, protege_config_override=None, *,
+                 seed=0, learning_rate=1e-2, max_batch=None, device=None):
+        self.protege_model = protege_model
+        self.config = protege_model.config
+        if protege_config_override:
+            self.config.override(protege_config_override, protege_model.ctx)
+        dev = torch.device("cuda", protege_model.device) if device is None else torch.device(device)
+        self.handle = _lib.Defender(protege_model.ctx, max_batch or protege_model.max_batch, seed)
+        self.manifest = self.handle.manifest()
+        n = self.handle.num_params
+        if initial_weights is None:
+            init = init_unet_params(self.manifest, seed)
+        elif isinstance(initial_weights, (str, os.PathLike)):
+            init = self._read_npz(initial_weights)
+        else:
+            init = np.asarray(initial_weights, np.float32).reshape(-1)
+        if init.size != n:
+            raise ValueError(f"U-Net variables: {init.size} floats, manifest needs {n}")
+        self.params = torch.as_tensor(init, device=dev).contiguous()
+        # [d variables | loss]: the step's one SUM all-reduce
+        self._red = torch.zeros(n + 1, device=dev)
+        self.grad = self._red[:n]
+        self.loss_buf = self._red[n:]
+        self.m = torch.zeros_like(self.params)
+        self.v = torch.zeros_like(self.params)
+        self.learning_rate = learning_rate
+        self.iterations = 0
+        self.cur_step = 0
+
+    @property
+    def _trainable_variables(self):
+        return {p["name"]: self.params[p["offset"]:p["offset"] + int(np.prod(p["shape"]))].view(*p["shape"])
+                for p in self.manifest["params"]}
+
+    def moving_statistics(self) -> np.ndarray:
+        out = np.empty(self.handle.num_moving, np.float32)
+        self.handle.call("phx_def_moving", out.ctypes.data, None, None)
+        return out
+
+    def call(self, images, *, training=True, boxes=None):
+        """PatchAttackDefender.call(images, training=True) (attack_detection.py:168-206): returns the
+        gradient of the loss w.r.t. the U-Net variables (flat, manifest order); the loss of the step is
+        left in loss_buf.  `boxes` optionally replaces the first pass's detections for placement."""
+        if not training:
+            raise NotImplementedError("the defender's evaluation path (adversarial eval patch) is not built")
+        images = self.protege_model._check_images(images)
+        B = images.shape[0]
+        if boxes is not None:
+            bx, cnt = _pad_boxes(boxes, B, images.device)
+            if bx.shape[1] != _lib.MAX_OUT:
+                pad = torch.zeros(B, _lib.MAX_OUT, 4, device=images.device)
+                pad[:, :bx.shape[1]] = bx
+                bx = pad.contiguous()
+            self._keep = (bx, cnt)
+            bp, cp = bx.data_ptr(), cnt.data_ptr()
+        else:
+            bp = cp = None
+        self.handle.call("phx_def_step_grad", images.data_ptr(), B, bp, cp, self.params.data_ptr(),
+                         self._red.data_ptr(), int(self.cur_step), ddp.global_offset(B), _stream())
+        return self.grad
+
+    __call__ = call
+
+    def apply_gradients(self):
+        """Keras Adam (defender_train.py:35, lr 1e-2), no constraints."""
+        self.iterations += 1
+        rc = self.handle.lib.phx_adam(self.params.data_ptr(), self.grad.data_ptr(), self.m.data_ptr(),
+                                      self.v.data_ptr(), self.params.numel(), float(self.learning_rate),
+                                      int(self.iterations), _stream())
+        if rc != 0:
+            raise _lib.PhxError(f"phx_adam failed ({rc})")
+
+    def train_step(self, inputs, boxes=None):
+        """attack_detection.py:327-336: grads = self(inputs); apply_gradients.  Returns the loss as a
+        device scalar (reading it synchronises)."""
+        self.call(inputs, boxes=boxes)
+        ddp.allreduce_sum_(self._red)
+        self.apply_gradients()
+        self.cur_step += 1
+        return {"loss": self.loss_buf[0]}
+
+    def debug(self, what: int, B: int):
+        S = self.protege_model.ctx.image_size
+        shape = {_lib.DEF_PATCHED: (B, S, S, 3), _lib.DEF_TARGETS: (B, S, S, 3), _lib.DEF_UPDATES: (B, S, S, 3),
+                 _lib.DEF_BOXES: (B, _lib.MAX_OUT, 4), _lib.DEF_COUNTS: (B,)}[what]
+        out = torch.empty(shape, device=self.params.device)
+        self.handle.call("phx_def_debug", int(what), out.data_ptr(), out.numel(), _stream())
+        if what == _lib.DEF_COUNTS:
+            return out.view(torch.int32)
+        return out
+
+    def save_weights(self, dirpath, **kwargs):
+        """attack_detection.py:300-308 saves antipatch.h5; h5py is not available here, so the same
+        variables go to antipatch.npz under their Keras names (plus the BN moving statistics)."""
+        os.makedirs(dirpath)
+        arrs = {k: v.detach().cpu().numpy() for k, v in self._trainable_variables.items()}
+        mv = self.moving_statistics()
+        for b in self.manifest["bn"]:
+            arrs[b["name"] + "/moving_mean"] = mv[b["moving_mean"]:b["moving_mean"] + b["channels"]]
+            arrs[b["name"] + "/moving_variance"] = mv[b["moving_variance"]:b["moving_variance"] + b["channels"]]
+        np.savez(os.path.join(dirpath, "antipatch.npz"), **arrs)
+
+    def _read_npz(self, path):
+        p = os.path.join(path, "antipatch.npz") if os.path.isdir(path) else path
+        z = np.load(p)
+        out = np.zeros(self.handle.num_params, np.float32)
+        for q in self.manifest["params"]:
+            out[q["offset"]:q["offset"] + int(np.prod(q["shape"]))] = z[q["name"]].reshape(-1)
+        mv = np.zeros(self.handle.num_moving, np.float32)
+        for b in self.manifest["bn"]:
+            mv[b["moving_mean"]:b["moving_mean"] + b["channels"]] = z[b["name"] + "/moving_mean"]
+            mv[b["moving_variance"]:b["moving_variance"] + b["channels"]] = z[b["name"] + "/moving_variance"]
+        self.handle.call("phx_def_moving", None, mv.ctypes.data, None)
+        return out
