@@ -234,7 +234,7 @@ void phx_def::workspace(int B) {
   bt = F(nbt);
   size_t maxMC = 0, maxcol = 0, maxpart = 1, maxw = 1, maxcr = 1;
   auto note_gemm = [&](long M, int N, int K) { maxpart = std::max(maxpart, gemm_partial_floats((int)M, N, K)); };
-  auto note_w = [&](long M, int Co, int Kp) { maxw = std::max(maxw, (size_t)un_wgrad_slices(M) * Co * Kp); };
+  auto note_w = [&](long M, int Co, int Kp) { maxw = std::max(maxw, (size_t)un_wgrad_slices(M, Co, Kp) * Co * Kp); };
   auto note_cr = [&](long M, int C) { maxcr = std::max(maxcr, un_colred_doubles(M, C)); };
   auto note_conv = [&](const UConv& c, long M_out, long M_in) {
     maxcol = std::max(maxcol, (size_t)std::max(M_out * c.kp_f, M_in * (long)c.kp_d));
@@ -357,6 +357,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   // ---- U-Net forward ----
   auto conv3_fwd = [&](const float* x, int H, const UConv& c, float* y) {
     const long M = (long)B * H * H;
+    if (un_conv3_small(x, bt + c.bt_f, W + c.b, y, B, H, H, c.ci, H, H, c.co, c.kp_f, 0, 1, 1, 1, s)) return;
     un_im2col(x, col, B, H, H, c.ci, H, H, c.kp_f, 0, 1, 1, 1, s);
     gemm(col, bt + c.bt_f, W + c.b, y, M, c.co, c.kp_f, false, gpart, s);
   };
@@ -388,8 +389,10 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     const UConv& up = convs[a.up];
     const int n = up.co;
     DecT& d = dt[i];
-    un_im2col(x, col, B, hin, hin, up.ci, H, H, up.kp_f, 1, 2, 0, 0, s);
-    gemm(col, bt + up.bt_f, W + up.b, d.up, M, n, up.kp_f, false, gpart, s);
+    if (!un_conv3_small(x, bt + up.bt_f, W + up.b, d.up, B, hin, hin, up.ci, H, H, n, up.kp_f, 1, 2, 0, 0, s)) {
+      un_im2col(x, col, B, hin, hin, up.ci, H, H, up.kp_f, 1, 2, 0, 0, s);
+      gemm(col, bt + up.bt_f, W + up.b, d.up, M, n, up.kp_f, false, gpart, s);
+    }
     const float* skip = et[3 - i].a2;
     gemm(d.up, bt + convs[a.cnv1].bt_f, W + convs[a.cnv1].b, d.g, M, n, n, false, gpart, s);
     bn_fwd(bns[a.bn1], d.g, M, nullptr, 0);
@@ -416,12 +419,12 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   };
   auto conv3_wgrad = [&](const float* xin, int H, const UConv& c, const float* dy) {
     const long M = (long)B * H * H;
-    un_im2col(xin, col, B, H, H, c.ci, H, H, c.kp_f, 0, 1, 1, 1, s);
-    un_wgrad(dy, c.co, col, c.kp_f, M, c.co, c.kp_f, c.ci, 9, 0, wpart, G + c.w, s);
+    un_wgrad(dy, c.co, xin, c.ci, 1, B, H, H, c.ci, M, c.co, c.kp_f, c.ci, 9, 0, wpart, G + c.w, s);
     bias_grad(dy, M, c);
   };
   auto conv3_dgrad = [&](const float* dy, int H, const UConv& c, float* dx) {
     const long M = (long)B * H * H;
+    if (un_conv3_small(dy, bt + c.bt_d, nullptr, dx, B, H, H, c.co, H, H, c.ci, c.kp_d, 0, 1, 1, 1, s)) return;
     un_im2col(dy, col, B, H, H, c.co, H, H, c.kp_d, 0, 1, 1, 1, s);
     gemm(col, bt + c.bt_d, nullptr, dx, M, c.ci, c.kp_d, false, gpart, s);
   };
@@ -437,7 +440,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     if (dx) conv3_dgrad(tmp, H, convs[k.c1], dx);
   };
   // output layer: dz [Mf,3]
-  un_wgrad(dz, 3, x, oc.ci, Mf, 3, oc.ci, oc.ci, 1, 4, wpart, G + oc.w, s);
+  un_wgrad(dz, 3, x, oc.ci, 0, 1, 1, 1, 1, Mf, 3, oc.ci, oc.ci, 1, 4, wpart, G + oc.w, s);
   un_colsum(dz, Mf, 3, G + oc.b, cpart, s);
   un_small_dgrad(dz, W + oc.w, tmpX, Mf, oc.ci, 3, false, s);
   // decoders, last first: tmpX holds the gradient of the decoder block's output
@@ -456,29 +459,30 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
                    4 + i, s);  // tmpX = d up, denc = d skip (direct), d1 = d bn3 output
     bn_bwd(b3, d1, d.t, M, 0, d2);  // d2 = d t
     const UConv& c3 = convs[a.conv3];
-    un_wgrad(d2, 1, d.s, n, M, 1, n, n, 1, 4, wpart, G + c3.w, s);
+    un_wgrad(d2, 1, d.s, n, 0, 1, 1, 1, 1, M, 1, n, n, 1, 4, wpart, G + c3.w, s);
     un_colsum(d2, M, 1, G + c3.b, cpart, s);
     UBn &b1 = bns[a.bn1], &b2 = bns[a.bn2];
     un_att_s_bwd(d2, W + c3.w, d.g, d.xs, b1.mean, b1.sc, W + b1.beta, b2.mean, b2.sc, W + b2.beta, tmpY, M, n, s);
     // bn1 / cnv1 on up
     bn_bwd(b1, tmpY, d.g, M, 0, tmpT);
     const UConv& k1 = convs[a.cnv1];
-    un_wgrad(tmpT, n, d.up, n, M, n, n, n, 1, 4, wpart, G + k1.w, s);
+    un_wgrad(tmpT, n, d.up, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k1.w, s);
     bias_grad(tmpT, M, k1);
     gemm(tmpT, bt + k1.bt_d, nullptr, tmpX, M, n, n, true, gpart, s);
     // bn2 / cnv2 on skip
     bn_bwd(b2, tmpY, d.xs, M, 0, tmpT);
     const UConv& k2 = convs[a.cnv2];
-    un_wgrad(tmpT, n, skip, n, M, n, n, n, 1, 4, wpart, G + k2.w, s);
+    un_wgrad(tmpT, n, skip, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k2.w, s);
     bias_grad(tmpT, M, k2);
     gemm(tmpT, bt + k2.bt_d, nullptr, denc, M, n, n, true, gpart, s);
     // transposed conv: input = the previous decoder's output (or the bottleneck's)
     const float* xin = i == 0 ? c4t.a2 : dt[i - 1].a2;
-    un_im2col(xin, col, B, hin, hin, up.ci, H, H, up.kp_f, 1, 2, 0, 0, s);
-    un_wgrad(tmpX, n, col, up.kp_f, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, s);
+    un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, s);
     bias_grad(tmpX, M, up);
-    un_im2col(tmpX, col, B, H, H, n, hin, hin, up.kp_d, 0, 2, 0, 0, s);
-    gemm(col, bt + up.bt_d, nullptr, tmpY, (long)B * hin * hin, up.ci, up.kp_d, false, gpart, s);
+    if (!un_conv3_small(tmpX, bt + up.bt_d, nullptr, tmpY, B, H, H, n, hin, hin, up.ci, up.kp_d, 0, 2, 0, 0, s)) {
+      un_im2col(tmpX, col, B, H, H, n, hin, hin, up.kp_d, 0, 2, 0, 0, s);
+      gemm(col, bt + up.bt_d, nullptr, tmpY, (long)B * hin * hin, up.ci, up.kp_d, false, gpart, s);
+    }
     std::swap(tmpX, tmpY);  // tmpX = gradient of the next (earlier) block's output
   }
   // bottleneck: tmpX = d c4 output

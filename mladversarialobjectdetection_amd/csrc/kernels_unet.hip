@@ -96,51 +96,275 @@ __global__ __launch_bounds__(256) void k_wprep(const float* __restrict__ w, floa
 }
 
 // ------------------------------------------------------------------------------------------
-// weight gradient: part[z][co][k] = sum over rows of slice z of dy[m][co] * col[m][k]
-// 64 x 64 tile per workgroup, 16 x 16 threads with 4 x 4 outputs each, 32-row chunks in LDS
+// weight gradient on the fp32 matrix cores: part[z][co][k] = sum over the rows m of slice z of
+// dy[m][co] * col[m][k], with col gathered on the fly (no column matrix in HBM):
+//   SRC 0: col = a row-major matrix x[m * ldx + k] (1x1 convs: the layer input itself)
+//   SRC 1: 3x3 conv, stride 1, pads (1, 1): col[m][(ky*3 + kx)*C + c] = x[b, oy+ky-1, ox+kx-1, c]
+//   SRC 2: transposed conv (stride 2): col[m][(ky*3 + kx)*C + c] = x[b, (oy-ky)/2, (ox-kx)/2, c]
+//          when both differences are even and >= 0 (x is H/2 x W/2; rows m are the H x W outputs)
+// v_mfma_f32_16x16x4_f32: lane l feeds A[i = l&15][kk = l>>4] = dy[m0 + kk][co0 + i] and
+// B[kk][j = l&15] of four accumulators t (a wave owns a 16 (co) x 64 (k) tile sharing the A
+// operand).  VEC (channels a multiple of 4): the lane's four columns are k0 + 4j + t — one 16-B
+// load feeds all four tiles (a 4-B load per tile made the kernel bound by address processing);
+// otherwise k0 + 16t + j.  A wave takes every fourth 4-row step of the workgroup's slice, U steps'
+// loads in flight; the four waves' tiles are summed through LDS in a fixed order
+// (bit-reproducible).  A lane's columns never change, so their (tap, channel) decomposition is
+// hoisted; its pixel advances by 16 rows per step.
 // ------------------------------------------------------------------------------------------
-constexpr int kWgT = 64, kWgR = 32;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-__global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dy, int ldy, const float* __restrict__ col,
-                                               int ldc, long M, int Co, int Kp, long rows_per_slice,
-                                               float* __restrict__ part) {
-  __shared__ float sd[kWgR][kWgT + 4], sc[kWgR][kWgT + 4];
-  const int co0 = blockIdx.x * kWgT, k0 = blockIdx.y * kWgT;
+template <int SRC, bool VEC>
+__global__ __launch_bounds__(256) void k_wgrad_mfma(const float* __restrict__ dy, int ldy,
+                                                    const float* __restrict__ x, int ldx, int H, int W, int C,
+                                                    long M, int Co, int Kp, long rows_per_slice,
+                                                    float* __restrict__ part) {
+  __shared__ floatx4 red[4][4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const int co = blockIdx.x * 16 + i16;
+  const int k0 = blockIdx.y * 64;
   const long r0 = (long)blockIdx.z * rows_per_slice, r1 = min(M, r0 + rows_per_slice);
-  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  float acc[4][4] = {};
-  for (long rb = r0; rb < r1; rb += kWgR) {
-    for (int e = threadIdx.x; e < kWgR * kWgT; e += 256) {
-      const int rr = e / kWgT, cc = e - rr * kWgT;
-      const long row = rb + rr;
-      const bool rok = row < r1;
-      sd[rr][cc] = (rok && co0 + cc < Co) ? dy[row * ldy + co0 + cc] : 0.f;
-      sc[rr][cc] = (rok && k0 + cc < Kp) ? col[row * ldc + k0 + cc] : 0.f;
+  const bool cok = co < Co;
+  const int Kend = SRC == 0 ? Kp : 9 * C;
+  // hoisted column decomposition of this lane's k columns (VEC: one quad, NQ = 1)
+  constexpr int NQ = VEC ? 1 : 4;
+  int koff[NQ], ky[NQ], kx[NQ];
+  bool kok[NQ];
+#pragma unroll
+  for (int t = 0; t < NQ; ++t) {
+    const int k = VEC ? k0 + 4 * i16 : k0 + 16 * t + i16;
+    kok[t] = k < Kend;
+    if (SRC == 0) {
+      koff[t] = k;
+      ky[t] = kx[t] = 0;
+    } else {
+      const int tap = kok[t] ? k / C : 0;
+      koff[t] = kok[t] ? k - tap * C : 0;
+      ky[t] = tap / 3;
+      kx[t] = tap - ky[t] * 3;
     }
-    __syncthreads();
-#pragma unroll 4
-    for (int rr = 0; rr < kWgR; ++rr) {
-      float a[4], b[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = sd[rr][ty * 4 + i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) b[j] = sc[rr][tx * 4 + j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
-    }
-    __syncthreads();
   }
+  floatx4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // this lane's first row and its pixel
+  long m = r0 + 4 * wave + kk;
+  int ox = 0, oy = 0, b = 0;
+  if (SRC != 0) {
+    const long mm = min(m, M - 1);
+    ox = (int)(mm % W);
+    const long q = mm / W;
+    oy = (int)(q % H);
+    b = (int)(q / H);
+  }
+  const int Hi = SRC == 2 ? H / 2 : H, Wi = SRC == 2 ? W / 2 : W;
+  constexpr int U = 4;  // row steps whose loads are in flight together
+  for (long m0 = r0 + 4 * wave; m0 < r1; m0 += 16 * U) {
+    float av[U];
+    floatx4 bv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      // loads from clamped (always valid) addresses, zeroed after they land
+      const bool rok = m < r1;
+      av[u] = dy[(rok && cok) ? m * ldy + co : 0];
+      if (!(rok && cok)) av[u] = 0.f;
+#pragma unroll
+      for (int t = 0; t < NQ; ++t) {
+        long addr = 0;
+        bool ok = rok && kok[t];
+        if (SRC == 0) {
+          addr = m * ldx + koff[t];
+        } else {
+          int iy, ix;
+          bool g;
+          if (SRC == 1) {
+            iy = oy + ky[t] - 1;
+            ix = ox + kx[t] - 1;
+            g = true;
+          } else {
+            const int dyy = oy - ky[t], dxx = ox - kx[t];
+            g = dyy >= 0 && dxx >= 0 && !(dyy & 1) && !(dxx & 1);
+            iy = dyy >> 1;
+            ix = dxx >> 1;
+          }
+          ok = ok && g && iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+          addr = (((long)b * Hi + iy) * Wi + ix) * C + koff[t];
+        }
+        if constexpr (VEC) {
+          const floatx4 v = *reinterpret_cast<const floatx4*>(x + (ok ? addr : 0));
+          bv[u] = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+        } else {
+          const float v = x[ok ? addr : 0];
+          bv[u][t] = ok ? v : 0.f;
+        }
+      }
+      m += 16;
+      if (SRC != 0) {
+        ox += 16;
+        while (ox >= W) {
+          ox -= W;
+          if (++oy == H) {
+            oy = 0;
+            ++b;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u][t], acc[t], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < 4; ++t) red[wave][t][lane] = acc[t];
+  __syncthreads();
+  // D layout: lane l holds column j = l&15, rows 4*(l>>4) + r
   float* out = part + (long)blockIdx.z * Co * Kp;
+  for (int e = threadIdx.x; e < 4 * 64; e += 256) {
+    const int t = e >> 6, l = e & 63;
+    floatx4 s = red[0][t][l];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = co0 + ty * 4 + i;
-    if (co >= Co) continue;
+    for (int w = 1; w < 4; ++w) s += red[w][t][l];
+    const int k = VEC ? k0 + 4 * (l & 15) + t : k0 + 16 * t + (l & 15);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = k0 + tx * 4 + j;
-      if (k < Kp) out[(long)co * Kp + k] = acc[i][j];
+    for (int r = 0; r < 4; ++r) {
+      const int c = blockIdx.x * 16 + 4 * (l >> 4) + r;
+      if (c < Co && k < Kp) out[(long)c * Kp + k] = s[r];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// 3x3 convolutions with few channels (the U-Net's full-resolution levels): out[m][n] = bias[n] +
+// sum_k col[m][k] * Bt[n][k] with the column matrix gathered on the fly (k_im2col's modes: 0 conv
+// with stride s and pads (pt, pl), 1 stride-2 transposed conv) — the column matrix of these layers
+// is 9x the layer input and would be written and read once more through HBM.
+// v_mfma_f32_16x16x4_f32: lane l feeds A[i = l&15][kk = l>>4] = col[m0 + i][k0 + kk] (one gather)
+// and B[kk][j = l&15] = Bt[16t + j][k0 + kk] from LDS; a wave owns 16 output rows x 16*NT
+// columns and walks 16-row tiles (persistent).  The lane's (tap, channel) advances by 4 per step.
+// ------------------------------------------------------------------------------------------
+constexpr int kConvMaxKp = 288, kConvMaxN = 32;
+
+template <int NT, int MODE, bool VEC>
+__global__ __launch_bounds__(256) void k_conv3_small(const float* __restrict__ x, const float* __restrict__ Bt,
+                                                     const float* __restrict__ bias, float* __restrict__ out, int B,
+                                                     int H, int W, int C, int Ho, int Wo, int N, int Kp, int s,
+                                                     int pt, int pl) {
+  constexpr int KB = 16;  // k steps (of 4) whose gathers are in flight together
+  __shared__ float sb[(kConvMaxKp + 4 * KB - 1) / (4 * KB) * 4 * KB][16 * NT + 1];  // [k][n]
+  const int KpR = (Kp + 4 * KB - 1) / (4 * KB) * (4 * KB);
+  for (int e = threadIdx.x; e < KpR * 16 * NT; e += 256) {
+    const int k = e / (16 * NT), n = e - k * 16 * NT;
+    sb[k][n] = (n < N && k < Kp) ? Bt[(long)n * Kp + k] : 0.f;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kk = lane >> 4;
+  const long M = (long)B * Ho * Wo;
+  const long tiles = (M + 15) / 16;
+  const int K9 = 9 * C;
+  float bv[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) bv[t] = (bias && 16 * t + i16 < N) ? bias[16 * t + i16] : 0.f;
+  for (long tile = (long)blockIdx.x * 4 + wave; tile < tiles; tile += (long)gridDim.x * 4) {
+    const long m = tile * 16 + i16;
+    const bool rok = m < M;
+    const long mm = rok ? m : M - 1;
+    const int ox = (int)(mm % Wo);
+    const long q = mm / Wo;
+    const int oy = (int)(q % Ho);
+    const int b = (int)(q / Ho);
+    const float* xb = x + (long)b * H * W * C;
+    floatx4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+    // this lane's column (VEC: its quad of columns 16 qs + 4 kk .. +3; else k0 + kk) as
+    // (tap (ky, kx), channel c)
+    int c = VEC ? 4 * kk : kk, ky = 0, kx = 0;
+    while (c >= C) {
+      c -= C;
+      if (++kx == 3) {
+        kx = 0;
+        ++ky;
+      }
+    }
+    auto gather_at = [&](bool& ok) -> long {
+      int iy, ix;
+      bool g;
+      if (MODE == 0) {
+        iy = oy * s + ky - pt;
+        ix = ox * s + kx - pl;
+        g = true;
+      } else {
+        const int dyy = oy - ky, dxx = ox - kx;
+        g = dyy >= 0 && dxx >= 0 && !(dyy & 1) && !(dxx & 1);
+        iy = dyy >> 1;
+        ix = dxx >> 1;
+      }
+      ok = ok && g && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      return ok ? ((long)iy * W + ix) * C + c : 0;
+    };
+    auto advance = [&](int by) {
+      c += by;
+      while (c >= C) {
+        c -= C;
+        if (++kx == 3) {
+          kx = 0;
+          ++ky;
+        }
+      }
+    };
+    if constexpr (VEC) {
+      // one 16-B gather per lane feeds 4 MFMA steps: step e of quad-step q uses column 16q + 4kk + e
+      constexpr int QB = 4;
+      for (int kb = 0; kb < Kp; kb += 16 * QB) {
+        floatx4 a[QB];
+#pragma unroll
+        for (int u = 0; u < QB; ++u) {
+          bool ok = rok && kb + 16 * u + 4 * kk < K9;
+          const long off = gather_at(ok);
+          const floatx4 v = *reinterpret_cast<const floatx4*>(xb + off);
+          a[u] = ok ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+          advance(16);
+        }
+#pragma unroll
+        for (int u = 0; u < QB; ++u)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][e], sb[kb + 16 * u + 4 * kk + e][16 * t + i16],
+                                                            acc[t], 0, 0, 0);
+      }
+    } else {
+      for (int kb = 0; kb < Kp; kb += 4 * KB) {
+        // gathers of KB steps from clamped (always valid) addresses, zeroed after the loads
+        float a[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+          bool ok = rok && kb + 4 * u + kk < K9;
+          const long off = gather_at(ok);
+          const float v = xb[off];
+          a[u] = ok ? v : 0.f;
+          advance(4);
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u)
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], sb[kb + 4 * u + kk][16 * t + i16], acc[t], 0, 0, 0);
+      }
+    }
+    // D layout: lane holds column j = l&15, rows 4*(l>>4) + r
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int n = 16 * t + i16;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long row = tile * 16 + 4 * kk + r;
+        if (row < M) out[row * N + n] = acc[t][r] + bv[t];
+      }
     }
   }
 }
@@ -148,19 +372,28 @@ __global__ __launch_bounds__(256) void k_wgrad(const float* __restrict__ dy, int
 // fold the slices (fixed order) and scatter into the Keras kernel layout of the gradient
 //  kind 0: conv  [ky][kx][ci][co] from (co, (ky,kx,ci));  kind 2: tconv [ky][kx][co][ci];
 //  kind 4: 1x1 [ci][co]
+// A workgroup folds 16 consecutive (co, k) outputs: 16 slice lanes per output each add every 16th
+// slice (independent loads in flight), then lane 0 adds the 16 lane sums in order.
 __global__ __launch_bounds__(256) void k_wgrad_fold(const float* __restrict__ part, int nslice, int Co, int Kp,
                                                     int Kin, int taps, int kind, float* __restrict__ g) {
+  __shared__ float sh[16][17];
+  const int j = threadIdx.x & 15, q = threadIdx.x >> 4;
   const long n = (long)Co * taps * Kin;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int co = (int)(i / ((long)taps * Kin));
-    const int k = (int)(i % ((long)taps * Kin));
-    float s = 0.f;
-    for (int z = 0; z < nslice; ++z) s += part[((long)z * Co + co) * Kp + k];
+  const long i = (long)blockIdx.x * 16 + j;
+  const int co = (int)(min(i, n - 1) / ((long)taps * Kin));
+  const int k = (int)(min(i, n - 1) % ((long)taps * Kin));
+  float s = 0.f;
+  for (int z = q; z < nslice; z += 16) s += part[((long)z * Co + co) * Kp + k];
+  sh[q][j] = s;
+  __syncthreads();
+  if (q == 0 && i < n) {
+    float t = sh[0][j];
+    for (int z = 1; z < 16; ++z) t += sh[z][j];
     const int tap = k / Kin, c = k - tap * Kin;
     long dst;
     if (kind == 2) dst = ((long)tap * Co + co) * Kin + c;
     else dst = ((long)tap * Kin + c) * Co + co;
-    g[dst] = s;
+    g[dst] = t;
   }
 }
 
@@ -194,7 +427,35 @@ __global__ __launch_bounds__(256) void k_colred64(ColRed r, long M, int C, long 
     mu = r.mu[c]; rs = r.rstd[c]; scv = r.sc[c]; be = r.be[c];
   }
   double a0 = 0.0, a1 = 0.0;
-  for (long row = r0 + r_off; active && row < r1; row += lane_rows) {
+  long row = r0 + r_off;
+  // 8 rows per lane in flight (a load-then-add loop waits one memory latency per row)
+  if (active) {
+    for (; row + 7 * (long)lane_rows < r1; row += 8 * (long)lane_rows) {
+      float v[8], g[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = r.y[(row + u * (long)lane_rows) * r.ld + c];
+        g[u] = mode == 1 ? r.da[(row + u * (long)lane_rows) * r.ld + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (mode == 0) {
+          const double d = (double)v[u] - shift;
+          a0 += d;
+          a1 += d * d;
+        } else if (mode == 1) {
+          const float yc = v[u] - mu;
+          float dz = g[u];
+          if (r.act) dz *= leaky_grad(yc * scv + be);
+          a0 += (double)dz;
+          a1 += (double)dz * (double)(yc * rs);
+        } else {
+          a0 += (double)v[u];
+        }
+      }
+    }
+  }
+  for (; active && row < r1; row += lane_rows) {
     const float v = r.y[row * r.ld + c];
     if (mode == 0) {
       const double d = (double)v - shift;
@@ -224,18 +485,35 @@ __global__ __launch_bounds__(256) void k_colred64(ColRed r, long M, int C, long 
   }
 }
 
-// BN statistics: mean / rstd / sc = gamma * rstd, moving statistics (momentum 0.99, Bessel)
-__global__ void k_un_bn_final(const double* __restrict__ part, int nblk, long M, int C,
-                              const float* __restrict__ y0, const float* __restrict__ gamma,
-                              float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ sc,
-                              float* __restrict__ mmean, float* __restrict__ mvar) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double s0 = 0.0, s1 = 0.0;
-  for (int z = 0; z < nblk; ++z) {
+// The finals fold the nblk row-block partials of a channel with one wave: lane l adds blocks
+// l, l+64, ... (independent loads in flight), then a fixed xor tree (bit-reproducible).
+__device__ __forceinline__ void wave_fold(const double* __restrict__ part, int nblk, int C, int c, double& s0,
+                                          double& s1) {
+  const int lane = threadIdx.x & 63;
+  s0 = 0.0;
+  s1 = 0.0;
+  for (int z = lane; z < nblk; z += 64) {
     s0 += part[((long)z * C + c) * 2];
     s1 += part[((long)z * C + c) * 2 + 1];
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s0 += __shfl_xor(s0, o);
+    s1 += __shfl_xor(s1, o);
+  }
+}
+
+// BN statistics: mean / rstd / sc = gamma * rstd, moving statistics (momentum 0.99, Bessel)
+__global__ __launch_bounds__(256) void k_un_bn_final(const double* __restrict__ part, int nblk, long M, int C,
+                                                     const float* __restrict__ y0, const float* __restrict__ gamma,
+                                                     float* __restrict__ mean, float* __restrict__ rstd,
+                                                     float* __restrict__ sc, float* __restrict__ mmean,
+                                                     float* __restrict__ mvar) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  double s0, s1;
+  wave_fold(part, nblk, C, c, s0, s1);
+  if ((threadIdx.x & 63) != 0) return;
   const double dm = s0 / (double)M;
   double var = s1 / (double)M - dm * dm;
   if (var < 0.0) var = 0.0;
@@ -252,15 +530,14 @@ __global__ void k_un_bn_final(const double* __restrict__ part, int nblk, long M,
 }
 
 // BN backward: mean(dz), mean(dz*xhat); d gamma = sum dz*xhat, d beta = sum dz
-__global__ void k_un_bnb_final(const double* __restrict__ part, int nblk, long M, int C, float* __restrict__ mdz,
-                               float* __restrict__ mdzx, float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_un_bnb_final(const double* __restrict__ part, int nblk, long M, int C,
+                                                      float* __restrict__ mdz, float* __restrict__ mdzx,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  double s0 = 0.0, s1 = 0.0;
-  for (int z = 0; z < nblk; ++z) {
-    s0 += part[((long)z * C + c) * 2];
-    s1 += part[((long)z * C + c) * 2 + 1];
-  }
+  double s0, s1;
+  wave_fold(part, nblk, C, c, s0, s1);
+  if ((threadIdx.x & 63) != 0) return;
   mdz[c] = (float)(s0 / (double)M);
   mdzx[c] = (float)(s1 / (double)M);
   dgamma[c] = (float)s1;
@@ -268,12 +545,13 @@ __global__ void k_un_bnb_final(const double* __restrict__ part, int nblk, long M
 }
 
 // column sums (bias gradients)
-__global__ void k_un_colsum_final(const double* __restrict__ part, int nblk, int C, float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_un_colsum_final(const double* __restrict__ part, int nblk, int C,
+                                                         float* __restrict__ out) {
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (c >= C) return;
-  double s0 = 0.0;
-  for (int z = 0; z < nblk; ++z) s0 += part[((long)z * C + c) * 2];
-  out[c] = (float)s0;
+  double s0, s1;
+  wave_fold(part, nblk, C, c, s0, s1);
+  if ((threadIdx.x & 63) == 0) out[c] = (float)s0;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -608,17 +886,62 @@ void un_wprep(const float* w, float* bt, int kind, int ci, int co, int Kp, hipSt
   PHX_LAUNCH_CHECK();
 }
 
-int un_wgrad_slices(long M) { return (int)std::min<long>(std::max<long>(cdiv(M, 2048), 1), 256); }
-
-void un_wgrad(const float* dy, int ldy, const float* col, int ldc, long M, int Co, int Kp, int Kin, int taps,
-              int kind, float* part, float* g, hipStream_t st) {
-  const int ns = un_wgrad_slices(M);
-  const long rps = (M + ns - 1) / ns;
-  hipLaunchKernelGGL(k_wgrad, dim3(cdiv(Co, kWgT), cdiv(Kp, kWgT), ns), dim3(256), 0, st, dy, ldy, col, ldc, M, Co,
-                     Kp, rps, part);
+bool un_conv3_small(const float* x, const float* Bt, const float* bias, float* out, int B, int H, int W, int C,
+                    int Ho, int Wo, int N, int Kp, int mode, int s, int pt, int pl, hipStream_t st) {
+  if (N > kConvMaxN || Kp > kConvMaxKp || Kp < 9 * C || (Kp & 3)) return false;
+  const long tiles = cdiv((long)B * Ho * Wo, 16);
+  const dim3 grid((unsigned)std::min<long>(std::max<long>(cdiv(tiles, 4), 1), 2048));
+  const bool vec = C % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+#define PHX_CV(NT, MD, V) hipLaunchKernelGGL((k_conv3_small<NT, MD, V>), grid, dim3(256), 0, st, x, Bt, bias, out, B, H, W, C, Ho, Wo, N, Kp, s, pt, pl)
+  switch ((N > 16 ? 4 : 0) + (mode ? 2 : 0) + (vec ? 1 : 0)) {
+    case 0: PHX_CV(1, 0, false); break;
+    case 1: PHX_CV(1, 0, true); break;
+    case 2: PHX_CV(1, 1, false); break;
+    case 3: PHX_CV(1, 1, true); break;
+    case 4: PHX_CV(2, 0, false); break;
+    case 5: PHX_CV(2, 0, true); break;
+    case 6: PHX_CV(2, 1, false); break;
+    default: PHX_CV(2, 1, true); break;
+  }
+#undef PHX_CV
   PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_wgrad_fold, grid_for((long)Co * taps * Kin), dim3(256), 0, st, part, ns, Co, Kp, Kin, taps,
-                     kind, g);
+  return true;
+}
+
+// row slices of a weight gradient: about 2048 workgroups over the (co, k) tiles, at least 64 rows
+// (and a multiple of 16) per slice, at most 256 slices (the fold's per-output loop)
+static long wgrad_rows_per_slice(long M, int Co, int Kp) {
+  const long tiles = (long)cdiv(Co, 16) * cdiv(Kp, 64);
+  long ns = std::min<long>(std::max<long>(cdiv(2048, tiles), 1), 256);
+  ns = std::max<long>(1, std::min<long>(ns, cdiv(M, 64)));
+  return (cdiv(M, ns) + 15) / 16 * 16;
+}
+
+int un_wgrad_slices(long M, int Co, int Kp) { return (int)cdiv(M, wgrad_rows_per_slice(M, Co, Kp)); }
+
+void un_wgrad(const float* dy, int ldy, const float* x, int ldx, int src, int B, int H, int W, int C, long M,
+              int Co, int Kp, int Kin, int taps, int kind, float* part, float* g, hipStream_t st) {
+  if (src != 0 && (M != (long)B * H * W || (src == 2 && ((H | W) & 1)) || Kp < 9 * C))
+    throw std::runtime_error("un_wgrad: gather geometry does not match the rows");
+  const long rps = wgrad_rows_per_slice(M, Co, Kp);
+  const int ns = (int)cdiv(M, rps);
+  const dim3 grid(cdiv(Co, 16), cdiv(Kp, 64), ns);
+  // 16-B column loads when every quad of columns is one tap's channels and 16-B aligned
+  const bool vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                   (src == 0 ? (ldx % 4 == 0 && Kp % 4 == 0) : (C % 4 == 0));
+#define PHX_WG(S, V) hipLaunchKernelGGL((k_wgrad_mfma<S, V>), grid, dim3(256), 0, st, dy, ldy, x, ldx, H, W, C, M, Co, Kp, rps, part)
+  switch (src * 2 + (vec ? 1 : 0)) {
+    case 0: PHX_WG(0, false); break;
+    case 1: PHX_WG(0, true); break;
+    case 2: PHX_WG(1, false); break;
+    case 3: PHX_WG(1, true); break;
+    case 4: PHX_WG(2, false); break;
+    default: PHX_WG(2, true); break;
+  }
+#undef PHX_WG
+  PHX_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_wgrad_fold, dim3((unsigned)cdiv((long)Co * taps * Kin, 16)), dim3(256), 0, st, part, ns, Co,
+                     Kp, Kin, taps, kind, g);
   PHX_LAUNCH_CHECK();
 }
 
@@ -638,7 +961,7 @@ void un_bn_stats(const float* y, long M, int C, const float* gamma, float* mean,
   ColRed r{y, nullptr, nullptr, nullptr, nullptr, nullptr, 0, C};
   int nb;
   colred(r, M, C, 0, part, &nb, st);
-  hipLaunchKernelGGL(k_un_bn_final, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nb, M, C, y, gamma, mean, rstd, sc,
+  hipLaunchKernelGGL(k_un_bn_final, dim3(cdiv(C, 4)), dim3(256), 0, st, part, nb, M, C, y, gamma, mean, rstd, sc,
                      mmean, mvar);
   PHX_LAUNCH_CHECK();
 }
@@ -649,7 +972,7 @@ void un_bn_bwd(const float* da, const float* y, long M, int C, const float* mu, 
   ColRed r{y, da, mu, rstd, sc, be, act, C};
   int nb;
   colred(r, M, C, 1, part, &nb, st);
-  hipLaunchKernelGGL(k_un_bnb_final, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nb, M, C, mdz, mdzx, dgamma, dbeta);
+  hipLaunchKernelGGL(k_un_bnb_final, dim3(cdiv(C, 4)), dim3(256), 0, st, part, nb, M, C, mdz, mdzx, dgamma, dbeta);
   PHX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_un_bnb_apply, grid_for(M * C), dim3(256), 0, st, da, y, mu, rstd, sc, be, mdz, mdzx, dy, M * C,
                      C, act);
@@ -660,7 +983,7 @@ void un_colsum(const float* v, long M, int C, float* out, double* part, hipStrea
   ColRed r{v, nullptr, nullptr, nullptr, nullptr, nullptr, 0, C};
   int nb;
   colred(r, M, C, 2, part, &nb, st);
-  hipLaunchKernelGGL(k_un_colsum_final, dim3(cdiv(C, 256)), dim3(256), 0, st, part, nb, C, out);
+  hipLaunchKernelGGL(k_un_colsum_final, dim3(cdiv(C, 4)), dim3(256), 0, st, part, nb, C, out);
   PHX_LAUNCH_CHECK();
 }
 

@@ -13,14 +13,20 @@ namespace phx {
 // col [B*Ho*Wo, Kp]: mode 0 conv (stride s, pads pt / pl), mode 1 transposed conv (stride 2)
 void un_im2col(const float* x, float* col, int B, int H, int W, int C, int Ho, int Wo, int Kp, int mode, int s,
                int pt, int pl, hipStream_t st);
+// out [B*Ho*Wo, N] = col (gathered as un_im2col's mode / stride / pads, never stored) x Bt^T + bias,
+// for the few-channel levels (N <= 32, Kp <= 288); false = shape not covered (use im2col + GEMM)
+bool un_conv3_small(const float* x, const float* Bt, const float* bias, float* out, int B, int H, int W, int C,
+                    int Ho, int Wo, int N, int Kp, int mode, int s, int pt, int pl, hipStream_t st);
 // GEMM B operands from Keras kernels: kind 0 conv fwd, 1 conv dgrad, 2 tconv fwd, 3 tconv dgrad,
 // 4 1x1 fwd, 5 1x1 dgrad (bt [N][Kp])
 void un_wprep(const float* w, float* bt, int kind, int ci, int co, int Kp, hipStream_t st);
 // weight gradient of (dy [M][Co], col [M][Kp]) into the Keras layout of g (kind 0 conv, 2 tconv,
-// 4 1x1); part: un_wgrad_slices(M) * Co * Kp floats
-int un_wgrad_slices(long M);
-void un_wgrad(const float* dy, int ldy, const float* col, int ldc, long M, int Co, int Kp, int Kin, int taps,
-              int kind, float* part, float* g, hipStream_t st);
+// 4 1x1); part: un_wgrad_slices(M, Co, Kp) * Co * Kp floats.  The column matrix is gathered on the
+// fly from x: src 0 = x itself [M][ldx]; src 1 = 3x3 conv (stride 1, pads 1) over x [B,H,W,C];
+// src 2 = stride-2 transposed conv over x [B,H/2,W/2,C] (rows = the B*H*W outputs)
+int un_wgrad_slices(long M, int Co, int Kp);
+void un_wgrad(const float* dy, int ldy, const float* x, int ldx, int src, int B, int H, int W, int C, long M,
+              int Co, int Kp, int Kin, int taps, int kind, float* part, float* g, hipStream_t st);
 
 // ---- BN (training) and column sums: fp64 partials (un_colred_doubles) ----------------------
 size_t un_colred_doubles(long M, int C);
