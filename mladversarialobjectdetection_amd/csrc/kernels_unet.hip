@@ -703,29 +703,34 @@ __global__ __launch_bounds__(256) void k_att_cat_bwd(const float* __restrict__ d
                                                      float* __restrict__ dup, float* __restrict__ dskip,
                                                      float* __restrict__ dz3, int B, long HW, int C, uint64_t seed,
                                                      int64_t step, int gimg0, int layer) {
+  // C lanes per pixel (C a power of two <= 64): lane c handles channels c (up) and C + c (skip);
+  // the skip half's dot product with the gradient is reduced by a fixed xor tree
   const long M = (long)B * HW;
-  for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += (long)gridDim.x * blockDim.x) {
-    const int b = (int)(m / HW);
-    const float z = (t[m] - mu3[0]) * sc3[0] + be3[0];
-    const float a = 1.0f / (1.0f + expf(-z));
-    float da = 0.f;
-    for (int c2 = 0; c2 < 2 * C; ++c2) {
-      const long i = m * 2 * C + c2;
-      const long e = i - (long)b * HW * 2 * C;
-      const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
-                                          (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
-                                    (uint32_t)seed, (uint32_t)(seed >> 32));
-      const float g = u01(q.x) >= 0.2f ? dcat[i] * 1.25f : 0.f;
-      if (c2 < C) {
-        dup[m * C + c2] = g;
-      } else {
-        const float sk = skip[m * C + c2 - C];
-        dskip[m * C + c2 - C] = g * a;
-        da = fmaf(g, sk, da);
-      }
-    }
-    dz3[m] = da * (a * (1.0f - a));
+  const long gi = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long m = gi / C;
+  const int c = (int)(gi - m * C);
+  const bool ok = m < M;
+  const long mc = ok ? m : M - 1;
+  const int b = (int)(mc / HW);
+  const float z = (t[mc] - mu3[0]) * sc3[0] + be3[0];
+  const float a = 1.0f / (1.0f + expf(-z));
+  auto keep = [&](int c2) {
+    const long e = (mc - (long)b * HW) * 2 * C + c2;
+    const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
+                                        (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
+                                  (uint32_t)seed, (uint32_t)(seed >> 32));
+    return u01(q.x) >= 0.2f;
+  };
+  const float g0 = keep(c) ? dcat[mc * 2 * C + c] * 1.25f : 0.f;
+  const float g1 = keep(C + c) ? dcat[mc * 2 * C + C + c] * 1.25f : 0.f;
+  const float sk = skip[mc * C + c];
+  if (ok) {
+    dup[mc * C + c] = g0;
+    dskip[mc * C + c] = g1 * a;
   }
+  float da = g1 * sk;
+  for (int o = 1; o < C; o <<= 1) da += __shfl_xor(da, o);
+  if (ok && c == 0) dz3[mc] = da * (a * (1.0f - a));
 }
 
 // d(pre-leaky sum) of the attention: ds[m][c] = dt[m] * w3[c] * leaky'(bn1(g) + bn2(x))
@@ -945,11 +950,14 @@ void un_wgrad(const float* dy, int ldy, const float* x, int ldx, int src, int B,
   PHX_LAUNCH_CHECK();
 }
 
-int un_colred_blocks(long M) { return (int)std::min<long>(std::max<long>(cdiv(M, 1024), 1), 1024); }
+// row blocks of a column reduction: about 8192 elements per block (32 per lane), at most 1024
+static int un_colred_blocks(long M, int C) {
+  return (int)std::min<long>(std::max<long>(std::min<long>(cdiv(M * C, 8192), M), 1), 1024);
+}
 
 static void colred(const ColRed& r, long M, int C, int mode, double* part, int* nblk, hipStream_t st) {
   if (C < 1 || C > 256) throw std::runtime_error("unet column reduction: C must be in [1, 256]");
-  const int nb = un_colred_blocks(M);
+  const int nb = un_colred_blocks(M, C);
   const long rpb = (M + nb - 1) / nb;
   hipLaunchKernelGGL(k_colred64, dim3(nb), dim3(256), 0, st, r, M, C, rpb, mode, part);
   PHX_LAUNCH_CHECK();
@@ -987,7 +995,7 @@ void un_colsum(const float* v, long M, int C, float* out, double* part, hipStrea
   PHX_LAUNCH_CHECK();
 }
 
-size_t un_colred_doubles(long M, int C) { return (size_t)un_colred_blocks(M) * C * 2; }
+size_t un_colred_doubles(long M, int C) { return (size_t)un_colred_blocks(M, C) * C * 2; }
 
 void un_bnact(const float* y, const float* mu, const float* sc, const float* be, float* a, long M, int C, int act,
               hipStream_t st) {
@@ -1031,8 +1039,9 @@ void un_att_cat(const float* up, const float* skip, const float* t, const float*
 void un_att_cat_bwd(const float* dcat, const float* skip, const float* t, const float* mu3, const float* sc3,
                     const float* be3, float* dup, float* dskip, float* dz3, int B, long HW, int C, uint64_t seed,
                     int64_t step, int gimg0, int layer, hipStream_t st) {
-  hipLaunchKernelGGL(k_att_cat_bwd, grid_for((long)B * HW), dim3(256), 0, st, dcat, skip, t, mu3, sc3, be3, dup, dskip,
-                     dz3, B, HW, C, seed, step, gimg0, layer);
+  if (C < 1 || C > 64 || (C & (C - 1))) throw std::runtime_error("att_cat_bwd: C must be a power of two <= 64");
+  hipLaunchKernelGGL(k_att_cat_bwd, dim3((unsigned)cdiv((long)B * HW * C, 256)), dim3(256), 0, st, dcat, skip, t, mu3,
+                     sc3, be3, dup, dskip, dz3, B, HW, C, seed, step, gimg0, layer);
   PHX_LAUNCH_CHECK();
 }
 
