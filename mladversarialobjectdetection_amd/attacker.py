@@ -100,6 +100,11 @@ class EfficientDetVictim:
         self.manifest = self.ctx.manifest()
         if isinstance(weights, str) and weights == "synthetic":
             blob = wmod.synthetic_blob(self.manifest, seed=seed, person_bias=person_bias)
+        elif isinstance(weights, (str, os.PathLike)):
+            # a TensorFlow checkpoint (directory or prefix), restored as KerasDriver does
+            # (util_keras.restore_ckpt with ema_decay 0.9998, skip_mismatch=False)
+            from .ckpt import checkpoint_to_blob
+            blob = np.ascontiguousarray(checkpoint_to_blob(os.fspath(weights), self.manifest, ema_decay=0.9998))
         else:
             blob = np.ascontiguousarray(np.asarray(weights, dtype=np.float32))
         self.load_weights(blob)

@@ -1,0 +1,117 @@
+"""Victim checkpoint converter (mladversarialobjectdetection_amd/ckpt.py) on CPU.
+
+No TensorFlow checkpoint ships with the reference or exists in this image, so the bundle reader is
+checked against the format's published constants (CRC-32C check value, LevelDB's checksum mask and
+table magic) and against bundles written by this module's writer (parity unpinned beyond those);
+the restore rule is the reference's (util_keras.restore_ckpt, util_keras.py:153-203): EMA shadows win,
+missing keys raise KeyError and shape mismatches ValueError unless skip_mismatch.
+"""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from mladversarialobjectdetection_amd import ckpt as C
+from mladversarialobjectdetection_amd import weights as W
+
+
+def test_crc32c_known_answers():
+    assert C.crc32c(b"123456789") == 0xE3069283          # the CRC-32C check value
+    assert C.crc32c(b"") == 0
+    assert C.crc32c(bytes(32)) == 0x8A9136AA             # RFC 3720 B.4: 32 bytes of zeros
+    assert C.crc32c(bytes([0xFF] * 32)) == 0x62A8AB43     # RFC 3720 B.4: 32 bytes of ones
+    assert C.crc32c(bytes(range(32))) == 0x46DD794E       # RFC 3720 B.4: incrementing
+    for v in (0, 1, 0xE3069283, 0xFFFFFFFF):
+        assert C.crc32c_unmask(C.crc32c_mask(v)) == v
+    assert C.crc32c_mask(0) == 0xA282EAD8
+
+
+def _manifest():
+    from mladversarialobjectdetection_amd import _lib
+    return _lib.Context("efficientdet-d0", 128, 1).manifest()
+
+
+@pytest.fixture(scope="module")
+def d0():
+    man = _manifest()
+    return man, W.synthetic_blob(man, seed=3)
+
+
+def test_round_trip_is_bit_exact(tmp_path, d0):
+    man, blob = d0
+    prefix = str(tmp_path / "ckpt" / "model")
+    C.blob_to_checkpoint(prefix, man, blob)
+    with open(prefix + ".index", "rb") as f:
+        raw = f.read()
+    assert struct.unpack_from("<Q", raw, len(raw) - 8)[0] == 0xDB4775248B80FB57
+    r = C.CheckpointReader(os.path.dirname(prefix))       # directory: `checkpoint` file -> prefix
+    assert len(r.list_variables()) == 2 * len(man)
+    out = C.checkpoint_to_blob(r, man)
+    assert out.dtype == np.float32 and out.shape == blob.shape
+    assert np.array_equal(out.view(np.uint32), blob.view(np.uint32))
+
+
+def test_ema_shadow_wins_unless_disabled(tmp_path, d0):
+    man, blob = d0
+    t = {}
+    for p in man[:40]:
+        v = blob[p["offset"]:p["offset"] + int(np.prod(p["shape"]))].reshape(p["shape"])
+        t[p["name"]] = v
+        t[p["name"] + C.EMA_SUFFIX] = v * 2 + 1
+    prefix = str(tmp_path / "m")
+    C.write_checkpoint(prefix, t)
+    part = man[:40]
+    n = part[-1]["offset"] + int(np.prod(part[-1]["shape"]))
+    ema = C.checkpoint_to_blob(prefix, part, ema_decay=0.9998)
+    raw = C.checkpoint_to_blob(prefix, part, ema_decay=0)
+    np.testing.assert_array_equal(raw[:n], blob[:n])
+    np.testing.assert_array_equal(ema[:n], blob[:n] * 2 + 1)
+
+
+def test_missing_and_mismatched_keys(tmp_path, d0):
+    man, blob = d0
+    part = man[:10]
+    t = {p["name"]: blob[p["offset"]:p["offset"] + int(np.prod(p["shape"]))].reshape(p["shape"]) for p in part}
+    prefix = str(tmp_path / "m")
+    C.write_checkpoint(prefix, t)
+    with pytest.raises(KeyError):                        # no EMA shadows, ema_decay > 0
+        C.checkpoint_to_blob(prefix, part)
+    ok = C.checkpoint_to_blob(prefix, part, ema_decay=0)
+    n = part[-1]["offset"] + int(np.prod(part[-1]["shape"]))
+    np.testing.assert_array_equal(ok[:n], blob[:n])
+    bad = dict(t)
+    bad[part[0]["name"]] = np.zeros((2, 2), np.float32)
+    C.write_checkpoint(prefix, bad)
+    with pytest.raises(ValueError):
+        C.checkpoint_to_blob(prefix, part, ema_decay=0)
+    skipped = C.checkpoint_to_blob(prefix, part, ema_decay=0, skip_mismatch=True)
+    assert skipped.missing == [part[0]["name"]]
+    assert not skipped[:int(np.prod(part[0]["shape"]))].any()
+
+
+def test_corruption_and_object_graph_are_rejected(tmp_path):
+    prefix = str(tmp_path / "m")
+    C.write_checkpoint(prefix, {"a/kernel": np.arange(6, dtype=np.float32).reshape(2, 3)})
+    assert np.array_equal(C.CheckpointReader(prefix).get_tensor("a/kernel"), np.arange(6).reshape(2, 3))
+    data = bytearray(open(prefix + ".data-00000-of-00001", "rb").read())
+    data[0] ^= 1
+    open(prefix + ".data-00000-of-00001", "wb").write(bytes(data))
+    with pytest.raises(ValueError):
+        C.CheckpointReader(prefix).get_tensor("a/kernel")
+    C.write_checkpoint(prefix, {"_CHECKPOINTABLE_OBJECT_GRAPH": np.zeros(1, np.float32)})
+    with pytest.raises(NotImplementedError):
+        C.checkpoint_to_blob(prefix, [{"name": "x", "shape": [1], "offset": 0}])
+
+
+def test_many_blocks_and_shared_prefixes(tmp_path):
+    # more than one data block and restart interval, long shared key prefixes
+    rng = np.random.default_rng(0)
+    t = {f"efficientnet-b0/blocks_{i}/conv2d/kernel": rng.standard_normal((i % 5 + 1, 3)).astype(np.float32)
+         for i in range(300)}
+    prefix = str(tmp_path / "m")
+    C.write_checkpoint(prefix, t, block_entries=7)
+    r = C.CheckpointReader(prefix)
+    assert sorted(r.entries) == sorted(t)
+    for k in list(t)[::37]:
+        np.testing.assert_array_equal(r.get_tensor(k), t[k])
