@@ -116,10 +116,14 @@ class PatchAttackDefender:
         else:
             bp = cp = None
         self.handle.call("phx_def_step_grad", images.data_ptr(), B, bp, cp, self.params.data_ptr(),
-                         self._red.data_ptr(), int(self.cur_step), ddp.global_offset(B), _stream())
+                         self._red.data_ptr(), int(self.cur_step), self.global_offset(B), _stream())
         return self.grad
 
     __call__ = call
+
+    def global_offset(self, B):
+        """Global index of this rank's first image (RNG keys: draws do not depend on the GPU count)."""
+        return ddp.global_offset(B)
 
     def apply_gradients(self):
         """Keras Adam (defender_train.py:35, lr 1e-2), no constraints."""

@@ -1,0 +1,97 @@
+"""GPU, world size 2: the product's PatchAttackDefender.train_step under data parallelism (BASELINE C5,
+SURVEY.md 8f rank 1 / 8e).
+
+Two ranks share cuda:0 through a gloo process group (RCCL refuses two ranks on one device). Each rank
+holds one image of a 2-image global batch and runs the real train_step: libphx defender step ->
+one SUM all-reduce of [d U-Net variables | loss] -> Adam. Checked against single-process runs of the
+same library on each shard (RNG keyed by global image index; the U-Net's BN domain is the rank):
+  * the all-reduced gradient and loss == the sums of the two shard gradients / losses (bit-exact)
+  * the U-Net variables after Adam are bit-identical on both ranks, and again after a second step
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+S = 256
+
+
+def _case():
+    imgs = np.random.default_rng(3).uniform(-1, 1, (2, S, S, 3)).astype(np.float32)
+    boxes = [np.array([[20, 30, 200, 120]], np.float32), np.array([[5, 5, 240, 140], [100, 100, 250, 250]], np.float32)]
+    return imgs, boxes
+
+
+def _make():
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim
+    from mladversarialobjectdetection_amd.defender import PatchAttackDefender
+    v = EfficientDetVictim("efficientdet-d0", "synthetic", seed=0, image_size=S, max_batch=1, rng_seed=5,
+                           bn_mode="frozen")
+    d = PatchAttackDefender(v, protege_config_override={"nms_configs": {"iou_thresh": .5, "score_thresh": .5}},
+                            seed=9)
+    d.cur_step = 3
+    return d
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    imgs, boxes = _case()
+    d = _make()
+    x = torch.as_tensor(imgs[rank:rank + 1]).cuda()
+    out = d.train_step(x, boxes=[boxes[rank]])
+    red = d._red.cpu().numpy().copy()
+    params = d.params.cpu().numpy().copy()
+    loss = float(out["loss"].item())
+    d.train_step(x, boxes=[boxes[rank]])
+    p2 = d.params.cpu().numpy().copy()
+    q.put((rank, red, params, loss, p2))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(600)
+def test_two_rank_defender_step_equals_sum_of_shards():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r = q.get(timeout=500)
+        res[r[0]] = r
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (_, red0, p0, l0, p20), (_, red1, p1, l1, p21) = res[0], res[1]
+    assert np.array_equal(red0, red1) and np.array_equal(p0, p1) and np.array_equal(p20, p21)
+    assert l0 == l1
+
+    imgs, boxes = _case()
+    d = _make()
+    shard = []
+    for r in range(2):
+        d.global_offset = lambda B, r=r: r * B
+        d.call(torch.as_tensor(imgs[r:r + 1]).cuda(), boxes=[boxes[r]])
+        shard.append(d._red.cpu().numpy().copy())
+    assert np.array_equal(red0, shard[0] + shard[1])
+    assert np.abs(shard[0][:-1]).max() > 0 and np.abs(shard[1][:-1]).max() > 0
+    assert l0 == float(shard[0][-1] + shard[1][-1])
