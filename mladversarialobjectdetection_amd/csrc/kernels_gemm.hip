@@ -371,7 +371,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
           }
         }
         if constexpr (STATS) {
-          // per-wave column statistics over its TM*32 rows, then merged across the WM waves
+          // per-wave column statistics of this tile's TM*32 rows (two passes in registers), folded
+          // into the wave's running statistics; the WM waves sharing these columns are merged once,
+          // after the last tile (a per-tile workgroup barrier here stalled the pipeline)
           const float nw = (float)max(0, min(TM * 32, a.M - mrow0));
 #pragma unroll
           for (int j = 0; j < TN; ++j) {
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
               for (int e = 0; e < 16; ++e)
-                if (mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) s += acc[i][j][e];
+                if (full || mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) s += acc[i][j][e];
             s += __shfl_xor(s, 32);
             const float mean = nw > 0.f ? s / nw : 0.f;
             float q = 0.f;
@@ -388,33 +390,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             for (int i = 0; i < TM; ++i)
 #pragma unroll
               for (int e = 0; e < 16; ++e)
-                if (mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) {
+                if (full || mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) {
                   const float d = acc[i][j][e] - mean;
                   q = fmaf(d, d, q);
                 }
             q += __shfl_xor(q, 32);
-            if (h == 0) wst[wave][j * 32 + r32] = make_float2(mean, q);
+            float n_ = sn;
+            chan_merge(n_, smean[j], sm2[j], nw, mean, q);
           }
-          if (lane == 0) wcn[wave] = nw;
-          __syncthreads();
-          if (wm == 0 && h == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              float tn = 0.f, tm = 0.f, t2 = 0.f;
-#pragma unroll
-              for (int w = 0; w < WM; ++w) {
-                const int wv = wn * WM + w;
-                const float2 v = wst[wv][j * 32 + r32];
-                chan_merge(tn, tm, t2, wcn[wv], v.x, v.y);
-              }
-              float n_ = sn;
-              chan_merge(n_, smean[j], sm2[j], tn, tm, t2);
-            }
-            float tn = 0.f;
-#pragma unroll
-            for (int w = 0; w < WM; ++w) tn += wcn[wn * WM + w];
-            sn += tn;
-          }
+          sn += nw;
         }
         if constexpr (SK == 2) {
           // BN-backward sums of the finished gradient tile (BN input y at the same elements)
@@ -443,18 +427,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             }
             s1 += __shfl_xor(s1, 32);
             s2 += __shfl_xor(s2, 32);
-            if (h == 0) wst[wave][j * 32 + r32] = make_float2(s1, s2);
-          }
-          __syncthreads();
-          if (wm == 0 && h == 0) {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-              for (int w = 0; w < WM; ++w) {
-                const float2 v = wst[wn * WM + w][j * 32 + r32];
-                smean[j] += v.x;
-                sm2[j] += v.y;
-              }
+            smean[j] += s1;
+            sm2[j] += s2;
           }
         }
 #pragma unroll
@@ -488,23 +462,38 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       }
     }
   }
-  if constexpr (STATS) {
+  if constexpr (SK != 0) {
+    // merge the running statistics / sums of the WM waves that share each column (fixed order)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      if (h == 0) wst[wave][j * 32 + r32] = make_float2(smean[j], sm2[j]);
+    if (lane == 0) wcn[wave] = sn;
+    __syncthreads();
     if (wm == 0 && h == 0) {
+      float ntot = 0.f;
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int col = n0 + wn * TN * 32 + j * 32 + r32;
-        if (col < a.N) sink_put(a.sink, blockIdx.x, col, sn, smean[j], sm2[j]);
-      }
-      if (blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[blockIdx.x] = sn;
-    }
-  }
-  if constexpr (SK == 2) {
-    if (wm == 0 && h == 0) {
+        float tn = 0.f, tm = 0.f, t2 = 0.f;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int col = n0 + wn * TN * 32 + j * 32 + r32;
-        if (col < a.N) gsink_put(a.gsk, blockIdx.x, col, smean[j], sm2[j]);
+        for (int w = 0; w < WM; ++w) {
+          const int wv = wn * WM + w;
+          const float2 v = wst[wv][j * 32 + r32];
+          if constexpr (STATS) {
+            chan_merge(tn, tm, t2, wcn[wv], v.x, v.y);
+          } else {
+            tm += v.x;
+            t2 += v.y;
+          }
+        }
+        ntot = tn;
+        if (col < a.N) {
+          if constexpr (STATS) sink_put(a.sink, blockIdx.x, col, tn, tm, t2);
+          else gsink_put(a.gsk, blockIdx.x, col, tm, t2);
+        }
       }
+      if constexpr (STATS)
+        if (blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[blockIdx.x] = ntot;
     }
   }
 }

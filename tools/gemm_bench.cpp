@@ -69,7 +69,8 @@ int main(int argc, char** argv) {
   const int wgs = argc > 1 ? atoi(argv[1]) : 1024;
   for (auto& s : shapes) {
     InX ax{A, nullptr, nullptr, nullptr, 0};
-    StatSink sink = s.stats ? StatSink{sp, sc, s.N, 0} : StatSink{};
+    // GEMM_NOSTATS=1: every shape without the statistics epilogue (its cost by difference)
+    StatSink sink = (s.stats && !getenv("GEMM_NOSTATS")) ? StatSink{sp, sc, s.N, 0} : StatSink{};
     int impl = 1;
     auto run = [&]() {
       if (impl == 1)
