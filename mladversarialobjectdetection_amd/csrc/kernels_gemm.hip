@@ -505,12 +505,24 @@ struct G2Cfg {
   int bn() const { return (4 / wm) * tn * 32; }
 };
 
-static G2Cfg g2_pick(int N) {
+// Wide outputs: a column tile that divides N wastes no matrix-core columns (tools/gemm_bench sweeps,
+// BN + swish view: N = 672 and 192 on 96-column tiles, N = 320 on 160-column tiles); the
+// class-head predict conv (N = 810, K = 64: store-heavy) runs fastest on 64x128 tiles.
+static G2Cfg g2_pick(int N, int K, bool bf16) {
   if (N <= 32) return {4, 1, 1};
   if (N <= 64) return {4, 1, 2};
   if (N <= 96) return {4, 1, 3};
   if (N <= 128) return {2, 2, 2};
   if (N <= 160) return {4, 1, 5};
+  static const bool waste = [] {
+    const char* e = std::getenv("PHX_G2PICK");
+    return !(e && e[0] == '0');
+  }();
+  if (waste && !bf16) {  // fp32 only: the bf16 tiles measured slightly slower with it (D4 C4)
+    if (N % 128 != 0 && N % 96 == 0) return {4, 1, 3};
+    if (N % 128 != 0 && N % 160 == 0) return {4, 1, 5};
+    if (N >= 512 && K <= 64) return {2, 1, 2};
+  }
   return {2, 2, 2};
 }
 
@@ -522,7 +534,7 @@ void gemm2_force_cfg(int wm, int tm, int tn, int splits) {
 
 Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
   Gemm2Plan p;
-  G2Cfg c = g2_pick(N);
+  G2Cfg c = g2_pick(N, K, bf16);
   if (g_force[0]) {
     p.wm = g_force[0]; p.tm = g_force[1]; p.tn = g_force[2];
     c = G2Cfg{p.wm, p.tm, p.tn};
