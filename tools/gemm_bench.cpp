@@ -35,6 +35,10 @@ int main(int argc, char** argv) {
       {65536, 64, 64, true, true},     {16384, 672, 112, false, true},  {16384, 112, 672, false, true},
       {4096, 1152, 192, false, true},  {4096, 192, 1152, false, true},  {16384, 64, 64, true, true},
       {4096, 64, 64, true, true},      {4096, 320, 1152, false, true},
+      // more D0 step shapes (indices 17-23)
+      {65536, 240, 40, false, true},   {16384, 480, 80, false, true},   {16384, 80, 480, false, true},
+      {16384, 112, 480, false, true},  {4096, 64, 320, true, true},     {65536, 40, 240, false, true},
+      {65536, 144, 24, false, true},
       // large, square-ish: the kernel's MFMA ceiling without shape effects
       {65536, 512, 512, false, false}, {65536, 512, 512, false, true},  {16384, 1024, 1024, false, false}};
   // GEMM_ONLY=i,j,...: run only those shape indices
