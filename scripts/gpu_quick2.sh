@@ -1,0 +1,17 @@
+# GPU: attack-path parity (incl. moving statistics, determinism, deep / bf16), then the default bench x2
+# and a kernel-trace summary
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py tests/test_gpu_firstpass.py tests/test_gpu_deep.py tests/test_gpu_bf16.py tests/test_gpu_distributed.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_q.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_q.log
+[ $rc -eq 0 ] || exit $rc
+for r in 1 2; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --no-profile > gpurun_out/ab.json 2> gpurun_out/ab.err
+  rc=$?; echo "bench rc=$rc $(python -c "import json;d=json.load(open('gpurun_out/ab.json'));print(d['ms_per_step'],d['value'])")"
+  [ $rc -eq 0 ] || exit $rc
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_q -o run --output-format csv -- \
+  python bench.py --no-cpu-baseline --steps 5 --warmup 2 --no-profile > gpurun_out/prof_q.log 2>&1
+echo "rocprof rc=$?"
