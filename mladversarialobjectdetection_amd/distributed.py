@@ -3,10 +3,11 @@
 One process per GPU (torchrun; backend "nccl" = RCCL over xGMI on ROCm, "gloo" on CPU for tests).
 The global batch is split contiguously: rank r holds global images [r*B, (r+1)*B), which also keys
 the EOT RNG, so every image sees the same random draws at any GPU count.  Exactly one exchange per
-step: a SUM all-reduce of the contiguous [d patch | d scale] buffer (PHX_NPARAM floats = 4.9 MB)
-between the victim dgrad and the Adam update; the 1e-5*TV term is added by rank 0 only, so the
-reduced gradient equals the sum of per-shard reference gradients (bn=local: BN statistics per
-shard).  Metrics add one 8-float all-reduce.
+step: a SUM all-reduce of the contiguous [d patch | d scale | metric row] buffer (4.9 MB) between
+the victim dgrad and the Adam update; the 1e-5*TV term (and its metric) is added by rank 0 only, so
+the reduced gradient equals the sum of per-shard reference gradients (bn=local: BN statistics per
+shard), and reading the metrics issues no further collective.  The defender reduces
+[d U-Net variables | loss] the same way.
 """
 from __future__ import annotations
 
