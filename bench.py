@@ -156,7 +156,9 @@ def main():
     from mladversarialobjectdetection_amd import distributed as ddp
     ddp.init_from_env()
     rank, world = ddp.rank(), ddp.world()
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; ranks beyond the visible GPUs share them (a rehearsal of the N>1 path on a
+    # one-GPU box with PHX_DIST_BACKEND=gloo — never the case on a real node)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

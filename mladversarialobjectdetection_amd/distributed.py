@@ -48,7 +48,8 @@ def init_from_env(backend: str | None = None):
     if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
         return
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # PHX_DIST_BACKEND=gloo: CUDA tensors reduced through the host (tests / one-GPU rehearsals)
+        backend = os.environ.get("PHX_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
