@@ -448,7 +448,27 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
       const SpanEntry si = sp[i0 + ii];
       const float* col = m + (long)(xlo + xo) * 3;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-      for (int y = si.start; y < si.end; ++y) {
+      // 4 source rows' loads in flight before any is accumulated (a load-then-add loop waits one
+      // L2 / MALL round trip per source row); the accumulation order is unchanged
+      int y = si.start;
+      for (; y + 4 <= si.end; y += 4) {
+        float q[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float* qq = col + (long)(y + u) * d.P * 3;
+          q[u][0] = qq[0];
+          q[u][1] = qq[1];
+          q[u][2] = qq[2];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float wy = span_weight(si, y + u, one_over_k);
+          a0 += wy * q[u][0];
+          a1 += wy * q[u][1];
+          a2 += wy * q[u][2];
+        }
+      }
+      for (; y < si.end; ++y) {
         const float wy = span_weight(si, y, one_over_k);
         const float* q = col + (long)y * d.P * 3;
         a0 += wy * q[0];
@@ -677,24 +697,38 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd_cols(EotDims d, const Bo
                                                              float* __restrict__ dmatched) {
   const int b = blockIdx.y;
   const long npx = (long)d.P * d.P;
-  long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npx) return;
-  const int y = (int)(p / d.P), x = (int)(p % d.P);
+  const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const ListView L = lists_of(d, place);
-  const int n = L.img_n[b], f = L.img_first[b];
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-  for (int q = 0; q < n; ++q) {
+  const int n = L.img_n[b], f = L.img_first[b];  // <= d.maxb <= PHX_MAX_OUT (launcher)
+  // the image's boxes, resolved once per workgroup (a lane walking vlist -> place -> spans per box
+  // paid two dependent global round trips per box before its own loads)
+  __shared__ int s_ps[PHX_MAX_OUT];
+  __shared__ long s_span[PHX_MAX_OUT], s_u[PHX_MAX_OUT];
+  __shared__ float s_inv[PHX_MAX_OUT], s_ks[PHX_MAX_OUT], s_ok[PHX_MAX_OUT];
+  for (int q = threadIdx.x; q < n; q += blockDim.x) {
     const int v = f + q;
     const int sl = L.vlist[v];
-    const BoxPlace& P = place[sl];
-    const float scale = (float)P.ps / (float)d.P;
+    const int ps = place[sl].ps;
+    const float scale = (float)ps / (float)d.P;
     const float inv_scale = (float)(1.0 / (double)scale);
     const float ks = fmaxf(inv_scale, 1.0f);
-    const float one_over_k = 1.0f / ks;
-    const SpanEntry* sp = spans + (long)sl * d.span_stride;
+    s_ps[q] = ps;
+    s_span[q] = (long)sl * d.span_stride;
+    s_u[q] = (long)L.tprefix[v] * kResizeRT * d.P * 3;
+    s_inv[q] = inv_scale;
+    s_ks[q] = ks;
+    s_ok[q] = 1.0f / ks;
+  }
+  __syncthreads();
+  if (p >= npx) return;
+  const int y = (int)(p / d.P), x = (int)(p % d.P);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  for (int q = 0; q < n; ++q) {
+    const SpanEntry* sp = spans + s_span[q];
+    const float one_over_k = s_ok[q];
     int ilo, ihi;
-    adj_range(y, inv_scale, ks, P.ps, &ilo, &ihi);
-    const float* U = tstore + (long)L.tprefix[v] * kResizeRT * d.P * 3 + (long)x * 3;
+    adj_range(y, s_inv[q], s_ks[q], s_ps[q], &ilo, &ihi);
+    const float* U = tstore + s_u[q] + (long)x * 3;
     for (int i = ilo; i <= ihi; ++i) {
       const SpanEntry si = sp[i];
       if (y < si.start || y >= si.end) continue;
@@ -711,6 +745,7 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd_cols(EotDims d, const Bo
 
 void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEntry* spans,
                            const float* dstore, float* tstore, float* dmatched, hipStream_t s) {
+  if (d.maxb > PHX_MAX_OUT) throw std::runtime_error("eot resize backward: more box slots than PHX_MAX_OUT");
   hipLaunchKernelGGL(k_eot_resize_bwd_rows, dim3(kBoxGrid), dim3(256), 0, s, d, place, spans, dstore,
                      tstore);
   PHX_LAUNCH_CHECK();
