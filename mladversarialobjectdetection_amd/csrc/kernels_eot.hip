@@ -691,12 +691,16 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd_rows(EotDims d, const Bo
   }
 }
 
+// PX source pixels per lane, P/PX apart in one row: they share the row's boxes, spans and weights,
+// and their U loads are independent (PX chains of loads in flight per lane instead of one)
+template <int PX>
 __global__ __launch_bounds__(256) void k_eot_resize_bwd_cols(EotDims d, const BoxPlace* __restrict__ place,
                                                              const SpanEntry* __restrict__ spans,
                                                              const float* __restrict__ tstore,
                                                              float* __restrict__ dmatched) {
   const int b = blockIdx.y;
   const long npx = (long)d.P * d.P;
+  const int pw = d.P / PX;  // lanes per row
   const long p = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const ListView L = lists_of(d, place);
   const int n = L.img_n[b], f = L.img_first[b];  // <= d.maxb <= PHX_MAX_OUT (launcher)
@@ -720,27 +724,42 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd_cols(EotDims d, const Bo
     s_ok[q] = 1.0f / ks;
   }
   __syncthreads();
-  if (p >= npx) return;
-  const int y = (int)(p / d.P), x = (int)(p % d.P);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+  if (p >= (long)d.P * pw) return;
+  const int y = (int)(p / pw), x0 = (int)(p % pw);
+  float a[PX][3];
+#pragma unroll
+  for (int k = 0; k < PX; ++k) a[k][0] = a[k][1] = a[k][2] = 0.f;
   for (int q = 0; q < n; ++q) {
     const SpanEntry* sp = spans + s_span[q];
     const float one_over_k = s_ok[q];
     int ilo, ihi;
     adj_range(y, s_inv[q], s_ks[q], s_ps[q], &ilo, &ihi);
-    const float* U = tstore + s_u[q] + (long)x * 3;
+    const float* U = tstore + s_u[q] + (long)x0 * 3;
     for (int i = ilo; i <= ihi; ++i) {
       const SpanEntry si = sp[i];
       if (y < si.start || y >= si.end) continue;
       const float wy = span_weight(si, y, one_over_k);
       const float* g = U + (long)i * d.P * 3;
-      a0 += wy * g[0];
-      a1 += wy * g[1];
-      a2 += wy * g[2];
+      float v[PX][3];
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        v[k][0] = g[(long)k * pw * 3 + 0];
+        v[k][1] = g[(long)k * pw * 3 + 1];
+        v[k][2] = g[(long)k * pw * 3 + 2];
+      }
+#pragma unroll
+      for (int k = 0; k < PX; ++k) {
+        a[k][0] += wy * v[k][0];
+        a[k][1] += wy * v[k][1];
+        a[k][2] += wy * v[k][2];
+      }
     }
   }
-  float* o = dmatched + ((long)b * npx + p) * 3;
-  o[0] = a0; o[1] = a1; o[2] = a2;
+#pragma unroll
+  for (int k = 0; k < PX; ++k) {
+    float* o = dmatched + ((long)b * npx + (long)y * d.P + x0 + (long)k * pw) * 3;
+    o[0] = a[k][0]; o[1] = a[k][1]; o[2] = a[k][2];
+  }
 }
 
 void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEntry* spans,
@@ -749,8 +768,12 @@ void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEn
   hipLaunchKernelGGL(k_eot_resize_bwd_rows, dim3(kBoxGrid), dim3(256), 0, s, d, place, spans, dstore,
                      tstore);
   PHX_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_eot_resize_bwd_cols, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d,
-                     place, spans, tstore, dmatched);
+  if (d.P % 4 == 0)
+    hipLaunchKernelGGL(k_eot_resize_bwd_cols<4>, dim3(cdiv((long)d.P * d.P / 4, 256), d.B), dim3(256), 0, s, d,
+                       place, spans, tstore, dmatched);
+  else
+    hipLaunchKernelGGL(k_eot_resize_bwd_cols<1>, dim3(cdiv((long)d.P * d.P, 256), d.B), dim3(256), 0, s, d,
+                       place, spans, tstore, dmatched);
   PHX_LAUNCH_CHECK();
 }
 
