@@ -448,20 +448,20 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
       const SpanEntry si = sp[i0 + ii];
       const float* col = m + (long)(xlo + xo) * 3;
       float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-      // 4 source rows' loads in flight before any is accumulated (a load-then-add loop waits one
+      // 8 source rows' loads in flight before any is accumulated (a load-then-add loop waits one
       // L2 / MALL round trip per source row); the accumulation order is unchanged
       int y = si.start;
-      for (; y + 4 <= si.end; y += 4) {
-        float q[4][3];
+      for (; y + 8 <= si.end; y += 8) {
+        float q[8][3];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const float* qq = col + (long)(y + u) * d.P * 3;
           q[u][0] = qq[0];
           q[u][1] = qq[1];
           q[u][2] = qq[2];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const float wy = span_weight(si, y + u, one_over_k);
           a0 += wy * q[u][0];
           a1 += wy * q[u][1];
