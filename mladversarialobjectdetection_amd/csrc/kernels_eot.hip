@@ -443,40 +443,57 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
     const float one_over_k = 1.0f / fmaxf(inv_scale, 1.0f);
     const int xlo = sp[0].start, nx = sp[P.ps - 1].end - xlo;
     const float* m = matched + (long)b * d.P * d.P * 3;
-    for (int e = threadIdx.x; e < ni * nx; e += blockDim.x) {
-      const int ii = e / nx, xo = e - ii * nx;
+    // two columns per lane (xa and xa + h2 of the same output row: one span, two independent
+    // chains of loads), 8 source rows' loads in flight per chain before any is accumulated; the
+    // accumulation order of each output value is unchanged
+    const int h2 = (nx + 1) >> 1;
+    for (int e2 = threadIdx.x; e2 < ni * h2; e2 += blockDim.x) {
+      const int ii = e2 / h2, xa = e2 - ii * h2, xb = xa + h2;
+      const bool okb = xb < nx;
       const SpanEntry si = sp[i0 + ii];
-      const float* col = m + (long)(xlo + xo) * 3;
-      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
-      // 8 source rows' loads in flight before any is accumulated (a load-then-add loop waits one
-      // L2 / MALL round trip per source row); the accumulation order is unchanged
+      const float* ca = m + (long)(xlo + xa) * 3;
+      const float* cb = m + (long)(xlo + (okb ? xb : xa)) * 3;
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
       int y = si.start;
       for (; y + 8 <= si.end; y += 8) {
-        float q[8][3];
+        float qa[8][3], qb[8][3];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-          const float* qq = col + (long)(y + u) * d.P * 3;
-          q[u][0] = qq[0];
-          q[u][1] = qq[1];
-          q[u][2] = qq[2];
+          const long ro = (long)(y + u) * d.P * 3;
+          qa[u][0] = ca[ro + 0];
+          qa[u][1] = ca[ro + 1];
+          qa[u][2] = ca[ro + 2];
+          qb[u][0] = cb[ro + 0];
+          qb[u][1] = cb[ro + 1];
+          qb[u][2] = cb[ro + 2];
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const float wy = span_weight(si, y + u, one_over_k);
-          a0 += wy * q[u][0];
-          a1 += wy * q[u][1];
-          a2 += wy * q[u][2];
+          a0 += wy * qa[u][0];
+          a1 += wy * qa[u][1];
+          a2 += wy * qa[u][2];
+          b0 += wy * qb[u][0];
+          b1 += wy * qb[u][1];
+          b2 += wy * qb[u][2];
         }
       }
       for (; y < si.end; ++y) {
         const float wy = span_weight(si, y, one_over_k);
-        const float* q = col + (long)y * d.P * 3;
-        a0 += wy * q[0];
-        a1 += wy * q[1];
-        a2 += wy * q[2];
+        const long ro = (long)y * d.P * 3;
+        a0 += wy * ca[ro + 0];
+        a1 += wy * ca[ro + 1];
+        a2 += wy * ca[ro + 2];
+        b0 += wy * cb[ro + 0];
+        b1 += wy * cb[ro + 1];
+        b2 += wy * cb[ro + 2];
       }
-      float* o = V + e * 3;
+      float* o = V + (ii * nx + xa) * 3;
       o[0] = a0; o[1] = a1; o[2] = a2;
+      if (okb) {
+        float* ob = V + (ii * nx + xb) * 3;
+        ob[0] = b0; ob[1] = b1; ob[2] = b2;
+      }
     }
     __syncthreads();
     for (int e = threadIdx.x; e < ni * P.ps; e += blockDim.x) {
