@@ -554,22 +554,46 @@ __global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* _
                                                        int16_t* __restrict__ owner,
                                                        float* __restrict__ mask) {
   const long npx = (long)d.H * d.W;
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // when a workgroup's pixels lie in one image (always for the image sizes the models use), its
+  // boxes' extents are staged in LDS once (a pixel walking vlist -> place per box paid two
+  // dependent global round trips per box); otherwise each lane reads them itself
+  const ListView L = lists_of(d, place);
+  const long first = (long)blockIdx.x * blockDim.x;
+  const long last = min(first + (long)blockDim.x, (long)d.B * npx) - 1;
+  const bool staged = first / npx == last / npx;
+  __shared__ int s_sl[PHX_MAX_OUT], s_y0[PHX_MAX_OUT], s_x0[PHX_MAX_OUT], s_dg[PHX_MAX_OUT];
+  if (staged) {
+    const int b0 = (int)(first / npx);
+    const int n0 = L.img_n[b0], f0 = L.img_first[b0];  // <= d.maxb <= PHX_MAX_OUT (launcher)
+    for (int q = threadIdx.x; q < n0; q += blockDim.x) {
+      const int sl = L.vlist[f0 + q];
+      s_sl[q] = sl;
+      s_y0[q] = place[sl].ymin;
+      s_x0[q] = place[sl].xmin;
+      s_dg[q] = place[sl].diag;
+    }
+    __syncthreads();
+  }
   if (idx >= (long)d.B * npx) return;
   const int b = (int)(idx / npx);
+  const int n = L.img_n[b], f = L.img_first[b];
   const int p = (int)(idx % npx);
   const int y = p / d.W, x = p % d.W;
-  const ListView L = lists_of(d, place);
   const float* ip = img_in + idx * 3;
   float v[3] = {ip[0], ip[1], ip[2]};
   int16_t own[3] = {-1, -1, -1};
   bool covered = false;
-  const int n = L.img_n[b], f = L.img_first[b];
   for (int q = 0; q < n; ++q) {
-    const int sl = L.vlist[f + q];
+    int sl, y0, x0, dg;
+    if (staged) {
+      sl = s_sl[q]; y0 = s_y0[q]; x0 = s_x0[q]; dg = s_dg[q];
+    } else {
+      sl = L.vlist[f + q]; y0 = place[sl].ymin; x0 = place[sl].xmin; dg = place[sl].diag;
+    }
+    const int qy = y - y0, qx = x - x0;
+    if (qy < 0 || qy >= dg || qx < 0 || qx >= dg) continue;
     const BoxPlace& P = place[sl];
-    const int qy = y - P.ymin, qx = x - P.xmin;
-    if (qy < 0 || qy >= P.diag || qx < 0 || qx >= P.diag) continue;
     covered = true;
     const float ox = (float)qx, oy = (float)qy;
     const float proj = 0.0f * ox + 0.0f * oy + 1.0f;
@@ -606,6 +630,7 @@ void launch_eot_composite(const EotDims& d, const float* img_in, const BoxPlace*
                           const float* rstore, float* img_out, int16_t* owner, hipStream_t s,
                           float* mask) {
   long n = (long)d.B * d.H * d.W;
+  if (d.maxb > PHX_MAX_OUT) throw std::runtime_error("eot composite: more box slots than PHX_MAX_OUT");
   hipLaunchKernelGGL(k_eot_composite, dim3(cdiv(n, 256)), dim3(256), 0, s, d, img_in, place, rstore,
                      img_out, owner, mask);
   PHX_LAUNCH_CHECK();
