@@ -239,6 +239,7 @@ typedef struct phx_def phx_def;
  * Dropout's Philox draws */
 int phx_def_create(phx_ctx* victim, int max_batch, uint64_t seed, phx_def** out);
 void phx_def_destroy(phx_def* d);
+/* d == NULL: the message of this thread's last failed phx_def_create. */
 const char* phx_def_last_error(phx_def* d);
 int64_t phx_def_num_params(phx_def* d);
 int64_t phx_def_num_moving(phx_def* d);

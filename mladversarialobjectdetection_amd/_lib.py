@@ -216,7 +216,8 @@ class Defender:
         h = c_void_p()
         rc = self.lib.phx_def_create(ctx.h, int(max_batch), int(seed) & ((1 << 64) - 1), ctypes.byref(h))
         if rc != 0:
-            raise PhxError(f"phx_def_create failed ({rc})")
+            msg = self.lib.phx_def_last_error(None)
+            raise PhxError(f"phx_def_create failed ({rc}): {msg.decode() if msg else ''}")
         self.h = h
         self.max_batch = int(max_batch)
         self.num_params = int(self.lib.phx_def_num_params(h))

@@ -54,18 +54,24 @@ class VictimConfig:
     mean_rgb: list
     stddev_rgb: list
     nms_configs: NmsConfig = field(default_factory=NmsConfig)
+    # the library context this config describes (set by EfficientDetVictim): overrides that change
+    # the computation are forwarded to it, as the reference's model.config.override reaches the model
+    ctx: object = field(default=None, repr=False, compare=False)
 
     def override(self, d: dict, ctx=None):
         """Config.override (hparams_config.py:91-109) for the keys the attack uses.  The values that
         change the computation are forwarded to the library context (score_thresh); overrides the
         library does not implement raise instead of diverging silently from the reference."""
+        ctx = ctx if ctx is not None else self.ctx
         for k, v in d.items():
             if k != "nms_configs":
                 raise ValueError(f"config_override: unsupported key {k!r} (only nms_configs)")
             for kk, vv in v.items():
                 if kk == "score_thresh":
-                    if ctx is not None:
-                        ctx.set_score_thresh(float(vv))
+                    if ctx is None:
+                        raise ValueError("config_override: score_thresh needs the victim's library context "
+                                         "(a VictimConfig not owned by an EfficientDetVictim)")
+                    ctx.set_score_thresh(float(vv))
                 elif kk == "iou_thresh":
                     pass  # unused by the gaussian method: iou_thresh = 1.0 (postprocess.py:184-188)
                 elif kk == "method" and vv != "gaussian":
@@ -110,7 +116,7 @@ class EfficientDetVictim:
         self.load_weights(blob)
         fam = "lite" if "lite" in model_name else "efficientdet"
         self.config = VictimConfig(model_name, self.ctx.image_size, MEAN_RGB[fam], STDDEV_RGB[fam],
-                                   NmsConfig(score_thresh=score_thresh))
+                                   NmsConfig(score_thresh=score_thresh), ctx=self.ctx)
         self.num_anchors = self.ctx.num_anchors
         self.max_batch = max_batch
 
@@ -388,7 +394,10 @@ class PatchAttacker:
         n, scale = float(v[_lib.M_NIMG]), float(v[_lib.NMETRIC])
         mean = v[_lib.M_SUM_M] / n
         var = max(v[_lib.M_SUM_M2] / n - mean * mean, 0.0)
-        asr = 1.0 - v[_lib.M_ASR_NUM] / (v[_lib.M_ASR_DEN] + 1e-7)
+        # calc_asr (attacker.py:253-255) divides tf.size of the flattened ragged [n,4] boxes, 4
+        # floats per box, in float32: 1 - 4n / (4d + epsilon)
+        asr = float(np.float32(1.0) - np.float32(4.0 * v[_lib.M_ASR_NUM])
+                    / (np.float32(4.0 * v[_lib.M_ASR_DEN]) + np.float32(1e-7)))
         return {"loss": float(v[_lib.M_LOSS]), "scale": scale, "scale_loss": float(v[_lib.M_SCALE_LOSS]),
                 "tv_loss": float(v[_lib.M_TV]), "mean_max_score": mean, "std_max_score": math.sqrt(var),
                 "asr": asr, "asr_to_scale": asr / scale if scale else float("inf"),

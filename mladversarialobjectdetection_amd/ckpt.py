@@ -27,6 +27,7 @@ writer emits is read: uncompressed blocks, float32 / float16 / bfloat16 / float6
 from __future__ import annotations
 
 import os
+import re
 import struct
 
 import numpy as np
@@ -270,10 +271,20 @@ def latest_checkpoint(directory: str) -> str:
                 if line.startswith("model_checkpoint_path:"):
                     p = line.split(":", 1)[1].strip().strip('"')
                     return p if os.path.isabs(p) else os.path.join(directory, p)
-    idx = sorted(n[:-6] for n in os.listdir(directory) if n.endswith(".index"))
+    idx = [n[:-6] for n in os.listdir(directory) if n.endswith(".index")]
     if not idx:
         raise FileNotFoundError(f"no checkpoint in {directory}")
-    return os.path.join(directory, idx[-1])
+    if len(idx) == 1:
+        return os.path.join(directory, idx[0])
+    # no `checkpoint` file and several prefixes: the newest is the one with the largest trailing
+    # step number (`model.ckpt-10` after `model.ckpt-9`); refuse to guess when they have none
+    steps = {}
+    for n in idx:
+        m = re.search(r"-(\d+)$", n)
+        if m is None:
+            raise FileNotFoundError(f"{directory}: several checkpoints {sorted(idx)} and no `checkpoint` file")
+        steps[n] = int(m.group(1))
+    return os.path.join(directory, max(idx, key=lambda n: steps[n]))
 
 
 # ---------------------------------------------------------------------------------------------
@@ -308,8 +319,12 @@ def _put_block(f, content: bytes) -> bytes:
     return _enc_varint(off) + _enc_varint(len(content))
 
 
-def write_checkpoint(prefix: str, tensors: dict, block_entries: int = 64):
-    """Write float32 tensors as a single-shard tensor bundle (<prefix>.index + .data-00000-of-00001)."""
+def write_checkpoint(prefix: str, tensors: dict, block_entries: int = 64, update_latest: bool | None = None):
+    """Write float32 tensors as a single-shard tensor bundle (<prefix>.index + .data-00000-of-00001).
+
+    update_latest: rewrite the directory's `checkpoint` file to point at this prefix.  None (the
+    default) writes it only when the directory has none, so exporting into an existing checkpoint
+    directory never silently redirects its latest pointer."""
     os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
     names = sorted(tensors)
     entries = []
@@ -334,8 +349,12 @@ def write_checkpoint(prefix: str, tensors: dict, block_entries: int = 64):
         footer = meta + ih
         footer += b"\x00" * (_FOOTER - 8 - len(footer)) + struct.pack("<Q", _TABLE_MAGIC)
         f.write(footer)
-    with open(os.path.join(os.path.dirname(os.path.abspath(prefix)), "checkpoint"), "w") as f:
-        f.write(f'model_checkpoint_path: "{os.path.basename(prefix)}"\n')
+    cp = os.path.join(os.path.dirname(os.path.abspath(prefix)), "checkpoint")
+    if update_latest is None:
+        update_latest = not os.path.exists(cp)
+    if update_latest:
+        with open(cp, "w") as f:
+            f.write(f'model_checkpoint_path: "{os.path.basename(prefix)}"\n')
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1289,6 +1289,9 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0) {
   Scope scope(ctx, "pre_nms", 0.0,
               (double)E.B * ctx->A * (ctx->mc.num_classes + 4 + 4 + 6) * 4.0, s);
   const float S = (float)ctx->mc.image_size;
+  // every list starts empty: a step that failed between a pre_nms and its run_nms (which
+  // normally resets the counts) must not leave stale candidates for the next soft-NMS
+  if (cand_mask) PHX_HIP(hipMemsetAsync(E.cand_count, 0, (size_t)E.B * sizeof(int), s));
   launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
                  ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->filter_thresh,

@@ -510,8 +510,16 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
 
 extern "C" {
 
+namespace {
+thread_local std::string g_def_create_err;  // phx_def_last_error(NULL): the last failed phx_def_create
+}
+
 int phx_def_create(phx_ctx* victim, int max_batch, uint64_t seed, phx_def** out) {
-  if (!victim || !out || max_batch <= 0) return PHX_EINVAL;
+  g_def_create_err.clear();
+  if (!victim || !out || max_batch <= 0) {
+    g_def_create_err = "phx_def_create: null victim / output pointer or max_batch <= 0";
+    return PHX_EINVAL;
+  }
   *out = nullptr;
   phx_def* d = nullptr;
   DEF_TRY
@@ -538,14 +546,14 @@ int phx_def_create(phx_ctx* victim, int max_batch, uint64_t seed, phx_def** out)
   }
   catch (const std::exception& e) {
     delete d;
-    (void)e;
-    return PHX_EINVAL;
+    g_def_create_err = std::string("phx_def_create: ") + e.what();
+    return dynamic_cast<const HipError*>(&e) ? PHX_EHIP : PHX_EINVAL;
   }
 }
 
 void phx_def_destroy(phx_def* d) { delete d; }
 
-const char* phx_def_last_error(phx_def* d) { return d ? d->err.c_str() : "null defender"; }
+const char* phx_def_last_error(phx_def* d) { return d ? d->err.c_str() : g_def_create_err.c_str(); }
 
 int64_t phx_def_num_params(phx_def* d) { return d ? d->nparams : -1; }
 int64_t phx_def_num_moving(phx_def* d) { return d ? d->nmoving : -1; }

@@ -92,10 +92,19 @@ class PatchAttackDefender:
         return {p["name"]: self.params[p["offset"]:p["offset"] + int(np.prod(p["shape"]))].view(*p["shape"])
                 for p in self.manifest["params"]}
 
-    def moving_statistics(self) -> np.ndarray:
-        out = np.empty(self.handle.num_moving, np.float32)
-        self.handle.call("phx_def_moving", out.ctypes.data, None, None)
-        return out
+    def moving_statistics(self, replica_mean: bool = False) -> np.ndarray:
+        """The U-Net BN moving mean / variance.  Each rank updates its own copy from its shard (as
+        each replica of a Keras MirroredStrategy does).  replica_mean=True returns what Keras reads
+        from those ON_READ/MEAN variables — the mean over ranks — through one SUM all-reduce, so
+        every rank must call it at the same point."""
+        if not (replica_mean and ddp.is_dist()):
+            out = np.empty(self.handle.num_moving, np.float32)
+            self.handle.call("phx_def_moving", out.ctypes.data, None, None)
+            return out
+        t = torch.empty(self.handle.num_moving, device=self.params.device)
+        self.handle.call("phx_def_moving", t.data_ptr(), None, _stream())
+        ddp.allreduce_sum_(t)
+        return (t / ddp.world()).cpu().numpy()
 
     def call(self, images, *, training=True, boxes=None):
         """PatchAttackDefender.call(images, training=True) (attack_detection.py:168-206): returns the
@@ -155,10 +164,14 @@ class PatchAttackDefender:
 
     def save_weights(self, dirpath, **kwargs):
         """attack_detection.py:300-308 saves antipatch.h5; h5py is not available here, so the same
-        variables go to antipatch.npz under their Keras names (plus the BN moving statistics)."""
+        variables go to antipatch.npz under their Keras names (plus the BN moving statistics, as
+        their mean over ranks).  Under data parallelism every rank calls it (the moving statistics
+        are all-reduced) and rank 0 writes the file."""
+        mv = self.moving_statistics(replica_mean=True)
+        if ddp.rank() != 0:
+            return
         os.makedirs(dirpath)
         arrs = {k: v.detach().cpu().numpy() for k, v in self._trainable_variables.items()}
-        mv = self.moving_statistics()
         for b in self.manifest["bn"]:
             arrs[b["name"] + "/moving_mean"] = mv[b["moving_mean"]:b["moving_mean"] + b["channels"]]
             arrs[b["name"] + "/moving_variance"] = mv[b["moving_variance"]:b["moving_variance"] + b["channels"]]

@@ -21,8 +21,13 @@ import math
 import numpy as np
 
 
-def synthetic_blob(manifest, seed: int = 0, person_bias: float = 0.0) -> np.ndarray:
-    """Return the float32 weight blob for `manifest` (list of {name, shape, offset, kind})."""
+def synthetic_blob(manifest, seed: int = 0, person_bias: float = 0.0, gamma=(0.5, 1.5),
+                   beta=(0.0, 0.1)) -> np.ndarray:
+    """Return the float32 weight blob for `manifest` (list of {name, shape, offset, kind}).
+
+    gamma = (lo, hi) of the BN scale's uniform draw, beta = (mean, std) of the BN shift's normal
+    draw.  The defaults are SURVEY.md 8(d)'s; a narrower gamma with a positive beta keeps most
+    relu6 inputs inside (0, 6), away from the kinks (a well-conditioned lite point for parity)."""
     total = 0
     for e in manifest:
         total = max(total, e["offset"] + int(np.prod(e["shape"])))
@@ -52,9 +57,9 @@ def synthetic_blob(manifest, seed: int = 0, person_bias: float = 0.0) -> np.ndar
             else:
                 v = rng.normal(0.0, 0.05, size=n)
         elif kind == "gamma":
-            v = rng.uniform(0.5, 1.5, size=n)
+            v = rng.uniform(gamma[0], gamma[1], size=n)
         elif kind == "beta":
-            v = rng.normal(0.0, 0.1, size=n)
+            v = rng.normal(beta[0], beta[1], size=n)
         elif kind == "moving_mean":
             v = rng.normal(0.0, 0.1, size=n)
         elif kind == "moving_variance":

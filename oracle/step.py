@@ -48,6 +48,15 @@ def asr_counts(first, second):
     return num, den
 
 
+def calc_asr(num, den, coords=4):
+    """calc_asr's value (attacker.py:253-255): 1 - tf.size(boxes_pred_filt.flat_values) /
+    (tf.size(labels_filt.flat_values) + epsilon), in float32.  The ragged boxes are [B,(n),4], so
+    each size counts 4 floats per box: 1 - 4n / (4d + 1e-7) (Keras epsilon 1e-7)."""
+    n = np.float32(coords * num)
+    d = np.float32(coords * den) + np.float32(1e-7)
+    return float(np.float32(1.0) - n / d)
+
+
 def attack_step(weights, images, patch, scale, boxes=None, seed=0, step=0, gimg0=0,
                 model="efficientdet-d0", image_size=None, add_tv=True, score_thresh=0.5,
                 dtype=torch.float64, training=True, image_grad=False, bn_frozen=False, bf16=False):

@@ -16,3 +16,28 @@ def pytest_configure(config):
 def d0_manifest():
     from mladversarialobjectdetection_amd import _lib
     return _lib.Context("efficientdet-d0").manifest()
+
+
+def pytest_sessionstart(session):
+    """PHX_HEARTBEAT=<file> (or "stderr"): a line every 30 s while the session runs, so a long
+    oracle comparison (minutes of fp64 CPU work inside one test) is not mistaken for a hung GPU
+    job."""
+    path = os.environ.get("PHX_HEARTBEAT")
+    if not path:
+        return
+    import threading
+    import time
+
+    def beat():
+        t0 = time.time()
+        while True:
+            time.sleep(30)
+            line = f"alive {time.time() - t0:.0f}s\n"
+            if path == "stderr":
+                sys.__stderr__.write(line)
+                sys.__stderr__.flush()
+            else:
+                with open(path, "a") as f:
+                    f.write(line)
+
+    threading.Thread(target=beat, daemon=True).start()

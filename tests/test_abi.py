@@ -60,3 +60,62 @@ def test_errors_without_gpu_work():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(_lib.PhxError):
         _lib.load(str(tmp_path / "libphx.so"))
+
+
+_CTYPES = {"const char*": ctypes.c_char_p, "int": ctypes.c_int, "float": ctypes.c_float,
+           "uint64_t": ctypes.c_uint64}
+
+
+def header_config_fields():
+    """(name, ctype) of `typedef struct phx_config` in include/phx.h, in declaration order."""
+    src = open(os.path.join(ROOT, "include", "phx.h")).read()
+    body = re.search(r"typedef struct phx_config \{(.*?)\} phx_config;", src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    out = []
+    for decl in body.split(";"):
+        decl = " ".join(decl.split())
+        if decl:
+            typ, name = decl.rsplit(" ", 1)
+            out.append((name, _CTYPES[typ]))
+    return out
+
+
+def header_define(name):
+    src = open(os.path.join(ROOT, "include", "phx.h")).read()
+    return int(re.search(rf"\b{name}\s*=\s*(\d+)", src).group(1))
+
+
+def integration_stub():
+    """The ctypes stub of INTEGRATION.md §2 as text."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = doc[doc.index("## 2."):]
+    return re.search(r"```python\n(.*?)```", sec, re.S).group(1)
+
+
+def test_integration_stub_matches_header_and_binding():
+    """The binding a reference maintainer copies from INTEGRATION.md must agree with phx.h and
+    _lib.py: phx_config's fields (name, type, order, sizeof), the metric-row length the library
+    writes, and the argtypes of every entry point the stub binds."""
+    stub = integration_stub()
+    ns = {k: getattr(ctypes, k) for k in dir(ctypes) if k.startswith("c_") or k == "POINTER"}
+    fields = eval(re.search(r"_fields_ = (\[.*?\])\n", stub, re.S).group(1), ns)
+    hdr = header_config_fields()
+    assert [f[0] for f in fields] == [h[0] for h in hdr] == [f[0] for f in _lib._Config._fields_]
+    assert [f[1] for f in fields] == [h[1] for h in hdr] == [f[1] for f in _lib._Config._fields_]
+    Stub = type("phx_config", (ctypes.Structure,), {"_fields_": fields})
+    assert ctypes.sizeof(Stub) == ctypes.sizeof(_lib._Config)
+    # the example constructor passes one value per field
+    call = re.search(r"cfg = phx_config\((.*?)\)\n", stub).group(1)
+    assert len(call.split(",")) == len(hdr)
+    # metric row: the stub allocates what the library writes
+    nmetric = int(re.search(r"PHX_NMETRIC = (\d+)", stub).group(1))
+    assert nmetric == header_define("PHX_NMETRIC") == _lib.NMETRIC
+    assert re.search(r"metrics = torch\.zeros\(PHX_NMETRIC\b", stub)
+    assert eval(re.search(r"PHX_NPARAM = ([^#\n]+)", stub).group(1)) == _lib.NPARAM
+    # argtypes of every function the stub binds
+    sigs = {n: (r, a) for n, r, a in _lib._SIGS}
+    bound = re.findall(r"lib\.(phx_\w+)\.argtypes = (\[.*?\])\n", stub, re.S)
+    ns["phx_config"] = _lib._Config  # layouts shown equal above
+    assert len(bound) >= 4
+    for name, args in bound:
+        assert eval(args, ns) == sigs[name][1], name

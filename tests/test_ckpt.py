@@ -115,3 +115,28 @@ def test_many_blocks_and_shared_prefixes(tmp_path):
     assert sorted(r.entries) == sorted(t)
     for k in list(t)[::37]:
         np.testing.assert_array_equal(r.get_tensor(k), t[k])
+
+
+def test_latest_checkpoint_without_pointer_file(tmp_path):
+    """No `checkpoint` file: the largest trailing step wins (model.ckpt-10 after -9), and several
+    prefixes without step numbers are refused rather than guessed."""
+    a = {"a/kernel": np.ones((1,), np.float32)}
+    for step in (9, 10, 2):
+        C.write_checkpoint(str(tmp_path / f"model.ckpt-{step}"), a, update_latest=False)
+    assert not (tmp_path / "checkpoint").exists()
+    assert C.latest_checkpoint(str(tmp_path)) == str(tmp_path / "model.ckpt-10")
+    other = tmp_path / "other"
+    C.write_checkpoint(str(other / "x"), a, update_latest=False)
+    assert C.latest_checkpoint(str(other)) == str(other / "x")      # a single prefix is unambiguous
+    C.write_checkpoint(str(other / "y"), a, update_latest=False)
+    with pytest.raises(FileNotFoundError):
+        C.latest_checkpoint(str(other))
+
+
+def test_export_keeps_an_existing_latest_pointer(tmp_path):
+    a = {"a/kernel": np.ones((1,), np.float32)}
+    C.write_checkpoint(str(tmp_path / "model.ckpt-5"), a)           # no pointer yet: written
+    C.write_checkpoint(str(tmp_path / "export"), a)                 # pointer exists: kept
+    assert C.latest_checkpoint(str(tmp_path)) == str(tmp_path / "model.ckpt-5")
+    C.write_checkpoint(str(tmp_path / "export"), a, update_latest=True)
+    assert C.latest_checkpoint(str(tmp_path)) == str(tmp_path / "export")

@@ -100,5 +100,5 @@ def test_metric_row_is_sum_reducible():
     assert d["mean_max_score"] == pytest.approx(allm.mean())
     assert d["std_max_score"] == pytest.approx(allm.std())  # tf.math.reduce_std: population std
     assert d["tv_loss"] == 123.0
-    assert d["asr"] == pytest.approx(1 - 1 / (5 + 1e-7))
+    assert d["asr"] == pytest.approx(1 - 4 / (20 + 1e-7))  # calc_asr counts 4 floats per box
     assert d["loss"] == pytest.approx((allm ** 2).sum() + ((allm - 0.4) ** 2).sum() + 1e-5 * 123)

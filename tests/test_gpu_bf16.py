@@ -113,20 +113,80 @@ def test_bf16_step_matches_oracle():
     assert _cos(gp, rem["grad"][:-1]) >= 0.99
 
 
-@pytest.mark.timeout(300)
-def test_bf16_d4_1024_deterministic():
-    """C4's model and size in bf16 (2 images): finite, non-trivial, bit-identical on rerun, and
-    the per-image max scores within bf16 precision of the fp32 build's."""
+@pytest.mark.timeout(900)
+def test_bf16_d4_256_matches_emulation_oracle():
+    """BASELINE C4's victim (EfficientDet-D4: b4 backbone with drop connect, 224-channel BiFPN x7)
+    in bf16 against the fp64 oracle with and without the product's bf16 rounding points, at 256^2
+    (the largest size whose fp64 oracle finishes in about a minute).  SURVEY 8c's C4 tolerance vs
+    fp64 (loss rel <= 1e-2, cosine >= 0.99), and against the emulation the same as D0's above."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd import weights as W
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
-    imgs = torch.as_tensor(synth_images([0, 1], 1024)).cuda()
-    boxes = synth_boxes([0, 1], 1024)
-    v = EfficientDetVictim("efficientdet-d4", "synthetic", seed=0, max_batch=2, rng_seed=5, dtype="bf16")
+    from oracle import step as ST
+    S4 = 256
+    v = EfficientDetVictim("efficientdet-d4", "synthetic", seed=0, image_size=S4, max_batch=2, rng_seed=5,
+                           dtype="bf16")
+    wd = W.unpack(v.manifest, v.blob.copy())
+    imgs = synth_images([0, 1], S4)
+    boxes = synth_boxes([0, 1], S4)
     att = PatchAttacker(v, seed=7)
     att.cur_step = 3
-    att.call(imgs, boxes=boxes)
-    g1 = att.grad.clone()
-    att.call(imgs, boxes=boxes)
-    torch.cuda.synchronize()
-    assert torch.isfinite(g1).all()
-    assert g1[:-1].abs().sum() > 0
-    assert torch.equal(att.grad, g1)
+    att.call(torch.as_tensor(imgs).cuda(), boxes=boxes)
+    g = att.grad.cpu().numpy().astype(np.float64)
+    loss = float(att.metrics_buf.cpu().numpy()[_lib.M_LOSS])
+    torch.set_num_threads(16)
+    kw = dict(boxes=boxes, seed=5, step=3, image_size=S4, model="efficientdet-d4")
+    r64 = ST.attack_step(wd, imgs, att.patch.cpu().numpy(), np.float32(0.4), **kw)
+    rem = ST.attack_step(wd, imgs, att.patch.cpu().numpy(), np.float32(0.4), bf16=True, **kw)
+    gp = g[:-1]
+    assert abs(loss - r64["loss"]) <= 1e-2 * abs(r64["loss"])
+    assert _cos(gp, r64["grad"][:-1]) >= 0.99
+    assert abs(loss - rem["loss"]) <= 1e-4 * abs(rem["loss"])
+    e_gpu, e_emul = _rel(gp, rem["grad"][:-1]), _rel(rem["grad"][:-1], r64["grad"][:-1])
+    assert e_gpu <= 2 * e_emul, (e_gpu, e_emul)
+    assert _cos(gp, rem["grad"][:-1]) >= 0.99
+
+
+@pytest.mark.timeout(600)
+def test_bf16_d4_1024_four_images():
+    """C4's model, size and per-GPU batch (D4 1024^2, 4 images, bf16): finite and non-trivial,
+    bit-identical on rerun, the detector's outputs of a permuted batch equal the permuted outputs,
+    and the step agrees with the fp32 build of the same victim within SURVEY 8c's C4 tolerance
+    (loss rel <= 1e-2, d patch cosine >= 0.99; per-image max scores within 2e-2).  The fp64 oracle
+    at this size would need ~100 GB of host memory, so the fp32 build (parity-tested against it at
+    256^2 in test_gpu_deep.py) is the reference here."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
+    B4 = 4
+    imgs = torch.as_tensor(synth_images(list(range(B4)), 1024)).cuda()
+    boxes = synth_boxes(list(range(B4)), 1024)
+    res = {}
+    for dt in ("bf16", "f32"):
+        v = EfficientDetVictim("efficientdet-d4", "synthetic", seed=0, max_batch=B4, rng_seed=5, dtype=dt,
+                               person_bias=2.0)
+        att = PatchAttacker(v, seed=7)
+        att.cur_step = 3
+        att.call(imgs, boxes=boxes)
+        g1 = att.grad.clone()
+        met = att.metrics_buf.cpu().numpy().copy()
+        m = torch.empty(B4, device="cuda")
+        v.ctx.call("phx_debug_last_maxscores", m.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        if dt == "bf16":
+            att.call(imgs, boxes=boxes)
+            torch.cuda.synchronize()
+            assert torch.isfinite(g1).all()
+            assert g1[:-1].abs().sum() > 0
+            assert torch.equal(att.grad, g1)
+            perm = [2, 0, 3, 1]
+            _, s0, c0 = v.detect(imgs)
+            _, s1, c1 = v.detect(imgs[perm].contiguous())
+            assert (s1 - s0[perm]).abs().max().item() <= 1e-3
+            assert (c1 == c0[perm]).float().mean().item() >= 0.999
+        res[dt] = (g1.cpu().numpy().astype(np.float64), met, m.cpu().numpy())
+        del att, v
+        torch.cuda.empty_cache()
+    (gb, mb, sb), (gf, mf, sf) = res["bf16"], res["f32"]
+    assert abs(mb[_lib.M_LOSS] - mf[_lib.M_LOSS]) <= 1e-2 * abs(mf[_lib.M_LOSS])
+    assert np.abs(sb - sf).max() <= 2e-2, (sb, sf)
+    assert _cos(gb[:-1], gf[:-1]) >= 0.99, _cos(gb[:-1], gf[:-1])
+    assert mb[_lib.M_NBOX] == mf[_lib.M_NBOX] and mb[_lib.M_NIMG] == B4

@@ -17,6 +17,10 @@ flips — and the device's transcendentals (v_exp / v_rcp, 1 ulp) round differen
 measured: lite0 320^2 9x (3.7e-2 vs 4.2e-3), D4 256^2 4.1x (1.0e-2 vs 2.5e-3).  A real defect (a
 wrong activation, fuse rule or gradient path) gives O(1) relative errors, far above these bounds.
 Sizes: lite0 at its native 320^2, lite4 at 384^2 (P7 3x3: BN over 18 rows instead of 2).
+
+lite4's gradient is not compared under this relative bound (at 8.8 % intrinsic deviation it would
+admit almost anything); test_lite4_640_well_conditioned_step_matches_oracle checks it at a
+well-conditioned point with a fixed tolerance instead.
 """
 import numpy as np
 import pytest
@@ -61,7 +65,7 @@ def test_lite_detect_matches_oracle(model, S):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("model,S", CASES)
+@pytest.mark.parametrize("model,S", [c for c in CASES if c[0] != "efficientdet-lite4"])
 def test_lite_step_matches_oracle(model, S):
     from mladversarialobjectdetection_amd import _lib
     from mladversarialobjectdetection_amd.attacker import PatchAttacker
@@ -93,3 +97,50 @@ def test_lite_step_matches_oracle(model, S):
     assert abs(g[-1] - r64["grad"][-1]) <= max(1e-5, 4 * abs(r32["grad"][-1] - r64["grad"][-1])) * max(
         1.0, abs(r64["grad"][-1]))
     assert met[_lib.M_NBOX] == r64["nbox"] and met[_lib.M_NIMG] == 2
+
+
+@pytest.mark.timeout(900)
+def test_lite4_640_well_conditioned_step_matches_oracle():
+    """The reference's default victim (efficientdet-lite4, attacker_train.py:17) at its native
+    640^2 (hparams_config.py:457-467), at a well-conditioned point, against the fp64
+    oracle with fixed tolerances: loss rel <= 1e-5, d scale rel <= 1e-5, d patch rel <= 1e-3 and
+    cosine >= 0.99999.
+
+    Why the point is chosen.  With SURVEY 8d's BN draw (gamma U(0.5, 1.5), beta N(0, 0.1)) half of
+    every relu6 input sits near the kink at 0; the ~1e-3 forward rounding noise the 7-cell BiFPN
+    accumulates then flips relu6 masks next to the loss anchor, where the backward support is a few
+    hundred values, and the fp32 restatement itself deviates 8.8 % from fp64 in d patch (measured at
+    640^2 and 384^2) — no fixed bound can tell a correct kernel from a wrong one there.  With gamma
+    U(0.2, 0.4) and beta N(1, 0.1) relu6 inputs sit 2.5-6 sigma inside (0, 6), so masks do not flip;
+    a person prior of 3 keeps the seed 4 m - 2 s away from 0.  The fp32 restatement then deviates
+    6.9e-6 from fp64 (measured at 640^2 with 4 images; 2 here keep the fp64 oracle near a minute), so 1e-3 leaves two orders of margin while any
+    wrong activation, fuse, drop-connect or gradient path gives O(1) errors.  The standard draw's
+    relu6 kinks are still exercised by the lite0 case above."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd import weights as W
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
+    from oracle import step as ST
+    model, S, B = "efficientdet-lite4", 640, 2
+    v = EfficientDetVictim(model, W.synthetic_blob(
+        _lib.Context(model, S, 1).manifest(), seed=0, person_bias=3.0, gamma=(0.2, 0.4), beta=(1.0, 0.1)),
+        image_size=S, max_batch=B, rng_seed=5)
+    wd = W.unpack(v.manifest, v.blob.copy())
+    imgs = synth_images(list(range(B)), S)
+    boxes = synth_boxes(list(range(B)), S)
+    att = PatchAttacker(v, seed=7)
+    att.cur_step = 3
+    att.call(torch.as_tensor(imgs).cuda(), boxes=boxes)
+    g = att.grad.cpu().numpy().astype(np.float64)
+    met = att.metrics_buf.cpu().numpy()
+    torch.set_num_threads(16)
+    r64 = ST.attack_step(wd, imgs, att.patch.cpu().numpy(), np.float32(0.4), boxes=boxes, seed=5, step=3,
+                         model=model, image_size=S)
+    gp, rp = g[:-1], r64["grad"][:-1]
+    rel = float(np.linalg.norm(gp - rp) / np.linalg.norm(rp))
+    cos = float(gp @ rp / (np.linalg.norm(gp) * np.linalg.norm(rp)))
+    assert abs(met[_lib.M_LOSS] - r64["loss"]) <= 1e-5 * abs(r64["loss"])
+    assert abs(g[-1] - r64["grad"][-1]) <= 1e-5 * max(1.0, abs(r64["grad"][-1]))
+    assert rel <= 1e-3, rel
+    assert cos >= 0.99999, cos
+    assert met[_lib.M_NBOX] == r64["nbox"] and met[_lib.M_NIMG] == B
+    np.testing.assert_allclose(met[_lib.M_SUM_M], r64["m"].sum(), rtol=1e-5)

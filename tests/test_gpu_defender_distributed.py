@@ -7,6 +7,7 @@ one SUM all-reduce of [d U-Net variables | loss] -> Adam. Checked against single
 same library on each shard (RNG keyed by global image index; the U-Net's BN domain is the rank):
   * the all-reduced gradient and loss == the sums of the two shard gradients / losses (bit-exact)
   * the U-Net variables after Adam are bit-identical on both ranks, and again after a second step
+  * the BN moving statistics read for saving are the mean of the two ranks' copies on both ranks
 """
 import os
 import socket
@@ -53,7 +54,9 @@ def _worker(rank, world, port, q):
     loss = float(out["loss"].item())
     d.train_step(x, boxes=[boxes[rank]])
     p2 = d.params.cpu().numpy().copy()
-    q.put((rank, red, params, loss, p2))
+    local_mv = d.moving_statistics()
+    mean_mv = d.moving_statistics(replica_mean=True)
+    q.put((rank, red, params, loss, p2, local_mv, mean_mv))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -81,9 +84,14 @@ def test_two_rank_defender_step_equals_sum_of_shards():
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    (_, red0, p0, l0, p20), (_, red1, p1, l1, p21) = res[0], res[1]
+    (_, red0, p0, l0, p20, lm0, mm0), (_, red1, p1, l1, p21, lm1, mm1) = res[0], res[1]
     assert np.array_equal(red0, red1) and np.array_equal(p0, p1) and np.array_equal(p20, p21)
     assert l0 == l1
+    # BN moving statistics: per-rank copies differ (shard statistics); what save_weights writes is
+    # their mean, identical on every rank (Keras ON_READ / MEAN)
+    assert not np.array_equal(lm0, lm1)
+    assert np.array_equal(mm0, mm1)
+    np.testing.assert_allclose(mm0, (lm0 + lm1) / 2, rtol=1e-6, atol=1e-7)
 
     imgs, boxes = _case()
     d = _make()

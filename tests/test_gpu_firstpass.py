@@ -183,7 +183,7 @@ def test_eval_step_matches_oracle(victim, wdict):
     # test_step wraps the same call and derives the add_metric values
     m, (ob2, os2, oc2) = att.test_step(torch.as_tensor(imgs).cuda())
     assert m["loss"] == pytest.approx(ref["loss"], rel=1e-5)
-    assert m["asr"] == pytest.approx(1 - ref["asr_num"] / (ref["asr_den"] + 1e-7), rel=1e-6)
+    assert m["asr"] == pytest.approx(ST.calc_asr(ref["asr_num"], ref["asr_den"]), rel=1e-6)
 
 
 def test_config_override_reaches_the_library(victim):
