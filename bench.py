@@ -134,8 +134,9 @@ def kernel_roofline(kind, r, mfma_peak=PEAK_FP32_TFLOPS, pmc=True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 200 steps of C2 take ~2.8 s: long enough for the driver's GPU-busy sampler to see the run
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=16, help="images per GPU")
     ap.add_argument("--image-size", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -151,6 +152,8 @@ def main():
                          "(C4: bf16 matrix cores, fp32 accumulation)")
     ap.add_argument("--person-bias", type=float, default=0.0,
                     help="lift the person class-logit bias so the clean pass yields real soft-NMS candidates")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary line (the reference's own placement flow, measured after the headline)")
     args = ap.parse_args()
 
     from mladversarialobjectdetection_amd import distributed as ddp
@@ -190,6 +193,7 @@ def main():
     elapsed = float(dt.item())
     images_per_s = world * B * args.steps / elapsed
 
+    patches_headline = att.step_metrics()["patches"] if rank == 0 else 0
     roofline = None
     step_roof = None
     if not args.no_profile:
@@ -211,13 +215,45 @@ def main():
         step_roof["roofline_ms_per_step"] = round(roof_ms, 3)
         step_roof["frac_of_roofline"] = round(roof_ms / (1e3 * elapsed / args.steps), 4)
 
+    # secondary line (not `value`): the same workload with the reference's placement flow — patches
+    # on the first pass's soft-NMS person boxes (attacker.py:180-184) with a person prior that gives
+    # ~1500 patches per step — timed the same way on a fresh victim after the headline
+    secondary = None
+    if not args.no_secondary and args.placement == "injected" and args.model == "efficientdet-d0":
+        del att
+        torch.cuda.empty_cache()
+        v2 = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
+                                device=local, person_bias=4.6, dtype=args.dtype)
+        a2 = PatchAttacker(v2, seed=7, device=dev)
+        steps2 = max(1, args.steps // 4)
+        for _ in range(args.warmup):
+            a2.train_step(images)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        t1 = time.perf_counter()
+        for _ in range(steps2):
+            a2.train_step(images)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        d2 = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        if world > 1:
+            torch.distributed.all_reduce(d2, op=torch.distributed.ReduceOp.MAX)
+        e2 = float(d2.item())
+        m2 = a2.step_metrics()
+        secondary = {"placement": "first-pass", "person_bias": 4.6, "steps": steps2,
+                     "value": round(world * B * steps2 / e2, 3), "unit": "images/s",
+                     "ms_per_step": round(1e3 * e2 / steps2, 3), "patches_per_step": int(m2["patches"])}
+        att = a2
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.model == "efficientdet-d0":
         threads = min(16, len(os.sched_getaffinity(0)))
         cpu = cpu_baseline(S, args.cpu_batch, threads)
 
     if rank == 0:
-        met = att.step_metrics()
+        met = att.step_metrics() if secondary is None else {"patches": patches_headline}
         line = {
             "metric": "patch-opt images/sec (EffDet-D0 512px fwd+bwd)" if args.model == "efficientdet-d0"
                       else f"patch-opt images/sec ({args.model} {S}px fwd+bwd)",
@@ -244,6 +280,7 @@ def main():
             "roofline": roofline,
             "step_roofline": step_roof,
             "cpu_baseline": cpu,
+            "secondary": secondary,
         }
         print(json.dumps(line))
 

@@ -254,6 +254,19 @@ int phx_def_workspace_bytes(phx_def* d, int B, size_t* bytes);
  * grad: num_params floats followed by the metric row [loss] (SUM-all-reducible). */
 int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,
                       const float* params, float* grad, int64_t step, int32_t global_image_offset, void* stream);
+/* PatchAttackDefender.call(images, training=False) as test_step runs it (attack_detection.py:168-198,
+ * 320-326): first pass (or the caller's boxes), the Masker's evaluation branch with the attacker's
+ * trained patch — eval_patch = [patch 640*640*3 | scale] (device; the PatchAttackDefender eval_patch
+ * directory's patch.tiff / scale.txt, :57-61) — print variation, brightness match, centred placement
+ * at the fixed scale (:454-456), the second detector pass odet_model(images, score_thresh=0.)
+ * (:185-187, soft-NMS threshold 0.001, filter_valid_boxes at the config's threshold), updates =
+ * 2 * PatchNeutralizer(images, training=False) (inference BN, no Dropout) and the loss.  metrics:
+ * [loss] (1 float, device).  out_boxes [B,100,4] / out_scores [B,100] / out_count [B]: the second
+ * pass's detections (NULL = skip).  No variable or moving statistic changes. */
+int phx_def_eval_step(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,
+                      const float* params, const float* eval_patch, float* metrics, float* out_boxes,
+                      float* out_scores, int32_t* out_count, int64_t step, int32_t global_image_offset,
+                      void* stream);
 /* debug copies of the last step (device->device): patched images / targets / updates [B,H,W,3],
  * first-pass boxes [B,100,4], counts [B] (int32 bits) */
 enum { PHX_DEF_PATCHED = 0, PHX_DEF_TARGETS = 1, PHX_DEF_UPDATES = 2, PHX_DEF_BOXES = 3, PHX_DEF_COUNTS = 4 };

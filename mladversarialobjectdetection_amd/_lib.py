@@ -99,6 +99,9 @@ _SIGS = [
     ("phx_def_workspace_bytes", c_int, [c_void_p, c_int, POINTER(c_size_t)]),
     ("phx_def_step_grad", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    ("phx_def_eval_step", c_int,
+     [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+      c_void_p, c_int64, c_int, c_void_p]),
     ("phx_def_debug", c_int, [c_void_p, c_int, c_void_p, c_size_t, c_void_p]),
     ("phx_adam", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_int64, c_void_p]),
 ]

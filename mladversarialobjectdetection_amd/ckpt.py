@@ -15,8 +15,16 @@ skip_mismatch=False).  For a name-keyed (TF1 graph) checkpoint its rule is, per 
 
 The libphx manifest (`phx_weight_manifest`) uses the reference's Keras variable names and TF
 layouts (HWIO kernels, [k, k, C, 1] depthwise kernels), so conversion is a copy of each tensor into
-its manifest offset.  Object-graph (`_CHECKPOINTABLE_OBJECT_GRAPH`) checkpoints, the reference's
-other branch (util_keras.py:131-152), are not converted here (NotImplementedError).
+its manifest offset.
+
+Object-graph checkpoints (`tf.train.Checkpoint` / Keras `save_weights` in the TF2 format), the
+reference's other branch (util_keras.py:131-152), restore by object path: tf.train.Checkpoint matches
+the saved TrackableObjectGraph against the model's attributes and assigns every matched variable; the
+EMA rule does not apply, unmatched variables keep their initial values, and a restore that matches
+nothing fails (assert_nontrivial_match).  The object graph (the DT_STRING tensor
+`_CHECKPOINTABLE_OBJECT_GRAPH`, a serialized TrackableObjectGraph) records for every variable its
+`full_name` — the Keras variable name the manifest uses — next to its `checkpoint_key`, so the same
+architecture's variables are found by full_name here (object_graph_keys).
 
 Format (TensorFlow core/util/tensor_bundle, LevelDB table format): `<prefix>.index` is an SSTable
 whose keys are tensor names (the empty key holds the BundleHeaderProto) and whose values are
@@ -121,7 +129,7 @@ def _enc_field(f: int, wt: int, v) -> bytes:
 
 
 # tensorflow/core/framework/types.proto
-DT_FLOAT, DT_DOUBLE, DT_BFLOAT16, DT_HALF = 1, 2, 14, 19
+DT_FLOAT, DT_DOUBLE, DT_STRING, DT_BFLOAT16, DT_HALF = 1, 2, 7, 14, 19
 _NP_OF = {DT_FLOAT: np.dtype("<f4"), DT_DOUBLE: np.dtype("<f8"), DT_HALF: np.dtype("<f2")}
 
 
@@ -245,6 +253,34 @@ class CheckpointReader:
             self._shards[i] = np.memmap(p, dtype=np.uint8, mode="r")
         return self._shards[i]
 
+    def get_strings(self, name: str) -> list:
+        """A DT_STRING tensor as a flat list of bytes.  tensor_bundle's string layout: every element's
+        length as a varint64, a masked CRC-32C of the lengths (taken over their uint64 little-endian
+        bytes), then the element bytes; the entry's crc32c extends the same running CRC over the
+        lengths' uint64 bytes, the 4 checksum bytes and the element bytes."""
+        e = self.entries[name]
+        if e.dtype != DT_STRING:
+            raise ValueError(f"checkpoint: {name} is not a string tensor")
+        raw = bytes(self._shard(e.shard)[e.offset:e.offset + e.size])
+        n = int(np.prod(e.shape)) if e.shape else 1
+        lens, pos = [], 0
+        for _ in range(n):
+            v, pos = _varint(raw, pos)
+            lens.append(v)
+        lraw = b"".join(struct.pack("<Q", v) for v in lens)
+        lck = struct.unpack_from("<I", raw, pos)[0]
+        if self.verify and crc32c_mask(crc32c(lraw)) != lck:
+            raise ValueError(f"checkpoint: length checksum mismatch for {name}")
+        body = raw[pos + 4:]
+        if self.verify and e.crc is not None and \
+                crc32c_mask(crc32c(lraw + raw[pos:pos + 4] + body)) != e.crc:
+            raise ValueError(f"checkpoint: checksum mismatch for {name}")
+        out, q = [], 0
+        for v in lens:
+            out.append(body[q:q + v])
+            q += v
+        return out
+
     def get_tensor(self, name: str) -> np.ndarray:
         e = self.entries[name]
         if e.sliced:
@@ -319,17 +355,31 @@ def _put_block(f, content: bytes) -> bytes:
     return _enc_varint(off) + _enc_varint(len(content))
 
 
-def write_checkpoint(prefix: str, tensors: dict, block_entries: int = 64, update_latest: bool | None = None):
+def write_checkpoint(prefix: str, tensors: dict, block_entries: int = 64, update_latest: bool | None = None,
+                     strings: dict | None = None):
     """Write float32 tensors as a single-shard tensor bundle (<prefix>.index + .data-00000-of-00001).
 
     update_latest: rewrite the directory's `checkpoint` file to point at this prefix.  None (the
     default) writes it only when the directory has none, so exporting into an existing checkpoint
     directory never silently redirects its latest pointer."""
     os.makedirs(os.path.dirname(os.path.abspath(prefix)), exist_ok=True)
-    names = sorted(tensors)
+    strings = strings or {}
+    names = sorted(list(tensors) + list(strings))
     entries = []
     with open(prefix + ".data-00000-of-00001", "wb") as d:
         for n in names:
+            if n in strings:  # DT_STRING, shape [] for one element (tensor_bundle's string layout)
+                elems = [bytes(x) for x in strings[n]]
+                lraw = b"".join(struct.pack("<Q", len(x)) for x in elems)
+                lck = struct.pack("<I", crc32c_mask(crc32c(lraw)))
+                raw = b"".join(_enc_varint(len(x)) for x in elems) + lck + b"".join(elems)
+                body_crc = crc32c_mask(crc32c(lraw + lck + b"".join(elems)))
+                shape = b"" if len(elems) == 1 else _enc_field(2, 2, _enc_field(1, 0, len(elems)))
+                msg = (_enc_field(1, 0, DT_STRING) + _enc_field(2, 2, shape) + _enc_field(4, 0, d.tell())
+                       + _enc_field(5, 0, len(raw)) + _enc_field(6, 5, body_crc))
+                entries.append((n.encode(), msg))
+                d.write(raw)
+                continue
             a = np.ascontiguousarray(np.asarray(tensors[n], dtype="<f4"))
             raw = a.tobytes()
             shape = b"".join(_enc_field(2, 2, _enc_field(1, 0, int(s))) for s in a.shape)
@@ -357,6 +407,59 @@ def write_checkpoint(prefix: str, tensors: dict, block_entries: int = 64, update
             f.write(f'model_checkpoint_path: "{os.path.basename(prefix)}"\n')
 
 
+def _enc_varint_field(f: int, v: int) -> bytes:
+    return _enc_field(f, 0, v)
+
+
+def write_object_graph_checkpoint(prefix: str, tensors: dict, paths: dict | None = None):
+    """A TF2 object-based checkpoint of float32 variables, as tf.train.Checkpoint(model=...).save
+    lays it out: each variable under `<object path>/.ATTRIBUTES/VARIABLE_VALUE`, and the
+    TrackableObjectGraph (nodes = root, one node per path component, one per variable with its
+    SerializedTensor {name "VARIABLE_VALUE", full_name, checkpoint_key}) as the DT_STRING scalar
+    `_CHECKPOINTABLE_OBJECT_GRAPH`.  paths: full_name -> object path (default "model/<full_name>")."""
+    paths = paths or {k: "model/" + k for k in tensors}
+    nodes = [dict(children={}, attr=None)]  # node 0: the root
+    for full, path in paths.items():
+        cur = 0
+        for comp in path.split("/"):
+            nxt = nodes[cur]["children"].get(comp)
+            if nxt is None:
+                nodes.append(dict(children={}, attr=None))
+                nxt = len(nodes) - 1
+                nodes[cur]["children"][comp] = nxt
+            cur = nxt
+        nodes[cur]["attr"] = (full, path + "/.ATTRIBUTES/VARIABLE_VALUE")
+    graph = b""
+    for nd in nodes:
+        body = b"".join(_enc_field(1, 2, _enc_varint_field(1, i) + _enc_field(2, 2, c.encode()))
+                        for c, i in nd["children"].items())
+        if nd["attr"]:
+            full, key = nd["attr"]
+            body += _enc_field(2, 2, _enc_field(1, 2, b"VARIABLE_VALUE") + _enc_field(2, 2, full.encode())
+                               + _enc_field(3, 2, key.encode()))
+        graph += _enc_field(1, 2, body)
+    t = {paths[k] + "/.ATTRIBUTES/VARIABLE_VALUE": v for k, v in tensors.items()}
+    write_checkpoint(prefix, t, strings={"_CHECKPOINTABLE_OBJECT_GRAPH": [graph]})
+
+
+def object_graph_keys(reader) -> dict:
+    """full_name -> checkpoint_key of every variable attribute in the checkpoint's object graph
+    (TrackableObjectGraph: nodes (1) {children (1), attributes (2) {name (1), full_name (2),
+    checkpoint_key (3)}})."""
+    graph = reader.get_strings("_CHECKPOINTABLE_OBJECT_GRAPH")[0]
+    out = {}
+    for f, _, node in _fields(graph):
+        if f != 1:
+            continue
+        for g, _, att in _fields(node):
+            if g != 2:
+                continue
+            a = {h: v for h, _, v in _fields(att)}
+            if a.get(1) == b"VARIABLE_VALUE" and 2 in a and 3 in a:
+                out[a[2].decode()] = a[3].decode()
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # restore_ckpt for the libphx manifest
 # ---------------------------------------------------------------------------------------------
@@ -377,8 +480,7 @@ def checkpoint_to_blob(ckpt, manifest, ema_decay: float = 0.9998, skip_mismatch:
     reader = ckpt if isinstance(ckpt, CheckpointReader) else CheckpointReader(ckpt, verify)
     keys = [k for k, _ in reader.list_variables()]
     if keys and keys[0] == "_CHECKPOINTABLE_OBJECT_GRAPH":
-        raise NotImplementedError("object-graph (Keras tf.train.Checkpoint) checkpoints are not converted; "
-                                  "use a name-keyed checkpoint (the automl release format)")
+        return _object_graph_to_blob(reader, manifest)
     shapes = reader.shape_map()
     n = max(p["offset"] + int(np.prod(p["shape"])) for p in manifest)
     blob = np.zeros(n, np.float32)
@@ -406,6 +508,34 @@ def checkpoint_to_blob(ckpt, manifest, ema_decay: float = 0.9998, skip_mismatch:
         if val is not None:
             off = p["offset"]
             blob[off:off + val.size] = val.reshape(-1)
+    out = blob.view(_Blob)
+    out.missing = missing
+    return out
+
+
+def _object_graph_to_blob(reader, manifest) -> np.ndarray:
+    """The object-graph branch of restore_ckpt (util_keras.py:131-152): every manifest variable whose
+    full_name the object graph records gets its saved value (no EMA rule); the others keep 0 and
+    are listed in `.missing`; a restore that matches nothing raises (assert_nontrivial_match, whose
+    hub-checkpoint fallback, load_from_hub_checkpoint, is not built)."""
+    by_name = object_graph_keys(reader)
+    shapes = reader.shape_map()
+    n = max(p["offset"] + int(np.prod(p["shape"])) for p in manifest)
+    blob = np.zeros(n, np.float32)
+    missing, matched = [], 0
+    for p in manifest:
+        key = by_name.get(p["name"])
+        if key is None or key not in shapes:
+            missing.append(p["name"])
+            continue
+        if tuple(shapes[key]) != tuple(p["shape"]):
+            raise ValueError(f"Shape mismatch: {key}, expected {tuple(p['shape'])}, but got {tuple(shapes[key])}")
+        val = reader.get_tensor(key)
+        blob[p["offset"]:p["offset"] + val.size] = val.reshape(-1)
+        matched += 1
+    if not matched:
+        raise AssertionError(f"{reader.prefix}: the object graph matches no variable of the model "
+                             "(assert_nontrivial_match; the hub-checkpoint fallback is not built)")
     out = blob.view(_Blob)
     out.missing = missing
     return out

@@ -1284,7 +1284,8 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
 // cand_mask: the keep bits whose anchors (above the NMS threshold) pre_nms appends to the
 // soft-NMS candidate list (2: the first pass's person/valid/>=thresh, 1: the second pass's
 // person/valid for the ASR metric, 0: no list); the run_nms that follows consumes it
-void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0) {
+// nms_t: the soft-NMS score threshold of the candidate list (< 0: the context's)
+void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0, float nms_t = -1.f) {
   const Program& P = E.prog;
   Scope scope(ctx, "pre_nms", 0.0,
               (double)E.B * ctx->A * (ctx->mc.num_classes + 4 + 4 + 6) * 4.0, s);
@@ -1296,15 +1297,18 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0) {
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
                  ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->filter_thresh,
                  E.scores, E.classes, E.boxes, E.keep, E.ntiles, s,
-                 cand_mask ? NmsCand{E.cand_list, E.cand_count, cand_mask, ctx->nms_thresh} : NmsCand{});
+                 cand_mask ? NmsCand{E.cand_list, E.cand_count, cand_mask, nms_t < 0.f ? ctx->nms_thresh : nms_t}
+                           : NmsCand{});
 }
 
 // postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25
-void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s) {
+void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc, hipStream_t s,
+             float nms_t = -1.f) {
   Scope scope(ctx, "soft_nms", 0.0, (double)E.B * ctx->A * 5.0, s);
-  launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, ctx->nms_thresh,
+  const float t = nms_t < 0.f ? ctx->nms_thresh : nms_t;
+  launch_soft_nms(E.boxes, E.scores, E.keep, keep_mask, nullptr, E.B, ctx->A, t,
                   0.25f, PHX_MAX_OUT, (float)ctx->mc.image_size, ob, os, oc, E.nms_ws, s,
-                  NmsCand{E.cand_list, E.cand_count, keep_mask, ctx->nms_thresh});
+                  NmsCand{E.cand_list, E.cand_count, keep_mask, t});
 }
 
 }  // namespace
@@ -1314,17 +1318,22 @@ uint64_t phx::ctx_seed(const phx_ctx* ctx) { return ctx->seed; }
 int phx::ctx_device(const phx_ctx* ctx) { return ctx->device; }
 
 void phx::def_first_pass(phx_ctx* ctx, const float* images, int B, int64_t step, int gimg0, float* boxes, int* count,
-                    hipStream_t s) {
+                    hipStream_t s, bool train, int pass, float score_thresh, float* scores) {
   if (!ctx->weights_loaded) throw std::logic_error("weights not loaded");
   if (B <= 0 || B > ctx->max_batch) throw std::out_of_range("batch exceeds max_batch");
   Exec& E = ctx->exec_for(B);
   // the protege's layers are frozen (inference BN); the call's training flag still reaches its
   // drop connect (attack_detection.py:46-47, 183)
-  run_forward(ctx, E, images, s, 0, step, gimg0, true, true);
-  run_pre_nms(ctx, E, s, 4);  // person anchors only (attack_detection.py:116-121)
-  run_nms(ctx, E, 4, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
+  run_forward(ctx, E, images, s, pass, step, gimg0, train, true);
+  // odet_model(images, score_thresh) (attack_detection.py:96-127): an explicit threshold replaces
+  // the config's for the soft-NMS only ("score_thresh or 0.001", postprocess.py:186-188), while
+  // filter_valid_boxes keeps reading self.config's (:79-94)
+  const float nt = score_thresh < 0.f ? -1.f : (score_thresh != 0.f ? score_thresh : 0.001f);
+  run_pre_nms(ctx, E, s, 4, nt);  // person anchors only (attack_detection.py:116-121)
+  run_nms(ctx, E, 4, E.nms1_boxes, E.nms1_scores, E.nms1_count, s, nt);
   const float S = (float)ctx->mc.image_size;
-  def_filter(E.nms1_boxes, E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, S, S, ctx->filter_thresh, boxes, count, s);
+  def_filter(E.nms1_boxes, E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, S, S, ctx->filter_thresh, boxes, count, s,
+             scores);
 }
 
 namespace {

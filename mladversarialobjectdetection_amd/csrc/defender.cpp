@@ -206,9 +206,21 @@ struct phx_def {
     js << "]}";
     return js.str();
   }
+  // evaluation Masker (the attacker's 640^2 patch), allocated at the first evaluation
+  float *ematched = nullptr, *erstore = nullptr;
+  int eB = 0;
+
   void workspace(int B);
+  void prep_weights(const float* W, hipStream_t s);
+  // U-Net forward on `patched` (train: batch-statistics BN with moving-statistics update and
+  // Dropout; else inference BN from the moving statistics, no Dropout), then the output layer and
+  // loss against `mask` into *loss (and dz, its gradient)
+  void unet_forward(int B, const float* W, bool train, int64_t stp, int gimg0, float* loss, hipStream_t s);
   void step(const float* images, int B, const float* boxes_in, const int* count_in, const float* params,
             float* grad, int64_t step, int gimg0, hipStream_t s);
+  void eval(const float* images, int B, const float* boxes_in, const int* count_in, const float* params,
+            const float* eval_patch, float* metrics, float* out_boxes, float* out_scores, int* out_count,
+            int64_t stp, int gimg0, hipStream_t s);
 };
 
 namespace {
@@ -323,38 +335,8 @@ void phx_def::workspace(int B) {
   eerr = alloc<int>(1);
 }
 
-void phx_def::step(const float* images, int B, const float* boxes_in, const int* count_in, const float* params,
-                   float* grad, int64_t stp, int gimg0, hipStream_t s) {
-  workspace(B);
-  const float* W = params;
-  float* G = grad;
-  // derived GEMM operands of this step's weights
-  for (const UConv& c : convs) {
-    if (c.bt_f < 0) continue;
-    const int kf = c.kind == 0 ? 0 : c.kind == 2 ? 2 : 4;
-    un_wprep(W + c.w, bt + c.bt_f, kf, c.ci, c.co, c.kp_f, s);
-    un_wprep(W + c.w, bt + c.bt_d, kf + 1, c.ci, c.co, c.kp_d, s);
-  }
-  // ---- first pass + Masker ----
-  const float* bx = boxes_in;
-  const int* cn = count_in;
-  if (!bx) {
-    def_first_pass(victim, images, B, stp, gimg0, boxes, count, s);
-    bx = boxes;
-    cn = count;
-  }
-  def_perm_crops(images, info, crops, B, S, S, ed.P, seed, stp, gimg0, s);
-  PlaceRule rule;
-  rule.tol = 0.5f;
-  rule.random_scale = 1;
-  rule.scale_lo = 0.3f;
-  rule.scale_hi = 0.5f;
-  launch_eot_place(ed, bx, cn, nullptr, seed, stp, gimg0, img, place, spans, eerr, s, rule);
-  launch_eot_match_batch(ed, crops, img, images, matched, ysum, ymean, s);
-  launch_eot_resize(ed, matched, place, spans, seed, stp, gimg0, rstore, s, 0.1f);
-  launch_eot_composite(ed, images, place, rstore, patched, nullptr, s, mask);
-
-  // ---- U-Net forward ----
+// ---- U-Net forward (generator.py:17-101) + output layer and loss ----
+void phx_def::unet_forward(int B, const float* W, bool train, int64_t stp, int gimg0, float* loss, hipStream_t s) {
   auto conv3_fwd = [&](const float* x, int H, const UConv& c, float* y) {
     const long M = (long)B * H * H;
     if (un_conv3_small(x, bt + c.bt_f, W + c.b, y, B, H, H, c.ci, H, H, c.co, c.kp_f, 0, 1, 1, 1, s)) return;
@@ -363,7 +345,8 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   };
   auto bn_fwd = [&](UBn& b, const float* y, long M, float* a, int act) {
     float* mv = reinterpret_cast<float*>(moving.get());
-    un_bn_stats(y, M, b.c, W + b.gamma, b.mean, b.rstd, b.sc, mv + b.mm, mv + b.mv, cpart, s);
+    if (train) un_bn_stats(y, M, b.c, W + b.gamma, b.mean, b.rstd, b.sc, mv + b.mm, mv + b.mv, cpart, s);
+    else launch_bn_frozen_stats(mv + b.mm, mv + b.mv, b.mean, b.rstd, W + b.gamma, b.sc, b.c, 1e-3f, s);
     if (a) un_bnact(y, b.mean, b.sc, W + b.beta, a, M, b.c, act, s);
   };
   auto block_fwd = [&](const Block& k, const float* x, int H, float* y1, float* a1, float* y2, float* a2) {
@@ -377,7 +360,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   for (int i = 0; i < 4; ++i) {
     const int H = S >> i;
     block_fwd(enc[i], x, H, et[i].y1, et[i].a1, et[i].y2, et[i].a2);
-    un_pool_drop(et[i].a2, et[i].p, et[i].arg, B, H, H, convs[enc[i].c2].co, seed, stp, gimg0, i, s);
+    un_pool_drop(et[i].a2, et[i].p, et[i].arg, B, H, H, convs[enc[i].c2].co, seed, stp, gimg0, train ? i : -1, s);
     x = et[i].p;
   }
   block_fwd(c4, x, S >> 4, c4t.y1, c4t.a1, c4t.y2, c4t.a2);
@@ -403,13 +386,55 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     un_att_t(d.s, W + convs[a.conv3].w, W + convs[a.conv3].b, d.t, M, n, s);
     UBn& b3 = bns[a.bn3];
     bn_fwd(b3, d.t, M, nullptr, 0);
-    un_att_cat(d.up, skip, d.t, b3.mean, b3.sc, W + b3.beta, d.cat, B, (long)H * H, n, seed, stp, gimg0, 4 + i, s);
+    un_att_cat(d.up, skip, d.t, b3.mean, b3.sc, W + b3.beta, d.cat, B, (long)H * H, n, seed, stp, gimg0,
+               train ? 4 + i : -1, s);
     block_fwd(a.blk, d.cat, H, d.y1, d.a1, d.y2, d.a2);
     x = d.a2;
   }
   const long Mf = (long)B * S * S;
   const UConv& oc = convs[out_conv];
-  un_out_loss(x, W + oc.w, W + oc.b, mask, upd, dz, lpart, G + nparams, Mf, (long)S * S, oc.ci, s);
+  un_out_loss(x, W + oc.w, W + oc.b, mask, upd, dz, lpart, loss, Mf, (long)S * S, oc.ci, s);
+}
+
+// derived GEMM operands of this step's weights
+void phx_def::prep_weights(const float* W, hipStream_t s) {
+  for (const UConv& c : convs) {
+    if (c.bt_f < 0) continue;
+    const int kf = c.kind == 0 ? 0 : c.kind == 2 ? 2 : 4;
+    un_wprep(W + c.w, bt + c.bt_f, kf, c.ci, c.co, c.kp_f, s);
+    un_wprep(W + c.w, bt + c.bt_d, kf + 1, c.ci, c.co, c.kp_d, s);
+  }
+}
+
+void phx_def::step(const float* images, int B, const float* boxes_in, const int* count_in, const float* params,
+                   float* grad, int64_t stp, int gimg0, hipStream_t s) {
+  workspace(B);
+  const float* W = params;
+  float* G = grad;
+  prep_weights(W, s);
+  // ---- first pass + Masker ----
+  const float* bx = boxes_in;
+  const int* cn = count_in;
+  if (!bx) {
+    def_first_pass(victim, images, B, stp, gimg0, boxes, count, s);
+    bx = boxes;
+    cn = count;
+  }
+  def_perm_crops(images, info, crops, B, S, S, ed.P, seed, stp, gimg0, s);
+  PlaceRule rule;
+  rule.tol = 0.5f;
+  rule.random_scale = 1;
+  rule.scale_lo = 0.3f;
+  rule.scale_hi = 0.5f;
+  launch_eot_place(ed, bx, cn, nullptr, seed, stp, gimg0, img, place, spans, eerr, s, rule);
+  launch_eot_match_batch(ed, crops, img, images, matched, ysum, ymean, s);
+  launch_eot_resize(ed, matched, place, spans, seed, stp, gimg0, rstore, s, 0.1f);
+  launch_eot_composite(ed, images, place, rstore, patched, nullptr, s, mask);
+
+  unet_forward(B, W, true, stp, gimg0, G + nparams, s);
+  const float* x = dt[3].a2;
+  const UConv& oc = convs[out_conv];
+  const long Mf = (long)B * S * S;
 
   // ---- backward ----
   auto bias_grad = [&](const float* dy, long M, const UConv& c) { un_colsum(dy, M, c.co, G + c.b, cpart, s); };
@@ -494,6 +519,49 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     const float* xin = i == 0 ? patched : et[i - 1].p;
     block_bwd(enc[i], xin, H, et[i].y1, et[i].a1, et[i].y2, et[i].denc, tmpT, i == 0 ? nullptr : tmpY);
   }
+}
+
+// PatchAttackDefender.call(images, training=False) as test_step runs it (attack_detection.py:168-198,
+// 320-326): the first pass; the Masker's evaluation branch — the attacker's trained patch and scale
+// (eval_patch, the [patch | scale] of patch.tiff / scale.txt, :57-61), print variation, brightness
+// match, centred placement (tolerance 0) at the fixed scale, resize + U(-0.1, 0.1) noise + brightness,
+// rotate, paste (:366-370, 454-456); the second detector pass odet_model(images, score_thresh=0.)
+// (:185-187); updates = 2 * PatchNeutralizer(images, training=False) (inference BN, no Dropout) and the
+// loss.  Nothing is updated (the BN moving statistics stay as they are).
+void phx_def::eval(const float* images, int B, const float* boxes_in, const int* count_in, const float* W,
+                   const float* eval_patch, float* metrics, float* out_boxes, float* out_scores, int* out_count,
+                   int64_t stp, int gimg0, hipStream_t s) {
+  workspace(B);
+  EotDims e2 = ed;
+  e2.P = PHX_PATCH_SIZE;
+  // placement side <= floor(longer side * scale) <= S for scale in [0, 1] (the attacker's clip)
+  e2.rcap = (long)B * PHX_MAX_OUT * S * S * 3;
+  if (eB != B) {
+    PHX_HIP(hipStreamSynchronize(s));
+    ematched = alloc<float>((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3);
+    erstore = alloc<float>(e2.rcap);
+    ws_bytes += ((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3 + e2.rcap) * 4;
+    eB = B;
+  }
+  prep_weights(W, s);
+  const float* bx = boxes_in;
+  const int* cn = count_in;
+  if (!bx) {
+    def_first_pass(victim, images, B, stp, gimg0, boxes, count, s, false, 0);
+    bx = boxes;
+    cn = count;
+  }
+  PlaceRule rule;
+  rule.tol = 0.f;  // Masker.create, evaluation: tolerance 0, scale = the attacker's (attack_detection.py:454-456)
+  launch_eot_place(e2, bx, cn, eval_patch, seed, stp, gimg0, img, place, spans, eerr, s, rule);
+  launch_eot_match(e2, eval_patch, img, images, ematched, ysum, ymean, true, s);
+  launch_eot_resize(e2, ematched, place, spans, seed, stp, gimg0, erstore, s, 0.1f);
+  launch_eot_composite(e2, images, place, erstore, patched, nullptr, s, mask);
+  // the second pass on the patched images (its detections are the evaluation's output)
+  float* ob = out_boxes ? out_boxes : boxes;
+  int* oc = out_count ? out_count : count;
+  def_first_pass(victim, patched, B, stp, gimg0, ob, oc, s, false, 1, 0.f, out_scores);
+  unet_forward(B, W, false, stp, gimg0, metrics, s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -596,6 +664,20 @@ int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes
   DEF_TRY
   PHX_HIP(hipSetDevice(d->device));
   d->step(images, B, boxes, count, params, grad, step, global_image_offset, (hipStream_t)stream);
+  return PHX_OK;
+  DEF_CATCH(d)
+}
+
+int phx_def_eval_step(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,
+                      const float* params, const float* eval_patch, float* metrics, float* out_boxes,
+                      float* out_scores, int32_t* out_count, int64_t step, int32_t global_image_offset, void* stream) {
+  if (!d || !images || !params || !eval_patch || !metrics || B <= 0) return PHX_EINVAL;
+  if (B > d->max_batch) return PHX_ECAP;
+  if ((boxes == nullptr) != (count == nullptr)) return PHX_EINVAL;
+  DEF_TRY
+  PHX_HIP(hipSetDevice(d->device));
+  d->eval(images, B, boxes, count, params, eval_patch, metrics, out_boxes, out_scores, out_count, step,
+          global_image_offset, (hipStream_t)stream);
   return PHX_OK;
   DEF_CATCH(d)
 }

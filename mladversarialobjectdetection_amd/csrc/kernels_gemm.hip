@@ -7,7 +7,7 @@
 // Design (MI355X):
 //  * 256-thread workgroup = WM x WN waves, each wave owns TM x TN tiles of 32x32; block tile
 //    BM x BN = (32*WM*TM) x (32*WN*TN), K advanced in BK = 16 chunks through a double-buffered
-//    LDS image (row pitch BK+4 floats).  Operand fragments are ds_read_b128: lane l feeds
+//    LDS image (unpadded rows, 16-B units XOR-swizzled: g2_off).  Operand fragments are ds_read_b128: lane l feeds
 //    k = 4*(l>>5) + s of its row/column at MFMA step s, so one 16-B read serves 4 MFMAs (the k
 //    order is permuted identically for A and B, so the products are unchanged).
 //  * Workgroups are persistent along M: the (m-tile, k-chunk) steps of all the tiles a workgroup
@@ -74,7 +74,7 @@ template <int WM, int TM, int TN, int MODE, bool BF = false>
 struct G2 {
   static constexpr int WN = 4 / WM;
   static constexpr int BM = WM * TM * 32, BN = WN * TN * 32, BK = BF ? PHX_GEMM_BK_BF16 : PHX_GEMM_BK_F32;
-  static constexpr int LD = BF ? BK + 8 : BK + 4;    // LDS row pitch in elements (16-B aligned rows)
+  static constexpr int LD = BK;                       // LDS row pitch in elements (unpadded; g2_off swizzles)
   static constexpr int KQ = BK / 4;                   // float4 per tile row per chunk
   static constexpr int RPP = 256 / KQ;                // tile rows loaded per pass of the 256 lanes
   static constexpr int NA = (BM + RPP - 1) / RPP;     // A float4 per thread per chunk
@@ -132,12 +132,28 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const G
   }
 }
 
+// Element offset of (row, k) in an A / B tile: unpadded rows of U = BK*ESZ/16 16-B units with the
+// unit index XORed by (row / (16/U)) mod U.  ds_read_b128 banks over a 256-B row in 16-lane groups
+// whose 16 rows (r32 of each half-wave) cover every residue mod 16, so the 16 rows of a group land
+// on 16 distinct 16-B slots for any fixed k: conflict-free.  The chunk stores (ds_write_b128 fp32 /
+// ds_write_b64 bf16, banked over 128 B in 8 / 16 contiguous lanes = two rows of U = 4 units) also
+// land on distinct slots.  The padded layout (pitch BK + 16 B) had conflict-free reads but 2-way
+// conflicts in every store group (0.6-1.2 M conflict cycles per launch).
+template <class P>
+__device__ __forceinline__ int g2_off(int row, int k) {
+  constexpr int EPU = 16 / P::ESZ;  // elements per 16-B unit
+  constexpr int U = P::BK / EPU;    // units per row
+  static_assert(U == 1 || U == 2 || U == 4 || U == 8 || U == 16, "g2_off: row of 1-16 units");
+  const int f = (row / (16 / U)) & (U - 1);
+  return row * P::LD + (((k / EPU) ^ f) * EPU) + k % EPU;
+}
+
 // element (row, k) of the A / B tile of LDS buffer `buf` (fp32 or bf16 elements)
 template <class P>
 __device__ __forceinline__ char* g2_tile(float* sm, int buf, bool b, int row, int k) {
   char* base = reinterpret_cast<char*>(sm) + (size_t)buf * (P::BM + P::BN) * P::LD * P::ESZ;
   if (b) base += (size_t)P::BM * P::LD * P::ESZ;
-  return base + ((size_t)row * P::LD + k) * P::ESZ;
+  return base + (size_t)g2_off<P>(row, k) * P::ESZ;
 }
 
 template <class P>
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
   const Gemm2Args a = pick_seg(grp.a, seg);
   constexpr bool STATS = SK == 1;
   using P = G2<WM, TM, TN, MODE, BF>;
-  constexpr int WN = P::WN, BM = P::BM, BN = P::BN, BK = P::BK;
+  constexpr int BM = P::BM, BN = P::BN, BK = P::BK;
   __shared__ __attribute__((aligned(16))) float sm[P::LDS_FLOATS];
   __shared__ float2 wst[SK ? 4 : 1][SK ? TN * 32 : 1];
   __shared__ float wcn[4];
@@ -299,18 +315,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
       } else {
-        constexpr int LD = P::LD;
         const float* As = reinterpret_cast<const float*>(g2_tile<P>(sm, buf, false, 0, 0));
-        const float* Bs = As + BM * LD;
+        const float* Bs = As + BM * P::LD;
 #pragma unroll
         for (int s8 = 0; s8 < BK / 8; ++s8) {
           float4 fa[TM], fb[TN];
 #pragma unroll
           for (int i = 0; i < TM; ++i)
-            fa[i] = *reinterpret_cast<const float4*>(As + (wm * TM * 32 + i * 32 + r32) * LD + 8 * s8 + 4 * h);
+            fa[i] = *reinterpret_cast<const float4*>(As + g2_off<P>(wm * TM * 32 + i * 32 + r32, 8 * s8 + 4 * h));
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            fb[j] = *reinterpret_cast<const float4*>(Bs + (wn * TN * 32 + j * 32 + r32) * LD + 8 * s8 + 4 * h);
+            fb[j] = *reinterpret_cast<const float4*>(Bs + g2_off<P>(wn * TN * 32 + j * 32 + r32, 8 * s8 + 4 * h));
 #pragma unroll
           for (int i = 0; i < TM; ++i)
 #pragma unroll

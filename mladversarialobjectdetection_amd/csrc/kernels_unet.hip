@@ -604,6 +604,10 @@ __global__ __launch_bounds__(256) void k_un_pool_drop(const float* __restrict__ 
     if (v2 > m) { m = v2; am = 2; }
     if (v3 > m) { m = v3; am = 3; }
     arg[i] = (uint8_t)am;
+    if (layer < 0) {  // inference (training=False): Dropout is the identity
+      out[i] = m;
+      continue;
+    }
     const long e = i - (long)b * Ho * Wo * C;  // element index within the image
     const u32x4 q = philox4x32_10(u32x4{(uint32_t)e, (uint32_t)layer, (uint32_t)(gimg0 + b),
                                         (uint32_t)((uint64_t)step << 8) | RNG_DROPOUT},
@@ -685,6 +689,10 @@ __global__ __launch_bounds__(256) void k_att_cat(const float* __restrict__ up, c
       const float z = (t[m] - mu3[0]) * sc3[0] + be3[0];
       const float a = 1.0f / (1.0f + expf(-z));
       v = skip[m * C + c2 - C] * a;
+    }
+    if (layer < 0) {  // inference: no Dropout
+      cat[i] = v;
+      continue;
     }
     const int b = (int)(m / HW);
     const long e = i - (long)b * HW * 2 * C;
@@ -856,7 +864,7 @@ __global__ __launch_bounds__(256) void k_def_crops(const float* __restrict__ ima
 // w / W <= 1, h / H <= 1, area > 100 and score >= thresh, in order
 __global__ void k_def_filter(const float* __restrict__ nb, const float* __restrict__ ns, const int* __restrict__ nc,
                              int B, int maxo, float Hf, float Wf, float thresh, float* __restrict__ ob,
-                             int* __restrict__ oc) {
+                             int* __restrict__ oc, float* __restrict__ os) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= B) return;
   int k = 0;
@@ -867,6 +875,7 @@ __global__ void k_def_filter(const float* __restrict__ nb, const float* __restri
     if (ok) {
       float* o = ob + ((long)b * maxo + k) * 4;
       o[0] = bx[0]; o[1] = bx[1]; o[2] = bx[2]; o[3] = bx[3];
+      if (os) os[(long)b * maxo + k] = ns[(long)b * maxo + i];
       ++k;
     }
   }
@@ -1083,8 +1092,8 @@ void def_perm_crops(const float* images, int* info, float* crops, int B, int H, 
 }
 
 void def_filter(const float* nb, const float* ns, const int* nc, int B, int maxo, float H, float W, float thresh,
-                float* ob, int* oc, hipStream_t st) {
-  hipLaunchKernelGGL(k_def_filter, dim3(cdiv(B, 64)), dim3(64), 0, st, nb, ns, nc, B, maxo, H, W, thresh, ob, oc);
+                float* ob, int* oc, hipStream_t st, float* os) {
+  hipLaunchKernelGGL(k_def_filter, dim3(cdiv(B, 64)), dim3(64), 0, st, nb, ns, nc, B, maxo, H, W, thresh, ob, oc, os);
   PHX_LAUNCH_CHECK();
 }
 

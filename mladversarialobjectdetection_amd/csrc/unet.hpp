@@ -41,6 +41,7 @@ void un_bnact(const float* y, const float* mu, const float* sc, const float* be,
               hipStream_t st);
 
 // ---- pooling, dropout, attention, output ----------------------------------------------------
+// layer < 0: inference (no Dropout), also for un_att_cat
 void un_pool_drop(const float* x, float* out, uint8_t* arg, int B, int H, int W, int C, uint64_t seed, int64_t step,
                   int gimg0, int layer, hipStream_t st);
 void un_pool_drop_bwd(const float* dout, const uint8_t* arg, float* dx, int B, int H, int W, int C, uint64_t seed,
@@ -67,14 +68,19 @@ void un_add(float* a, const float* b, long n, hipStream_t st);
 // info [B][3] = (source image, flip lr, flip ud); crops [B][P][P][3]
 void def_perm_crops(const float* images, int* info, float* crops, int B, int H, int W, int P, uint64_t seed,
                     int64_t step, int gimg0, hipStream_t st);
+// filter_valid_boxes (attack_detection.py:79-94); os (optional) receives the kept scores
 void def_filter(const float* nb, const float* ns, const int* nc, int B, int maxo, float H, float W, float thresh,
-                float* ob, int* oc, hipStream_t st);
+                float* ob, int* oc, hipStream_t st, float* os = nullptr);
 
 // ---- victim side (api.cpp) -----------------------------------------------------------------
 // odet_model (attack_detection.py:96-127): frozen-BN forward, person anchors, soft-NMS, clip and
 // filter_valid_boxes; boxes [B][100][4], count [B]
+// train: the call's training flag (drop connect), pass: drop-connect key (0 first, 1 second);
+// score_thresh >= 0: odet_model(images, score_thresh) — the soft-NMS threshold only (0 -> 0.001);
+// scores (optional): the kept boxes' scores [B][100]
 void def_first_pass(phx_ctx* ctx, const float* images, int B, int64_t step, int gimg0, float* boxes, int* count,
-                    hipStream_t s);
+                    hipStream_t s, bool train = true, int pass = 0, float score_thresh = -1.f,
+                    float* scores = nullptr);
 int ctx_image_size(const phx_ctx* ctx);
 uint64_t ctx_seed(const phx_ctx* ctx);
 int ctx_device(const phx_ctx* ctx);

@@ -4,7 +4,9 @@ the HIP library (phx_def_step_grad), and data parallelism is one SUM all-reduce 
 [d variables | loss] per step (torch.distributed, RCCL on ROCm).
 
   PatchAttackDefender.__init__  attack_detection.py:34-71 (U-Net built at the protege's image size)
-  PatchAttackDefender.call      attack_detection.py:168-206 (training=True)
+  PatchAttackDefender.call      attack_detection.py:168-206 (training=True, and training=False with the
+                                attacker's eval patch)
+  PatchAttackDefender.test_step attack_detection.py:320-326
   PatchAttackDefender.train_step attack_detection.py:327-336
   generator.define_model        generator.py:269-281 (Keras initialisers restated in numpy)
 """
@@ -59,7 +61,11 @@ class PatchAttackDefender:
     the trainable variables are the U-Net's."""
 
     def __init__(self, protege_model: EfficientDetVictim, initial_weights=None, protege_config_override=None, *,
-                 seed=0, learning_rate=1e-2, max_batch=None, device=None):
+                 eval_patch=None, seed=0, learning_rate=1e-2, max_batch=None, device=None):
+        """eval_patch (attack_detection.py:33, 57-61): the attacker's trained patch for the evaluation
+        branch — a directory holding patch.tiff / scale.txt (PatchAttacker.save_weights), a
+        (patch [640,640,3], scale) pair, or a PatchAttacker (its current variables).  Only
+        call(training=False) / test_step need it."""
         self.protege_model = protege_model
         self.config = protege_model.config
         if protege_config_override:
@@ -86,6 +92,24 @@ class PatchAttackDefender:
         self.learning_rate = learning_rate
         self.iterations = 0
         self.cur_step = 0
+        self.eval_params = None if eval_patch is None else self._eval_params(eval_patch, dev)
+        self.eval_loss = torch.zeros(1, device=dev)
+
+    @staticmethod
+    def _eval_params(eval_patch, dev):
+        """[patch | scale] of the evaluation patch as one device vector (the layout phx_def_eval_step
+        reads, the same as the attacker's parameters)."""
+        from .attacker import PatchAttacker, load_patch
+        if isinstance(eval_patch, PatchAttacker):
+            return eval_patch.params.detach().clone().to(dev)
+        if isinstance(eval_patch, (str, os.PathLike)):
+            patch, scale = load_patch(eval_patch)
+        else:
+            patch, scale = eval_patch
+        patch = np.asarray(patch, np.float32)
+        if patch.shape != (_lib.PATCH_SIZE, _lib.PATCH_SIZE, 3):
+            raise ValueError(f"eval patch must be [640,640,3], got {patch.shape}")
+        return torch.as_tensor(np.concatenate([patch.reshape(-1), [np.float32(scale)]]), device=dev).contiguous()
 
     @property
     def _trainable_variables(self):
@@ -107,11 +131,15 @@ class PatchAttackDefender:
         return (t / ddp.world()).cpu().numpy()
 
     def call(self, images, *, training=True, boxes=None):
-        """PatchAttackDefender.call(images, training=True) (attack_detection.py:168-206): returns the
-        gradient of the loss w.r.t. the U-Net variables (flat, manifest order); the loss of the step is
-        left in loss_buf.  `boxes` optionally replaces the first pass's detections for placement."""
-        if not training:
-            raise NotImplementedError("the defender's evaluation path (adversarial eval patch) is not built")
+        """PatchAttackDefender.call(images, training) (attack_detection.py:168-206).
+
+        training=True: returns the gradient of the loss w.r.t. the U-Net variables (flat, manifest
+        order); the loss of the step is left in loss_buf.
+        training=False (test_step): the Masker pastes the attacker's eval patch at its trained scale,
+        the protege makes a second pass at score_thresh 0 and the U-Net runs in inference mode;
+        returns the second pass's detections (boxes [B,100,4], scores [B,100], count [B]) and leaves
+        the loss in eval_loss.  `boxes` optionally replaces the first pass's detections for
+        placement."""
         images = self.protege_model._check_images(images)
         B = images.shape[0]
         if boxes is not None:
@@ -124,6 +152,16 @@ class PatchAttackDefender:
             bp, cp = bx.data_ptr(), cnt.data_ptr()
         else:
             bp = cp = None
+        if not training:
+            if self.eval_params is None:
+                raise ValueError("evaluation needs eval_patch (attack_detection.py:57-61)")
+            ob = torch.empty(B, _lib.MAX_OUT, 4, device=images.device)
+            os_ = torch.zeros(B, _lib.MAX_OUT, device=images.device)
+            oc = torch.empty(B, dtype=torch.int32, device=images.device)
+            self.handle.call("phx_def_eval_step", images.data_ptr(), B, bp, cp, self.params.data_ptr(),
+                             self.eval_params.data_ptr(), self.eval_loss.data_ptr(), ob.data_ptr(), os_.data_ptr(),
+                             oc.data_ptr(), int(self.cur_step), self.global_offset(B), _stream())
+            return ob, os_, oc
         self.handle.call("phx_def_step_grad", images.data_ptr(), B, bp, cp, self.params.data_ptr(),
                          self._red.data_ptr(), int(self.cur_step), self.global_offset(B), _stream())
         return self.grad
@@ -151,6 +189,13 @@ class PatchAttackDefender:
         self.apply_gradients()
         self.cur_step += 1
         return {"loss": self.loss_buf[0]}
+
+    def test_step(self, inputs, boxes=None):
+        """attack_detection.py:320-326: self(inputs, training=False); the loss metric summed over
+        ranks (the one collective; every rank calls it).  Returns ({"loss": float}, detections)."""
+        preds = self.call(inputs, training=False, boxes=boxes)
+        ddp.allreduce_sum_(self.eval_loss)
+        return {"loss": float(self.eval_loss.item())}, preds
 
     def debug(self, what: int, B: int):
         S = self.protege_model.ctx.image_size

@@ -255,9 +255,11 @@ def noise(seed, step, gimg, k, ps, amp=0.1):
                     -1).reshape(ps, ps, 3)
 
 
-def mask_image(image, patch, boxes, seed, step, gimg):
-    """Masker.add_patches_to_image (attack_detection.py:362-396, training) for one image:
-    returns (patched image, target mask), torch fp64 [H,W,3]."""
+def mask_image(image, patch, boxes, seed, step, gimg, eval_scale=None):
+    """Masker.add_patches_to_image (attack_detection.py:362-396) for one image: returns (patched
+    image, target mask), torch fp64 [H,W,3].  Training: `patch` is the image's 240^2 crop and the
+    placement draws tolerance 0.5 / scale U(0.3, 0.5); evaluation (eval_scale given): `patch` is the
+    attacker's 640^2 patch placed centred (tolerance 0) at eval_scale (:454-456)."""
     H, W = image.shape[0], image.shape[1]
     w, b = eot.print_params(seed, step, gimg)
     p = torch.clamp(torch.as_tensor(w.astype(np.float64)) * patch + torch.as_tensor(b.astype(np.float64)),
@@ -266,7 +268,10 @@ def mask_image(image, patch, boxes, seed, step, gimg):
     img = image.clone()
     mask = torch.zeros_like(image)
     for k, box in enumerate(boxes):
-        pl = placement(box, H, W, seed, step, gimg, k)
+        if eval_scale is None:
+            pl = placement(box, H, W, seed, step, gimg, k)
+        else:
+            pl = eot.placement(box, eval_scale, H, W, seed, step, gimg, k, tol=0.0)
         if not pl["valid"]:
             continue
         ps, diag, pad = pl["ps"], pl["diag"], pl["pad"]
@@ -301,11 +306,26 @@ def masker(images, boxes, seed, step, gimg0):
     return np.stack(outs), np.stack(masks)
 
 
+def masker_eval(images, boxes, patch, scale, seed, step, gimg0):
+    """Masker.call(training=False) over a batch with the attacker's patch: (patched, targets)."""
+    outs, masks = [], []
+    pt = torch.as_tensor(np.asarray(patch, np.float64))
+    for b in range(images.shape[0]):
+        img = torch.as_tensor(np.asarray(images[b], np.float64))
+        o, m = mask_image(img, pt, boxes[b], seed, step, gimg0 + b, eval_scale=np.float32(scale))
+        outs.append(o.numpy())
+        masks.append(m.numpy())
+    return np.stack(outs), np.stack(masks)
+
+
 # ------------------------------------------------------------------------------------------
 # first pass and the step
 # ------------------------------------------------------------------------------------------
-def first_pass(det, images_t, image_size, score_thresh=0.5):
-    """odet_model (attack_detection.py:96-127): person anchors -> soft-NMS -> clip -> valid."""
+def first_pass(det, images_t, image_size, score_thresh=0.5, filter_thresh=None):
+    """odet_model (attack_detection.py:96-127): person anchors -> soft-NMS -> clip -> valid.
+    score_thresh sets the soft-NMS threshold (`or 0.001`); filter_valid_boxes reads the config's
+    threshold, filter_thresh (default: score_thresh)."""
+    filter_thresh = score_thresh if filter_thresh is None else filter_thresh
     with torch.no_grad():
         cls, box = det(images_t)
         scores, classes, boxes = D.pre_nms(cls, box, image_size, det.cfg["anchor_scale"])
@@ -319,7 +339,7 @@ def first_pass(det, images_t, image_size, score_thresh=0.5):
         h = ob[:, 2] - ob[:, 0]
         w = ob[:, 3] - ob[:, 1]
         ok = ((w / f32(image_size) <= 1) & (h / f32(image_size) <= 1) & (f32(h * w) > f32(100.0))
-              & (os_ >= f32(score_thresh)))
+              & (os_ >= f32(filter_thresh)))
         out.append((ob[ok], os_[ok]))
     return out
 
@@ -361,3 +381,36 @@ def adam(params, grad, m, v, lr, t):
     m = m + (g - m) * (np.float32(1) - b1)
     v = v + (g * g - v) * (np.float32(1) - b2)
     return p - (m * alpha) / (np.sqrt(v) + eps), m, v
+
+
+def defender_eval(unet_params, moving, images, eval_patch, eval_scale, victim_weights, boxes=None,
+                  model="efficientdet-d0", image_size=None, seed=0, step=0, gimg0=0, score_thresh=0.5,
+                  masked=None):
+    """PatchAttackDefender.call(images, training=False) (attack_detection.py:168-198) as test_step
+    runs it: first pass (unless `boxes`), the Masker's evaluation branch with the attacker's patch,
+    the second detector pass odet_model(images, score_thresh=0.) (soft-NMS at 0.001, valid filter at
+    the config's score_thresh), updates = 2 * U-Net(images, training=False) and the loss.  Returns
+    dict(loss, patched, targets, updates, second=[(boxes, scores)] per image, boxes).  masked =
+    (patched, targets) skips the first pass and the Masker (the U-Net check feeds the product's own);
+    victim_weights None skips the second pass (second = None)."""
+    layout, _ = unet_layout()
+    images = np.asarray(images, np.float32)
+    image_size = image_size or images.shape[1]
+    det = D.Detector(victim_weights, model, image_size, training=False)
+    if masked is not None:
+        patched, targets = (np.asarray(a, np.float64) for a in masked)
+    else:
+        if boxes is None:
+            boxes = [b for b, _ in first_pass(det, torch.as_tensor(images.astype(np.float64)), image_size,
+                                               score_thresh)]
+        patched, targets = masker_eval(images, boxes, eval_patch, eval_scale, seed, step, gimg0)
+    second = None if victim_weights is None else first_pass(det, torch.as_tensor(patched), image_size, 0.0,
+                                                             filter_thresh=score_thresh)
+    net = UNet(unpack(unet_params, layout), moving, training=False, seed=seed, step=step, gimg0=gimg0)
+    with torch.no_grad():
+        upd = 2.0 * net(torch.as_tensor(patched))
+    t = torch.as_tensor(targets)
+    B = images.shape[0]
+    loss = ((t.reshape(B, -1) - upd.reshape(B, -1)) ** 2).mean(dim=1).sum()
+    return dict(loss=loss.item(), patched=patched, targets=targets, updates=upd.numpy(), second=second,
+                boxes=boxes)

@@ -40,8 +40,10 @@ def print_params(seed, step, gimg):
     return np.array(w, np.float32).reshape(3), np.array(b, np.float32).reshape(3)
 
 
-def placement(box, scale, H, W, seed, step, gimg, k):
-    """Patcher.create (attacker.py:448-488) in TF's fp32 op order; returns dict or None."""
+def placement(box, scale, H, W, seed, step, gimg, k, tol=0.2):
+    """Patcher.create (attacker.py:448-488) in TF's fp32 op order; returns dict or None.
+    tol: the centre tolerance (0.2 the attacker's; 0 the defender Masker's evaluation branch,
+    attack_detection.py:454-456, whose create has the same arithmetic)."""
     ymin, xmin, ymax, xmax = (f32(v) for v in box)
     scale = f32(scale)
     h = f32(ymax - ymin)
@@ -50,7 +52,7 @@ def placement(box, scale, H, W, seed, step, gimg, k):
     psf = f32(np.floor(f32(longer * scale)))
     diag = min(f32(f32(1.41421354) * psf), f32(W))
     r = ph.draw(seed, 0, k, gimg, step, ph.RNG_PLACE)
-    tol = f32(0.2)
+    tol = f32(tol)
     ry = ph.runif(r[0], f32(f32(-tol * h) / f32(2.0)), f32(f32(tol * h) / f32(2.0)))
     rx = ph.runif(r[1], f32(f32(-tol * w) / f32(2.0)), f32(f32(tol * w) / f32(2.0)))
     oy = f32(f32(ymin + f32(h / f32(2.0))) + ry)

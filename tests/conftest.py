@@ -19,11 +19,12 @@ def d0_manifest():
 
 
 def pytest_sessionstart(session):
-    """PHX_HEARTBEAT=<file> (or "stderr"): a line every 30 s while the session runs, so a long
-    oracle comparison (minutes of fp64 CPU work inside one test) is not mistaken for a hung GPU
-    job."""
-    path = os.environ.get("PHX_HEARTBEAT")
-    if not path:
+    """A line every 30 s while a GPU session runs (to stderr, or to the file PHX_HEARTBEAT names;
+    PHX_HEARTBEAT=0 turns it off), so a long oracle comparison (a minute or more of fp64 CPU work
+    inside one test) is not mistaken for a hung GPU job."""
+    path = os.environ.get("PHX_HEARTBEAT", "stderr")
+    if path == "0" or "gpu" not in (session.config.getoption("markexpr", "") or "") or \
+            "not gpu" in session.config.getoption("markexpr", ""):
         return
     import threading
     import time

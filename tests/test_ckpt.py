@@ -99,8 +99,9 @@ def test_corruption_and_object_graph_are_rejected(tmp_path):
     open(prefix + ".data-00000-of-00001", "wb").write(bytes(data))
     with pytest.raises(ValueError):
         C.CheckpointReader(prefix).get_tensor("a/kernel")
+    # an object-graph key that is not a serialized TrackableObjectGraph string
     C.write_checkpoint(prefix, {"_CHECKPOINTABLE_OBJECT_GRAPH": np.zeros(1, np.float32)})
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):
         C.checkpoint_to_blob(prefix, [{"name": "x", "shape": [1], "offset": 0}])
 
 
@@ -140,3 +141,40 @@ def test_export_keeps_an_existing_latest_pointer(tmp_path):
     assert C.latest_checkpoint(str(tmp_path)) == str(tmp_path / "model.ckpt-5")
     C.write_checkpoint(str(tmp_path / "export"), a, update_latest=True)
     assert C.latest_checkpoint(str(tmp_path)) == str(tmp_path / "export")
+
+
+def test_object_graph_checkpoint_restores_by_full_name(tmp_path, d0):
+    """The reference's object-graph branch (util_keras.py:131-152): variables are found through the
+    TrackableObjectGraph's full_name -> checkpoint_key records (Keras-style object paths), no EMA
+    rule applies, unmatched variables are reported, and a graph matching nothing is refused."""
+    man, blob = d0
+    t = {p["name"]: blob[p["offset"]:p["offset"] + int(np.prod(p["shape"]))].reshape(p["shape"]) for p in man}
+    # Keras-like object paths (attribute names, layer lists), unrelated to the variable names
+    paths = {name: f"model/net/_layers/{i}/{name.rsplit('/', 1)[-1]}" for i, name in enumerate(t)}
+    prefix = str(tmp_path / "og" / "ckpt-1")
+    C.write_object_graph_checkpoint(prefix, t, paths)
+    r = C.CheckpointReader(prefix)
+    assert r.list_variables()[0][0] == "_CHECKPOINTABLE_OBJECT_GRAPH"
+    keys = C.object_graph_keys(r)
+    assert len(keys) == len(man) and keys[man[0]["name"]] == paths[man[0]["name"]] + "/.ATTRIBUTES/VARIABLE_VALUE"
+    out = C.checkpoint_to_blob(prefix, man, ema_decay=0.9998)
+    assert np.array_equal(out.view(np.uint32), blob.view(np.uint32)) and out.missing == []
+    # a partial graph: the others keep 0 and are listed
+    half = dict(list(t.items())[: len(t) // 2])
+    C.write_object_graph_checkpoint(str(tmp_path / "og2" / "ckpt-1"), half, {k: paths[k] for k in half})
+    part = C.checkpoint_to_blob(str(tmp_path / "og2"), man)
+    assert len(part.missing) == len(man) - len(half)
+    p0 = man[0]
+    n0 = int(np.prod(p0["shape"]))
+    np.testing.assert_array_equal(part[p0["offset"]:p0["offset"] + n0], blob[p0["offset"]:p0["offset"] + n0])
+    # nothing matches: assert_nontrivial_match
+    C.write_object_graph_checkpoint(str(tmp_path / "og3" / "ckpt-1"), {"other/kernel": np.ones(2, np.float32)})
+    with pytest.raises(AssertionError):
+        C.checkpoint_to_blob(str(tmp_path / "og3"), man)
+    # the string tensor's checksums are verified
+    data = bytearray(open(prefix + ".data-00000-of-00001", "rb").read())
+    e = r.entries["_CHECKPOINTABLE_OBJECT_GRAPH"]
+    data[e.offset + e.size - 1] ^= 1
+    open(prefix + ".data-00000-of-00001", "wb").write(bytes(data))
+    with pytest.raises(ValueError):
+        C.object_graph_keys(C.CheckpointReader(prefix))
