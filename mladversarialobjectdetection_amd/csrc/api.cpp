@@ -1313,6 +1313,22 @@ void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc
 
 }  // namespace
 
+phx::ProfScope phx::prof_begin(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t s) {
+  ProfScope r{nullptr, 0, s};
+  if (!ctx || !ctx->prof.on) return r;
+  Prof* p = &ctx->prof;
+  Prof::Rec rec{kind, p->ev(), p->ev(), flops, bytes, 157.3};
+  PHX_HIP(hipEventRecord(rec.a, s));
+  p->recs.push_back(rec);
+  r.p = p;
+  r.idx = p->recs.size() - 1;
+  return r;
+}
+
+void phx::prof_end(const ProfScope& r) {
+  if (r.p) PHX_HIP(hipEventRecord(static_cast<Prof*>(r.p)->recs[r.idx].b, r.s));
+}
+
 int phx::ctx_image_size(const phx_ctx* ctx) { return ctx->mc.image_size; }
 uint64_t phx::ctx_seed(const phx_ctx* ctx) { return ctx->seed; }
 int phx::ctx_device(const phx_ctx* ctx) { return ctx->device; }

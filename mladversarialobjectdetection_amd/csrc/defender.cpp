@@ -225,6 +225,14 @@ struct phx_def {
 
 namespace {
 
+// a launch group on the victim context's profiler (phx_profile): kind, algorithmic FLOPs and bytes
+struct DScope {
+  ProfScope r;
+  DScope(phx_ctx* v, const char* kind, double flops, double bytes, hipStream_t s)
+      : r(prof_begin(v, kind, flops, bytes, s)) {}
+  ~DScope() noexcept(false) { prof_end(r); }
+};
+
 void gemm(const float* A, const float* Bt, const float* bias, float* C, long M, int N, int K, bool acc, float* part,
           hipStream_t s) {
   launch_gemm(InX{A, nullptr, nullptr, nullptr, 0}, Bt, bias, C, (int)M, N, K, acc, nullptr, 1, s, part);
@@ -339,11 +347,13 @@ void phx_def::workspace(int B) {
 void phx_def::unet_forward(int B, const float* W, bool train, int64_t stp, int gimg0, float* loss, hipStream_t s) {
   auto conv3_fwd = [&](const float* x, int H, const UConv& c, float* y) {
     const long M = (long)B * H * H;
+    DScope g(victim, "unet_conv", 2.0 * M * c.co * 9 * c.ci, 4.0 * M * (c.ci + c.co), s);
     if (un_conv3_small(x, bt + c.bt_f, W + c.b, y, B, H, H, c.ci, H, H, c.co, c.kp_f, 0, 1, 1, 1, s)) return;
     un_im2col(x, col, B, H, H, c.ci, H, H, c.kp_f, 0, 1, 1, 1, s);
     gemm(col, bt + c.bt_f, W + c.b, y, M, c.co, c.kp_f, false, gpart, s);
   };
   auto bn_fwd = [&](UBn& b, const float* y, long M, float* a, int act) {
+    DScope g(victim, "unet_bn", 0.0, (train ? 4.0 : 0.0) * M * b.c + (a ? 8.0 * M * b.c : 0.0), s);
     float* mv = reinterpret_cast<float*>(moving.get());
     if (train) un_bn_stats(y, M, b.c, W + b.gamma, b.mean, b.rstd, b.sc, mv + b.mm, mv + b.mv, cpart, s);
     else launch_bn_frozen_stats(mv + b.mm, mv + b.mv, b.mean, b.rstd, W + b.gamma, b.sc, b.c, 1e-3f, s);
@@ -360,6 +370,7 @@ void phx_def::unet_forward(int B, const float* W, bool train, int64_t stp, int g
   for (int i = 0; i < 4; ++i) {
     const int H = S >> i;
     block_fwd(enc[i], x, H, et[i].y1, et[i].a1, et[i].y2, et[i].a2);
+    DScope g(victim, "unet_other", 0.0, 5.0 * B * H * H * convs[enc[i].c2].co, s);
     un_pool_drop(et[i].a2, et[i].p, et[i].arg, B, H, H, convs[enc[i].c2].co, seed, stp, gimg0, train ? i : -1, s);
     x = et[i].p;
   }
@@ -372,27 +383,44 @@ void phx_def::unet_forward(int B, const float* W, bool train, int64_t stp, int g
     const UConv& up = convs[a.up];
     const int n = up.co;
     DecT& d = dt[i];
-    if (!un_conv3_small(x, bt + up.bt_f, W + up.b, d.up, B, hin, hin, up.ci, H, H, n, up.kp_f, 1, 2, 0, 0, s)) {
-      un_im2col(x, col, B, hin, hin, up.ci, H, H, up.kp_f, 1, 2, 0, 0, s);
-      gemm(col, bt + up.bt_f, W + up.b, d.up, M, n, up.kp_f, false, gpart, s);
+    {
+      const long Min = (long)B * hin * hin;
+      DScope g(victim, "unet_conv", 2.0 * Min * 9 * up.ci * n, 4.0 * (Min * up.ci + M * n), s);
+      if (!un_conv3_small(x, bt + up.bt_f, W + up.b, d.up, B, hin, hin, up.ci, H, H, n, up.kp_f, 1, 2, 0, 0, s)) {
+        un_im2col(x, col, B, hin, hin, up.ci, H, H, up.kp_f, 1, 2, 0, 0, s);
+        gemm(col, bt + up.bt_f, W + up.b, d.up, M, n, up.kp_f, false, gpart, s);
+      }
     }
     const float* skip = et[3 - i].a2;
-    gemm(d.up, bt + convs[a.cnv1].bt_f, W + convs[a.cnv1].b, d.g, M, n, n, false, gpart, s);
+    {
+      DScope g(victim, "unet_gemm", 2.0 * M * n * n, 8.0 * M * n, s);
+      gemm(d.up, bt + convs[a.cnv1].bt_f, W + convs[a.cnv1].b, d.g, M, n, n, false, gpart, s);
+    }
     bn_fwd(bns[a.bn1], d.g, M, nullptr, 0);
-    gemm(skip, bt + convs[a.cnv2].bt_f, W + convs[a.cnv2].b, d.xs, M, n, n, false, gpart, s);
+    {
+      DScope g(victim, "unet_gemm", 2.0 * M * n * n, 8.0 * M * n, s);
+      gemm(skip, bt + convs[a.cnv2].bt_f, W + convs[a.cnv2].b, d.xs, M, n, n, false, gpart, s);
+    }
     bn_fwd(bns[a.bn2], d.xs, M, nullptr, 0);
     const UBn &b1 = bns[a.bn1], &b2 = bns[a.bn2];
-    un_att_s(d.g, d.xs, b1.mean, b1.sc, W + b1.beta, b2.mean, b2.sc, W + b2.beta, d.s, M, n, s);
-    un_att_t(d.s, W + convs[a.conv3].w, W + convs[a.conv3].b, d.t, M, n, s);
+    {
+      DScope g(victim, "unet_other", 2.0 * M * n, 4.0 * M * (3 * n + 1), s);
+      un_att_s(d.g, d.xs, b1.mean, b1.sc, W + b1.beta, b2.mean, b2.sc, W + b2.beta, d.s, M, n, s);
+      un_att_t(d.s, W + convs[a.conv3].w, W + convs[a.conv3].b, d.t, M, n, s);
+    }
     UBn& b3 = bns[a.bn3];
     bn_fwd(b3, d.t, M, nullptr, 0);
-    un_att_cat(d.up, skip, d.t, b3.mean, b3.sc, W + b3.beta, d.cat, B, (long)H * H, n, seed, stp, gimg0,
-               train ? 4 + i : -1, s);
+    {
+      DScope g(victim, "unet_other", 0.0, 4.0 * M * (2 * n + 1 + 2 * n), s);
+      un_att_cat(d.up, skip, d.t, b3.mean, b3.sc, W + b3.beta, d.cat, B, (long)H * H, n, seed, stp, gimg0,
+                 train ? 4 + i : -1, s);
+    }
     block_fwd(a.blk, d.cat, H, d.y1, d.a1, d.y2, d.a2);
     x = d.a2;
   }
   const long Mf = (long)B * S * S;
   const UConv& oc = convs[out_conv];
+  DScope g(victim, "unet_other", 2.0 * Mf * 3 * oc.ci, 4.0 * Mf * (oc.ci + 9), s);
   un_out_loss(x, W + oc.w, W + oc.b, mask, upd, dz, lpart, loss, Mf, (long)S * S, oc.ci, s);
 }
 
@@ -420,6 +448,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     bx = boxes;
     cn = count;
   }
+  DScope gm(victim, "masker", 0.0, 4.0 * B * ((double)S * S * 3 * 3 + 2.0 * ed.P * ed.P * 3), s);
   def_perm_crops(images, info, crops, B, S, S, ed.P, seed, stp, gimg0, s);
   PlaceRule rule;
   rule.tol = 0.5f;
@@ -430,6 +459,8 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   launch_eot_match_batch(ed, crops, img, images, matched, ysum, ymean, s);
   launch_eot_resize(ed, matched, place, spans, seed, stp, gimg0, rstore, s, 0.1f);
   launch_eot_composite(ed, images, place, rstore, patched, nullptr, s, mask);
+  prof_end(gm.r);
+  gm.r.p = nullptr;
 
   unet_forward(B, W, true, stp, gimg0, G + nparams, s);
   const float* x = dt[3].a2;
@@ -439,16 +470,19 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   // ---- backward ----
   auto bias_grad = [&](const float* dy, long M, const UConv& c) { un_colsum(dy, M, c.co, G + c.b, cpart, s); };
   auto bn_bwd = [&](UBn& b, const float* da, const float* y, long M, int act, float* dy) {
+    DScope g(victim, "unet_bn", 0.0, 12.0 * M * b.c, s);
     un_bn_bwd(da, y, M, b.c, b.mean, b.rstd, b.sc, W + b.beta, act, b.mdz, b.mdzx, G + b.gamma, G + b.beta, dy, cpart,
               s);
   };
   auto conv3_wgrad = [&](const float* xin, int H, const UConv& c, const float* dy) {
     const long M = (long)B * H * H;
+    DScope g(victim, "unet_wgrad", 2.0 * M * c.co * 9 * c.ci, 4.0 * M * (c.co + c.ci), s);
     un_wgrad(dy, c.co, xin, c.ci, 1, B, H, H, c.ci, M, c.co, c.kp_f, c.ci, 9, 0, wpart, G + c.w, s);
     bias_grad(dy, M, c);
   };
   auto conv3_dgrad = [&](const float* dy, int H, const UConv& c, float* dx) {
     const long M = (long)B * H * H;
+    DScope g(victim, "unet_conv", 2.0 * M * c.ci * 9 * c.co, 4.0 * M * (c.co + c.ci), s);
     if (un_conv3_small(dy, bt + c.bt_d, nullptr, dx, B, H, H, c.co, H, H, c.ci, c.kp_d, 0, 1, 1, 1, s)) return;
     un_im2col(dy, col, B, H, H, c.co, H, H, c.kp_d, 0, 1, 1, 1, s);
     gemm(col, bt + c.bt_d, nullptr, dx, M, c.ci, c.kp_d, false, gpart, s);
@@ -465,9 +499,12 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     if (dx) conv3_dgrad(tmp, H, convs[k.c1], dx);
   };
   // output layer: dz [Mf,3]
-  un_wgrad(dz, 3, x, oc.ci, 0, 1, 1, 1, 1, Mf, 3, oc.ci, oc.ci, 1, 4, wpart, G + oc.w, s);
-  un_colsum(dz, Mf, 3, G + oc.b, cpart, s);
-  un_small_dgrad(dz, W + oc.w, tmpX, Mf, oc.ci, 3, false, s);
+  {
+    DScope g(victim, "unet_other", 4.0 * Mf * 3 * oc.ci, 4.0 * Mf * (6 + 2 * oc.ci), s);
+    un_wgrad(dz, 3, x, oc.ci, 0, 1, 1, 1, 1, Mf, 3, oc.ci, oc.ci, 1, 4, wpart, G + oc.w, s);
+    un_colsum(dz, Mf, 3, G + oc.b, cpart, s);
+    un_small_dgrad(dz, W + oc.w, tmpX, Mf, oc.ci, 3, false, s);
+  }
   // decoders, last first: tmpX holds the gradient of the decoder block's output
   for (int i = 3; i >= 0; --i) {
     const Att& a = dec[i];
@@ -480,33 +517,59 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     const float* skip = et[3 - i].a2;
     block_bwd(a.blk, d.cat, H, d.y1, d.a1, d.y2, tmpX, tmpT, tmpY);  // tmpY = d cat
     UBn& b3 = bns[a.bn3];
-    un_att_cat_bwd(tmpY, skip, d.t, b3.mean, b3.sc, W + b3.beta, tmpX, denc, d1, B, (long)H * H, n, seed, stp, gimg0,
-                   4 + i, s);  // tmpX = d up, denc = d skip (direct), d1 = d bn3 output
+    {
+      DScope g(victim, "unet_other", 0.0, 4.0 * M * (2 * n + n + 1 + 2 * n + 1), s);
+      un_att_cat_bwd(tmpY, skip, d.t, b3.mean, b3.sc, W + b3.beta, tmpX, denc, d1, B, (long)H * H, n, seed, stp,
+                     gimg0, 4 + i, s);  // tmpX = d up, denc = d skip (direct), d1 = d bn3 output
+    }
     bn_bwd(b3, d1, d.t, M, 0, d2);  // d2 = d t
     const UConv& c3 = convs[a.conv3];
-    un_wgrad(d2, 1, d.s, n, 0, 1, 1, 1, 1, M, 1, n, n, 1, 4, wpart, G + c3.w, s);
-    un_colsum(d2, M, 1, G + c3.b, cpart, s);
     UBn &b1 = bns[a.bn1], &b2 = bns[a.bn2];
-    un_att_s_bwd(d2, W + c3.w, d.g, d.xs, b1.mean, b1.sc, W + b1.beta, b2.mean, b2.sc, W + b2.beta, tmpY, M, n, s);
+    {
+      DScope g(victim, "unet_other", 4.0 * M * n, 4.0 * M * (2 * n + 1 + 2 * n + n), s);
+      un_wgrad(d2, 1, d.s, n, 0, 1, 1, 1, 1, M, 1, n, n, 1, 4, wpart, G + c3.w, s);
+      un_colsum(d2, M, 1, G + c3.b, cpart, s);
+      un_att_s_bwd(d2, W + c3.w, d.g, d.xs, b1.mean, b1.sc, W + b1.beta, b2.mean, b2.sc, W + b2.beta, tmpY, M, n,
+                   s);
+    }
     // bn1 / cnv1 on up
     bn_bwd(b1, tmpY, d.g, M, 0, tmpT);
     const UConv& k1 = convs[a.cnv1];
-    un_wgrad(tmpT, n, d.up, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k1.w, s);
-    bias_grad(tmpT, M, k1);
-    gemm(tmpT, bt + k1.bt_d, nullptr, tmpX, M, n, n, true, gpart, s);
+    {
+      DScope g(victim, "unet_wgrad", 2.0 * M * n * n, 8.0 * M * n, s);
+      un_wgrad(tmpT, n, d.up, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k1.w, s);
+      bias_grad(tmpT, M, k1);
+    }
+    {
+      DScope g(victim, "unet_gemm", 2.0 * M * n * n, 12.0 * M * n, s);
+      gemm(tmpT, bt + k1.bt_d, nullptr, tmpX, M, n, n, true, gpart, s);
+    }
     // bn2 / cnv2 on skip
     bn_bwd(b2, tmpY, d.xs, M, 0, tmpT);
     const UConv& k2 = convs[a.cnv2];
-    un_wgrad(tmpT, n, skip, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k2.w, s);
-    bias_grad(tmpT, M, k2);
-    gemm(tmpT, bt + k2.bt_d, nullptr, denc, M, n, n, true, gpart, s);
+    {
+      DScope g(victim, "unet_wgrad", 2.0 * M * n * n, 8.0 * M * n, s);
+      un_wgrad(tmpT, n, skip, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k2.w, s);
+      bias_grad(tmpT, M, k2);
+    }
+    {
+      DScope g(victim, "unet_gemm", 2.0 * M * n * n, 12.0 * M * n, s);
+      gemm(tmpT, bt + k2.bt_d, nullptr, denc, M, n, n, true, gpart, s);
+    }
     // transposed conv: input = the previous decoder's output (or the bottleneck's)
     const float* xin = i == 0 ? c4t.a2 : dt[i - 1].a2;
-    un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, s);
-    bias_grad(tmpX, M, up);
-    if (!un_conv3_small(tmpX, bt + up.bt_d, nullptr, tmpY, B, H, H, n, hin, hin, up.ci, up.kp_d, 0, 2, 0, 0, s)) {
-      un_im2col(tmpX, col, B, H, H, n, hin, hin, up.kp_d, 0, 2, 0, 0, s);
-      gemm(col, bt + up.bt_d, nullptr, tmpY, (long)B * hin * hin, up.ci, up.kp_d, false, gpart, s);
+    const long Min = (long)B * hin * hin;
+    {
+      DScope g(victim, "unet_wgrad", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
+      un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, s);
+      bias_grad(tmpX, M, up);
+    }
+    {
+      DScope g(victim, "unet_conv", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
+      if (!un_conv3_small(tmpX, bt + up.bt_d, nullptr, tmpY, B, H, H, n, hin, hin, up.ci, up.kp_d, 0, 2, 0, 0, s)) {
+        un_im2col(tmpX, col, B, H, H, n, hin, hin, up.kp_d, 0, 2, 0, 0, s);
+        gemm(col, bt + up.bt_d, nullptr, tmpY, Min, up.ci, up.kp_d, false, gpart, s);
+      }
     }
     std::swap(tmpX, tmpY);  // tmpX = gradient of the next (earlier) block's output
   }
@@ -515,7 +578,10 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   for (int i = 3; i >= 0; --i) {
     const int H = S >> i;
     const int n = convs[enc[i].c2].co;
-    un_pool_drop_bwd(tmpY, et[i].arg, et[i].denc, B, H, H, n, seed, stp, gimg0, i, true, s);
+    {
+      DScope g(victim, "unet_other", 0.0, 4.0 * B * H * H * n * 2.25, s);
+      un_pool_drop_bwd(tmpY, et[i].arg, et[i].denc, B, H, H, n, seed, stp, gimg0, i, true, s);
+    }
     const float* xin = i == 0 ? patched : et[i - 1].p;
     block_bwd(enc[i], xin, H, et[i].y1, et[i].a1, et[i].y2, et[i].denc, tmpT, i == 0 ? nullptr : tmpY);
   }

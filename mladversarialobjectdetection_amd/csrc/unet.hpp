@@ -82,6 +82,15 @@ void def_first_pass(phx_ctx* ctx, const float* images, int B, int64_t step, int 
                     hipStream_t s, bool train = true, int pass = 0, float score_thresh = -1.f,
                     float* scores = nullptr);
 int ctx_image_size(const phx_ctx* ctx);
+// a launch group on the victim context's profiler (phx_profile / phx_profile_report): events on
+// `s` around the group, with its algorithmic FLOPs / bytes; a no-op while profiling is off
+struct ProfScope {
+  void* p;
+  size_t idx;
+  hipStream_t s;
+};
+ProfScope prof_begin(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t s);
+void prof_end(const ProfScope& r);
 uint64_t ctx_seed(const phx_ctx* ctx);
 int ctx_device(const phx_ctx* ctx);
 

@@ -345,25 +345,26 @@ def first_pass(det, images_t, image_size, score_thresh=0.5, filter_thresh=None):
 
 
 def defender_step(unet_params, moving, images, boxes=None, victim_weights=None, model="efficientdet-d0",
-                  image_size=None, seed=0, step=0, gimg0=0, score_thresh=0.5, masked=None):
+                  image_size=None, seed=0, step=0, gimg0=0, score_thresh=0.5, masked=None, dtype=torch.float64):
     """PatchAttackDefender.call(images, training=True): dict(loss, grad (flat, manifest order),
     patched, targets, updates, moving (updated), first_pass).  masked = (patched, targets) skips the
-    Masker (the U-Net parity test feeds the product's own Masker outputs)."""
+    Masker (the U-Net parity test feeds the product's own Masker outputs).  dtype: the detector's and
+    U-Net's arithmetic (fp64 for parity; fp32 is the CPU baseline the defender bench times)."""
     layout, bns = unet_layout()
     images = np.asarray(images, np.float32)
     fp = None
     if boxes is None and masked is None:
         image_size = image_size or images.shape[1]
-        det = D.Detector(victim_weights, model, image_size, training=False)
-        fp = first_pass(det, torch.as_tensor(images.astype(np.float64)), image_size, score_thresh)
+        det = D.Detector(victim_weights, model, image_size, dtype=dtype, training=False)
+        fp = first_pass(det, torch.as_tensor(images.astype(np.float64), dtype=dtype), image_size, score_thresh)
         boxes = [b for b, _ in fp]
     if masked is not None:
         patched, targets = (np.asarray(a, np.float64) for a in masked)
     else:
         patched, targets = masker(images, boxes, seed, step, gimg0)
-    net = UNet(unpack(unet_params, layout), moving, seed=seed, step=step, gimg0=gimg0)
-    upd = 2.0 * net(torch.as_tensor(patched))
-    t = torch.as_tensor(targets)
+    net = UNet(unpack(unet_params, layout), moving, dtype=dtype, seed=seed, step=step, gimg0=gimg0)
+    upd = 2.0 * net(torch.as_tensor(patched, dtype=dtype))
+    t = torch.as_tensor(targets, dtype=dtype)
     B = images.shape[0]
     loss = ((t.reshape(B, -1) - upd.reshape(B, -1)) ** 2).mean(dim=1).sum()
     grads = torch.autograd.grad(loss, [net.p[n] for n, _ in layout])

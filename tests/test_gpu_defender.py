@@ -227,7 +227,8 @@ def test_eval_step_matches_oracle(victim):
         ok = (w / np.float32(S) <= 1) & (h / np.float32(S) <= 1) & (h * w > np.float32(100)) & (ns >= np.float32(.5))
         assert oc[b] == ok.sum()
         np.testing.assert_array_equal(ob[b, :oc[b]], nb[ok])
-        np.testing.assert_array_equal(os_[b, :oc[b]], ns[ok])
+        # decayed scores: the device expf and numpy's exp may differ by an ulp (test_gpu_parity.py)
+        np.testing.assert_allclose(os_[b, :oc[b]], ns[ok], rtol=2e-6, atol=0)
     # the U-Net in inference mode on the product's patched images
     ref = DF.defender_eval(params, mv0, imgs, epatch, 0.4, None, masked=(patched, targets), seed=9, step=d.cur_step)
     assert abs(loss - ref["loss"]) <= 1e-5 * abs(ref["loss"])
