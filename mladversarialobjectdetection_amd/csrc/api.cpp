@@ -128,6 +128,9 @@ struct Exec {
   float* dscale_scratch = nullptr;  // dL/dscale of a gradient-free (eval) step
 
   bool bf16 = false;  // the context's compute dtype (GEMM plans depend on it)
+  // activations (the arena tensors) stored as bf16: PHX_DTYPE_BF16, SURVEY.md 8a R4 "C4: bf16 act";
+  // the program input (the images) and every gradient stay fp32
+  bool abf = false;
   size_t bytes = 0;  // device bytes owned by this executor
   uint64_t used = 0;  // phx_ctx::clock at the last use
   template <typename T>
@@ -137,10 +140,13 @@ struct Exec {
     bytes += n * sizeof(T);
     return p;
   }
+  // base pointer of tensor t (bf16 elements when tbf(t): kernels index it as such)
   float* tptr(int t, const float* input) const {
     if (t == prog.input) return const_cast<float*>(input);
+    if (abf) return reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(act) + prog.tensors[t].off);
     return act + prog.tensors[t].off;
   }
+  int tbf(int t) const { return abf && t != prog.input ? 1 : 0; }
   float* gptr(int t) const {
     long g = prog.tensors[t].goff;
     return g < 0 ? nullptr : grad + g;
@@ -440,11 +446,12 @@ Exec& phx_ctx::exec_for(int B) {
   Exec& E = *ex;
   E.B = B;
   E.bf16 = bf16;
+  E.abf = bf16;
   NetBuilder nb(mc, B, bn_mode == PHX_BN_LOCAL);
   nb.build();
   E.prog = nb.program();
   Program& P = E.prog;
-  E.act = E.alloc<float>(P.act_floats);
+  E.act = E.alloc<float>(E.abf ? (P.act_floats + 1) / 2 : P.act_floats);
   E.grad = E.alloc<float>(P.grad_floats);
   // statistics slots and scratch
   E.slot_a.assign(P.n_slots, nullptr);
@@ -572,8 +579,6 @@ Exec& phx_ctx::exec_for(int B) {
   const int nlev = (int)P.cls_out.size();
   const int na = mc.num_anchors();
   int a0 = 0;
-  const float* base = E.act + P.tensors[P.cls_out[0]].off;
-  const float* bbase = E.act + P.tensors[P.box_out[0]].off;
   for (int l = 0; l < nlev; ++l) {
     const Tensor& tc = P.tensors[P.cls_out[l]];
     const Tensor& tb = P.tensors[P.box_out[l]];
@@ -591,7 +596,6 @@ Exec& phx_ctx::exec_for(int B) {
     for (const Op& op : P.ops)
       if (op.out == P.cls_out[l]) E.dxoff.push_back(P.tensors[op.in[0]].goff);
   }
-  (void)base; (void)bbase;
   if (a0 != A) throw std::runtime_error("anchor count mismatch");
   E.lev_dev = E.alloc<LevelDesc>(nlev);
   PHX_HIP(hipMemcpy(E.lev_dev, E.lev.data(), nlev * sizeof(LevelDesc), hipMemcpyHostToDevice));
@@ -681,9 +685,10 @@ namespace {
 // How consumers see tensor t: BN outputs are virtual (BN input + per-channel transform).
 InX view(phx_ctx* ctx, const Exec& E, int t, const float* input) {
   int bi = E.bn_of_tensor[t];
-  if (bi < 0) return InX{E.tptr(t, input), nullptr, nullptr, nullptr, 0};
+  if (bi < 0) return InX{E.tptr(t, input), nullptr, nullptr, nullptr, 0, E.tbf(t)};
   const Op& op = E.prog.ops[bi];
-  return InX{E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_c[op.slot], ctx->w() + op.beta, op.act};
+  return InX{E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_c[op.slot], ctx->w() + op.beta, op.act,
+             E.tbf(op.in[0])};
 }
 
 // The gradient w.r.t. tensor t as its producer's dgrad sees it: for a BN input the BN backward
@@ -693,7 +698,7 @@ GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
   if (bi >= 0 && E.prog.ops[bi].bwd) {
     const Op& op = E.prog.ops[bi];
     return GradX{E.gptr(op.out), E.tptr(t, input), E.slot_a[op.slot], E.slot_b[op.slot],
-                 E.slot_c[op.slot], ctx->w() + op.beta, E.slot_d[op.slot], E.slot_e[op.slot], op.act};
+                 E.slot_c[op.slot], ctx->w() + op.beta, E.slot_d[op.slot], E.slot_e[op.slot], op.act, E.tbf(t)};
   }
   return GradX{E.gptr(t), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 }
@@ -913,7 +918,7 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
     if (!gs_on) return GradSink{};
     const Op& bn = P.ops[g[r] - 1];
     return GradSink{E.spart + (size_t)r * E.sp_region, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input),
-                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act};
+                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
   };
   double fl = 0, by = 0;
   for (int i : g) {
@@ -1037,7 +1042,8 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     int np = 0;
     switch (op.t) {
       case OP_STEM:
-        np = launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s, sink);
+        np = launch_stem_fwd(x, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w, to.c, op.pad_t, op.pad_l, s, sink,
+                             E.tbf(op.out) != 0);
         break;
       case OP_PW: {
         InX A = view(ctx, E, op.in[0], input);
@@ -1086,7 +1092,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
                              W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
         else
           launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.gamma,
-                          E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
+                          E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s, E.tbf(op.in[0]) != 0);
         (void)y;
         break;
       }
@@ -1145,9 +1151,9 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       wpred = op.w;
     }
   }
-  launch_cls_scatter(E.scores, E.keep, E.mraw, E.nties, E.dm, E.act + P.tensors[P.cls_out[0]].off,
+  launch_cls_scatter(E.scores, E.keep, E.mraw, E.nties, E.dm, E.tptr(P.cls_out[0], input),
                      E.lev_dev, (int)E.lev.size(), ctx->A, E.B, ctx->mc.num_classes, na,
-                     W + wpred, K, E.grad, E.dxoff_dev, s);
+                     W + wpred, K, E.grad, E.dxoff_dev, s, E.tbf(P.cls_out[0]));
   // 2. reverse sweep
   for (int i = (int)P.ops.size() - 1; i >= 0; --i) {
     const Op& op = P.ops[i];
@@ -1184,7 +1190,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     if (i > 0 && E.gfused_bn[i - 1]) {
       const Op& bn = P.ops[i - 1];
       gsk = GradSink{E.spart, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input), E.slot_a[bn.slot],
-                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act};
+                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
       gsk_in = op.in[0] == bn.out ? 0 : 1;
     }
     if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
@@ -1225,7 +1231,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         else if (!frozen)
           launch_bn_bwd_reduce(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
                                W + op.gamma, W + op.beta, (long)ti.rows(), ti.c, op.act, E.red,
-                               E.slot_d[op.slot], E.slot_e[op.slot], s);
+                               E.slot_d[op.slot], E.slot_e[op.slot], s, E.tbf(op.in[0]) != 0);
         (void)dx;
         break;
       case OP_SE:
@@ -1293,12 +1299,13 @@ void run_pre_nms(phx_ctx* ctx, Exec& E, hipStream_t s, int cand_mask = 0, float 
   // every list starts empty: a step that failed between a pre_nms and its run_nms (which
   // normally resets the counts) must not leave stale candidates for the next soft-NMS
   if (cand_mask) PHX_HIP(hipMemsetAsync(E.cand_count, 0, (size_t)E.B * sizeof(int), s));
-  launch_pre_nms(E.act + P.tensors[P.cls_out[0]].off, E.act + P.tensors[P.box_out[0]].off,
+  launch_pre_nms(E.tptr(P.cls_out[0], nullptr), E.tptr(P.box_out[0], nullptr),
                  E.lev_dev, (int)E.lev.size(), reinterpret_cast<const float*>(ctx->d_anchors.get()),
                  ctx->A, E.B, ctx->mc.num_classes, ctx->mc.num_anchors(), S, S, ctx->filter_thresh,
                  E.scores, E.classes, E.boxes, E.keep, E.ntiles, s,
                  cand_mask ? NmsCand{E.cand_list, E.cand_count, cand_mask, nms_t < 0.f ? ctx->nms_thresh : nms_t}
-                           : NmsCand{});
+                           : NmsCand{},
+                 E.tbf(P.cls_out[0]) != 0);
 }
 
 // postprocess.nms with method 'gaussian': sigma 0.5 -> soft_nms_sigma 0.25
@@ -1873,7 +1880,8 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
       throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
     const float* src = which == 0 ? E.tptr(t, nullptr) : E.gptr(op.out);
     if (!src) throw std::invalid_argument("tap: no gradient for this tensor");
-    PHX_HIP(hipMemcpyAsync(out, src, nfloats * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    if (which == 0 && E.tbf(t)) launch_bf16_to_f32(src, out, (long)nfloats, (hipStream_t)stream);
+    else PHX_HIP(hipMemcpyAsync(out, src, nfloats * 4, hipMemcpyDeviceToDevice, (hipStream_t)stream));
     return PHX_OK;
   }
   throw std::invalid_argument(std::string("tap: no op named ") + op_name);

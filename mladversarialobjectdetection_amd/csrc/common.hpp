@@ -72,6 +72,40 @@ __device__ __forceinline__ float round_bf16(float f) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Activation storage.  A PHX_DTYPE_BF16 context stores every activation (the arena tensors: conv /
+// depthwise / fuse / resample / add outputs, i.e. the BN inputs) as bf16 — SURVEY.md 8a R4 "C4:
+// bf16 act, fp32 acc" — while gradients, statistics, EOT and the images stay fp32.  Kernels take the
+// storage type as a template flag (BF) and keep float* parameters as untyped base pointers; element
+// e of a bf16 tensor is the 16-bit word e.  Loads widen to fp32 (exact), stores round to nearest even.
+// ------------------------------------------------------------------------------------------
+template <bool BF>
+__device__ __forceinline__ float4 ald4(const float* p, long e) {
+  if constexpr (BF) return unpack_bf16x4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(p) + e));
+  else return *reinterpret_cast<const float4*>(p + e);
+}
+template <bool BF>
+__device__ __forceinline__ float ald1(const float* p, long e) {
+  if constexpr (BF) return __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(p)[e] << 16);
+  else return p[e];
+}
+template <bool BF>
+__device__ __forceinline__ void ast4(float* p, long e, float4 v) {
+  if constexpr (BF) *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p) + e) = pack_bf16x4(v);
+  else *reinterpret_cast<float4*>(p + e) = v;
+}
+template <bool BF>
+__device__ __forceinline__ void ast1(float* p, long e, float v) {
+  if constexpr (BF) reinterpret_cast<uint16_t*>(p)[e] = __builtin_bit_cast(unsigned short, (__bf16)v);
+  else p[e] = v;
+}
+// the value a store of v leaves in memory (BN statistics are taken over the stored values)
+template <bool BF>
+__device__ __forceinline__ float ast_val(float v) {
+  if constexpr (BF) return round_bf16(v);
+  else return v;
+}
+
+// ------------------------------------------------------------------------------------------
 // InX: an input tensor as its consumers see it.  The output of a training-mode batch norm is
 // never materialised: consumers read the BN input y and apply a = act((y - mu) * sc + be) on
 // load (sc = gamma * rstd, be = beta), so every BN costs one statistics pass instead of a
@@ -83,6 +117,7 @@ struct InX {
   const float* sc;
   const float* be;
   int act;
+  int bf = 0;  // p holds bf16 elements (a PHX_DTYPE_BF16 context's activation arena)
 };
 
 struct Chan4 {
@@ -108,16 +143,18 @@ __device__ __forceinline__ float4 inx_apply4(const InX& v, const Chan4& k, float
   return x;
 }
 
-// element e (flat index) of channel c
+// element e (flat index) of channel c (BF: bf16 storage)
+template <bool BF = false>
 __device__ __forceinline__ float inx_load1(const InX& v, long e, int c) {
-  float x = v.p[e];
+  float x = ald1<BF>(v.p, e);
   if (v.mu) x = act_fwd((x - v.mu[c]) * v.sc[c] + v.be[c], v.act);
   return x;
 }
 
 // 4 consecutive channels c..c+3 at flat index e
+template <bool BF = false>
 __device__ __forceinline__ float4 inx_load4(const InX& v, long e, int c) {
-  float4 x = *reinterpret_cast<const float4*>(v.p + e);
+  float4 x = ald4<BF>(v.p, e);
   if (v.mu) x = inx_apply4(v, inx_chan4(v, c), x);
   return x;
 }
@@ -139,6 +176,7 @@ struct GradX {
   const float* mdz;
   const float* mdzx;
   int act;
+  int ybf = 0;  // y holds bf16 elements (the gradient da stays fp32)
 };
 
 struct GChan4 {
@@ -173,11 +211,12 @@ __device__ __forceinline__ float4 gx_apply4(const GradX& g, const GChan4& k, flo
   return o;
 }
 
-// 4 consecutive channels c..c+3 at flat index e
+// 4 consecutive channels c..c+3 at flat index e (BF: y in bf16 storage)
+template <bool BF = false>
 __device__ __forceinline__ float4 gx_load4(const GradX& g, long e, int c) {
   float4 d = *reinterpret_cast<const float4*>(g.da + e);
   if (!g.y) return d;
-  float4 y = *reinterpret_cast<const float4*>(g.y + e);
+  float4 y = ald4<BF>(g.y, e);
   return gx_apply4(g, gx_chan4(g, c), d, y);
 }
 
@@ -271,6 +310,7 @@ struct GradSink {
   const float* sc;
   const float* be;
   int act;
+  int ybf = 0;  // y holds bf16 elements
 };
 
 struct GSChan4 {

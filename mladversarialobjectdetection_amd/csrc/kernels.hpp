@@ -13,8 +13,10 @@ namespace phx {
 // ---- convolutions (kernels_conv.hip) ------------------------------------------------------
 // 3x3 stride-2 stem, Cin = 3: x [B,H,W,3] -> y [B,Ho,Wo,Co]; w [3,3,3,Co] (HWIO)
 // returns the number of StatSink partial rows written (sink.part == nullptr: no statistics)
+// ybf: y in bf16 storage (a PHX_DTYPE_BF16 context's activations; the statistics are taken over
+// the stored values)
 int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                    int Co, int pt, int pl, hipStream_t s, StatSink sink = StatSink{});
+                    int Co, int pt, int pl, hipStream_t s, StatSink sink = StatSink{}, bool ybf = false);
 // dx [B,H,W,3] (+)= conv_transpose(dy); dy is a materialised gradient [B,Ho,Wo,Co]
 void launch_stem_bwd(const float* dy, const float* w, float* dx, int B, int H, int W, int Ho,
                      int Wo, int Co, int pt, int pl, bool acc, hipStream_t s);
@@ -53,8 +55,9 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
               float* partial, StatSink sink, int target_wgs, GradSink gsk = GradSink{}, bool bf16 = false);
 int gemm_splitk_stats_partials(int M, int N);
+// cbf: C holds bf16 activations (the partial slabs are fp32)
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
-                       bool acc, StatSink sink, hipStream_t s);
+                       bool acc, StatSink sink, hipStream_t s, bool cbf = false);
 // dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
 // with a GradSink, the BN-backward sums of the dgrad's result (returns the partial rows)
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
@@ -111,7 +114,7 @@ void launch_transpose(const float* in, float* out, int rows, int cols, hipStream
 size_t bn_stats_scratch_doubles(long M, int C);
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
                      const float* gamma, float* sc, float* mmean, float* mvar, float eps,
-                     hipStream_t s);
+                     hipStream_t s, bool ybf = false);
 // training-mode BN statistics from the P producer partials of a StatSink (k_bn_finalize)
 void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
                         float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
@@ -146,7 +149,7 @@ void launch_bn_bwd_apply2(GradX g, float* out, long M, int C, hipStream_t s);
 // half runs inside the consumer through a GradX view
 void launch_bn_bwd_reduce(const float* da, const float* y, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, long M, int C, int act,
-                          double* part, float* mdz, float* mdzx, hipStream_t s);
+                          double* part, float* mdz, float* mdzx, hipStream_t s, bool ybf = false);
 // squeeze-excite forward: pool[B,C] = mean_hw(x); scale[B,C]; y = x * scale
 void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
@@ -172,6 +175,8 @@ struct DropView {
 // keep[d*B + b] = floor(p[d] + U), U = u01(Philox(seed; block[d], pass, gimg0 + b, step<<8|RNG_DROP))
 void launch_drop_keep(const int* block, const float* p, int nd, int B, uint64_t seed, int64_t step,
                       int gimg0, int pass, float* keep, hipStream_t s);
+// dst[n] (fp32) = src[n] (bf16 storage)
+void launch_bf16_to_f32(const float* src, float* dst, long n, hipStream_t s);
 // y = drop(a) + b
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s, DropView dv = DropView{});
 // dst (+)= drop'(src); with a GradSink (C channels) the BN-backward sums of the result come along
@@ -222,7 +227,8 @@ struct NmsCand {
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
-                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand = NmsCand{});
+                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand = NmsCand{},
+                    bool bf = false);  // bf: class / box outputs in bf16 storage
 // soft-NMS (NonMaxSuppressionV5, gaussian) per image over candidates selected by keep&mask
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,

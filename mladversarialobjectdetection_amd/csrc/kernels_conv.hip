@@ -24,7 +24,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // filter index of every multiply is wave-uniform, so the 27*CO taps stream through scalar
 // registers (s_load) and each lane keeps all CO output channels of its pixel in VGPRs.
 // ------------------------------------------------------------------------------------------
-template <int CO, bool STATS>
+template <int CO, bool STATS, bool BF>
 __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
                                                   const float* __restrict__ w,
                                                   float* __restrict__ y, int B, int H, int W,
@@ -60,10 +60,13 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
       }
     }
   }
-  float4* yp = reinterpret_cast<float4*>(y + p * CO);
 #pragma unroll
-  for (int c = 0; c < CO / 4; ++c) yp[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+  for (int c = 0; c < CO / 4; ++c)
+    ast4<BF>(y, p * CO + 4 * c, make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]));
   if constexpr (STATS) {
+    // statistics of the values as stored
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc[c] = ast_val<BF>(acc[c]);
     // block statistics through an LDS transpose: G row groups x CO channels, two passes
     constexpr int G = 256 / CO, RG = (256 + G - 1) / G;
     __shared__ float tl[256][CO + 1];
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(256) void k_stem_bwd(const float* __restrict__ dy,
 // each lane computes one 2x2 input quad as k_stem_bwd does.
 constexpr int kStemTQ = 16;  // quads per tile side
 
-template <int CO>
+template <int CO, bool BF>
 __global__ __launch_bounds__(256) void k_stem_bwd_gx(GradX g, const float* __restrict__ w,
                                                      const int16_t* __restrict__ owner,
                                                      float* __restrict__ dx, int B, int H, int W,
@@ -229,7 +232,7 @@ __global__ __launch_bounds__(256) void k_stem_bwd_gx(GradX g, const float* __res
     if (oy >= 0 && oy < Ho && ox >= 0 && ox < Wo) {
       const long i = (((long)b * Ho + oy) * Wo + ox) * CO + c4 * 4;
       v = *reinterpret_cast<const float4*>(g.da + i);
-      if (g.y) v = gx_apply4(g, gx_chan4(g, c4 * 4), v, *reinterpret_cast<const float4*>(g.y + i));
+      if (g.y) v = gx_apply4(g, gx_chan4(g, c4 * 4), v, ald4<BF>(g.y, i));
     }
     sdy[e] = v;
   }
@@ -302,13 +305,18 @@ static void stem_dispatch(int Co, Args... args) {
 template <int CO>
 struct StemFwd {
   static void go(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                 StatSink sink, hipStream_t s) {
+                 StatSink sink, bool ybf, hipStream_t s) {
     long total = (long)B * Ho * Wo;
     sink.P = cdiv(total, 256);
-    if (sink.part)
-      hipLaunchKernelGGL((k_stem_fwd<CO, true>), dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
+    const dim3 g(cdiv(total, 256));
+    if (sink.part && ybf)
+      hipLaunchKernelGGL((k_stem_fwd<CO, true, true>), g, dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
+    else if (sink.part)
+      hipLaunchKernelGGL((k_stem_fwd<CO, true, false>), g, dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
+    else if (ybf)
+      hipLaunchKernelGGL((k_stem_fwd<CO, false, true>), g, dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
     else
-      hipLaunchKernelGGL((k_stem_fwd<CO, false>), dim3(cdiv(total, 256)), dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
+      hipLaunchKernelGGL((k_stem_fwd<CO, false, false>), g, dim3(256), 0, s, x, w, y, B, H, W, Ho, Wo, sink);
   }
 };
 template <int CO>
@@ -326,8 +334,12 @@ struct StemBwdGx {
   static void go(GradX g, const float* w, const int16_t* owner, float* dx, int B, int H, int W,
                  int Ho, int Wo, hipStream_t s) {
     const int tx = cdiv(W / 2, kStemTQ), ty = cdiv(H / 2, kStemTQ);
-    hipLaunchKernelGGL((k_stem_bwd_gx<CO>), dim3(tx * ty, B), dim3(256), 0, s, g, w, owner, dx, B, H, W,
-                       Ho, Wo, tx);
+    if (g.ybf)
+      hipLaunchKernelGGL((k_stem_bwd_gx<CO, true>), dim3(tx * ty, B), dim3(256), 0, s, g, w, owner, dx, B, H, W,
+                         Ho, Wo, tx);
+    else
+      hipLaunchKernelGGL((k_stem_bwd_gx<CO, false>), dim3(tx * ty, B), dim3(256), 0, s, g, w, owner, dx, B, H, W,
+                         Ho, Wo, tx);
   }
 };
 
@@ -346,9 +358,9 @@ void launch_stem_bwd_gx(GradX g, const float* w, const int16_t* owner, float* dx
 }
 
 int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                    int Co, int pt, int pl, hipStream_t s, StatSink sink) {
+                    int Co, int pt, int pl, hipStream_t s, StatSink sink, bool ybf) {
   if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
-  stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, sink, s);
+  stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, sink, ybf, s);
   PHX_LAUNCH_CHECK();
   return cdiv((long)B * Ho * Wo, 256);
 }
@@ -380,7 +392,7 @@ struct GemmFrag {
 };
 
 // MODE 0: raw A, 1: BN view (InX), 2: BN view x SE rowscale, 3: gradient view (GradX)
-template <int NT, int MODE>
+template <int NT, int MODE, int ST>
 __device__ __forceinline__ void gemm_load(GemmFrag<NT>& f, const InX& Ax, const GradX& Gx,
                                           const float* __restrict__ Bt, int K, int klim, int kk,
                                           const int* rows, const bool* rok, const int* cols,
@@ -402,10 +414,10 @@ __device__ __forceinline__ void gemm_load(GemmFrag<NT>& f, const InX& Ax, const 
       float4 v;
       if (MODE == 3) {
         v = *reinterpret_cast<const float4*>(Gx.da + e);
-        float4 yv = *reinterpret_cast<const float4*>(Gx.y + e);
+        float4 yv = ald4<ST == 2>(Gx.y, e);
         v = gx_apply4(Gx, gk, v, yv);
       } else {
-        v = *reinterpret_cast<const float4*>(Ax.p + e);
+        v = ald4<ST == 1>(Ax.p, e);
         if (MODE == 1 || MODE == 2) v = inx_apply4(Ax, ck, v);
         if (MODE == 2) {
           float4 sc = *reinterpret_cast<const float4*>(rowscale + (long)(rows[mt] / rows_per_img) * K + kk);
@@ -428,7 +440,7 @@ __device__ __forceinline__ void gemm_load(GemmFrag<NT>& f, const InX& Ax, const 
 // wave rows sit in 8 registers of 4 lanes (r, r+16, r+32, r+48).  Two passes over the registers
 // (mean, then M2 about it) plus xor-shuffles give each wave (n, mean, M2) per column; the WM
 // waves that share columns are merged through LDS (Chan) and written as partial row blockIdx.x.
-template <int NT, int WM>
+template <int NT, int WM, bool BF>
 __device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const float* __restrict__ bias,
                                            int M, int N, int m_base, int n_base, int wave, int wm,
                                            int wn, int lane, const StatSink& sink) {
@@ -445,7 +457,7 @@ __device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const fl
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        if (m_base + mt * 16 + 4 * q + j < M) s += acc[mt][nt][j] + b;
+        if (m_base + mt * 16 + 4 * q + j < M) s += ast_val<BF>(acc[mt][nt][j] + b);
     s += __shfl_xor(s, 16);
     s += __shfl_xor(s, 32);
     const float mean = n > 0.f ? s / n : 0.f;
@@ -455,7 +467,7 @@ __device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const fl
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         if (m_base + mt * 16 + 4 * q + j < M) {
-          const float d = acc[mt][nt][j] + b - mean;
+          const float d = ast_val<BF>(acc[mt][nt][j] + b) - mean;
           m2 = fmaf(d, d, m2);
         }
     m2 += __shfl_xor(m2, 16);
@@ -489,7 +501,7 @@ __device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const fl
 // BN-backward sums (GradSink) of a dgrad block's output tile: value v (+ the accumulated C when
 // acc_flag) at rows 4q+j of column r per accumulator tile, the BN input y loaded at the same
 // element; xor-shuffles over q, then the WM waves sharing the columns meet in LDS.
-template <int NT, int WM>
+template <int NT, int WM, bool YBF>
 __device__ __forceinline__ void gemm_gsums(const floatx4 (&acc)[2][NT], const float* __restrict__ C,
                                            int acc_flag, int M, int N, int m_base, int n_base, int wave,
                                            int wm, int wn, int lane, const GradSink& g) {
@@ -510,7 +522,7 @@ __device__ __forceinline__ void gemm_gsums(const floatx4 (&acc)[2][NT], const fl
             const long e = (long)row * N + col;
             float v = acc[mt][nt][j];
             if (acc_flag) v += C[e];
-            gs_one(v, g.y[e], mu, rs, sc, be, g.act, s1, s2);
+            gs_one(v, ald1<YBF>(g.y, e), mu, rs, sc, be, g.act, s1, s2);
           }
         }
     }
@@ -540,7 +552,8 @@ __device__ __forceinline__ void gemm_gsums(const floatx4 (&acc)[2][NT], const fl
 // STATS: the BN batch statistics of C (bias included) are reduced in the epilogue into partial
 // row blockIdx.x of the StatSink (one (sum, M2) per column over the block's 32*WM rows).
 // SK: 0 plain, 1 StatSink (forward BN statistics), 2 GradSink (BN-backward sums of a dgrad)
-template <int NT, int WM, int MODE, int SK>
+// ST: activation storage (as k_gemm2): 0 fp32; 1 forward with bf16 A and C; 2 dgrad with a bf16 y
+template <int NT, int WM, int MODE, int SK, int ST>
 __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __restrict__ Bt,
                                               const float* __restrict__ bias,
                                               float* __restrict__ C, int M, int N, int K,
@@ -583,12 +596,12 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
 
   GemmFrag<NT> cur, nxt;
   if (kbeg < kend)
-    gemm_load<NT, MODE>(cur, Ax, Gx, Bt, K, kend, kbeg + 4 * q, rows, rok, cols, cok, rowscale,
+    gemm_load<NT, MODE, ST>(cur, Ax, Gx, Bt, K, kend, kbeg + 4 * q, rows, rok, cols, cok, rowscale,
                         rows_per_img);
   for (int k0 = kbeg; k0 < kend; k0 += 16) {
     const bool more = k0 + 16 < kend;
     if (more)
-      gemm_load<NT, MODE>(nxt, Ax, Gx, Bt, K, kend, k0 + 16 + 4 * q, rows, rok, cols, cok, rowscale,
+      gemm_load<NT, MODE, ST>(nxt, Ax, Gx, Bt, K, kend, k0 + 16 + 4 * q, rows, rok, cols, cok, rowscale,
                           rows_per_img);
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -603,13 +616,15 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
     if (more) cur = nxt;
   }
 
-  if constexpr (SK == 1) gemm_stats<NT, WM>(acc, bias, M, N, m_base, n_base, wave, wm, wn, lane, sink);
-  if constexpr (SK == 2) gemm_gsums<NT, WM>(acc, C, acc_flag, M, N, m_base, n_base, wave, wm, wn, lane, gsk);
+  constexpr bool CBF = ST == 1;
+  if constexpr (SK == 1) gemm_stats<NT, WM, CBF>(acc, bias, M, N, m_base, n_base, wave, wm, wn, lane, sink);
+  if constexpr (SK == 2) gemm_gsums<NT, WM, ST == 2>(acc, C, acc_flag, M, N, m_base, n_base, wave, wm, wn, lane, gsk);
 
   // epilogue: accumulator element j of tile (mt,nt) is row 4q+j, col r.  Stage 16 rows at a
   // time through LDS and store row segments with 16-B lanes.
   float* st = stage[wave];
   const bool split = partial != nullptr;
+  const bool cbf = CBF && !split;  // split-K partial slabs stay fp32
   float* out = split ? partial + (long)blockIdx.z * M * N : C;
   const int ncols = min(16 * NT, N - n_base);  // valid columns of this wave
 #pragma unroll
@@ -633,12 +648,13 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
             if (bias) {
               v.x += bias[col]; v.y += bias[col + 1]; v.z += bias[col + 2]; v.w += bias[col + 3];
             }
-            float4* cp = reinterpret_cast<float4*>(out + (long)row * N + col);
+            const long ce = (long)row * N + col;
             if (acc_flag) {
-              float4 o = *cp;
+              const float4 o = cbf ? ald4<true>(out, ce) : *reinterpret_cast<const float4*>(out + ce);
               v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
             }
-            *cp = v;
+            if (cbf) ast4<true>(out, ce, v);
+            else *reinterpret_cast<float4*>(out + ce) = v;
           } else {
             *reinterpret_cast<float4*>(out + (long)row * N + col) = v;
           }
@@ -650,19 +666,21 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
           if (row >= M) continue;
           const int col = n_base + cc;
           float v = st[rr * LDW + cc];
-          float* cp = out + (long)row * N + col;
+          const long ce = (long)row * N + col;
           if (!split) {
             if (bias) v += bias[col];
-            if (acc_flag) v += *cp;
+            if (acc_flag) v += cbf ? ald1<true>(out, ce) : out[ce];
           }
-          *cp = v;
+          if (cbf) ast1<true>(out, ce, v);
+          else out[ce] = v;
         }
       }
     }
   }
 }
 
-// split-K reduction: C (+)= sum_s partial[s] + bias
+// split-K reduction: C (+)= sum_s partial[s] + bias (BF: C holds bf16 activations)
+template <bool BF>
 __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(const float* __restrict__ partial,
                                                             int S, long MN, int N,
                                                             const float* __restrict__ bias,
@@ -672,14 +690,16 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(const float* __restr
   float v = 0.f;
   for (int s = 0; s < S; ++s) v += partial[(long)s * MN + i];
   if (bias) v += bias[i % N];
-  if (acc_flag) v += C[i];
-  C[i] = v;
+  if (acc_flag) v += ald1<BF>(C, i);
+  ast1<BF>(C, i, v);
 }
 
 // split-K reduction with the BN column statistics of the result (forward GEMMs feeding a BN):
 // block b owns rows [b*RB, (b+1)*RB); lane t owns column quad t % N4 of every (256/N4)-th row,
 // keeps shifted sums (shift = its first value) and the block merges its lanes (Chan) into
-// partial row b of the StatSink.  N4 = N/4 <= 256.
+// partial row b of the StatSink.  N4 = N/4 <= 256.  BF: C holds bf16 activations (statistics of
+// the stored values).
+template <bool BF>
 __global__ __launch_bounds__(256) void k_gemm_splitk_reduce_stats(const float* __restrict__ partial,
                                                                   int S, int M, int N, int RB,
                                                                   const float* __restrict__ bias,
@@ -702,7 +722,8 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce_stats(const float* _
         const float4 p = *reinterpret_cast<const float4*>(partial + k * MN + e);
         v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
       }
-      *reinterpret_cast<float4*>(C + e) = v;
+      ast4<BF>(C, e, v);
+      if constexpr (BF) v = make_float4(round_bf16(v.x), round_bf16(v.y), round_bf16(v.z), round_bf16(v.w));
       if (n == 0.f) sh = v;
       const float4 d = make_float4(v.x - sh.x, v.y - sh.y, v.z - sh.z, v.w - sh.w);
       a.x += d.x; a.y += d.y; a.z += d.z; a.w += d.w;
@@ -746,25 +767,44 @@ struct GemmCall {
   GradSink gsk;
 };
 
+// st: activation storage (ST of k_gemm).  bf16 storage variants exist for NT = 1 only: a bf16
+// context runs this kernel for its N <= 16 convs (gemm_impl_for), which plan NT = 1.
 template <int WM, int MODE, int SK>
-static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, const GemmCall& a) {
-#define PHX_G(NT_)                                                                                 \
-  case NT_:                                                                                        \
-    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE, SK>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias,    \
-                       a.C, a.M, a.N, a.K, a.accf, a.rs, a.rpi, a.kslice, a.part, a.sink, a.gsk);  \
-    break;
+static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, const GemmCall& a, int st) {
+#define PHX_G(NT_, ST_)                                                                                \
+    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE, SK, ST_>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias,   \
+                       a.C, a.M, a.N, a.K, a.accf, a.rs, a.rpi, a.kslice, a.part, a.sink, a.gsk);
+  if (st) {
+    constexpr bool fwd = MODE == 1 || MODE == 2 || SK == 1, dgrad = MODE == 3 || SK == 2;
+    if (nt != 1) throw std::runtime_error("gemm: bf16 storage needs NT = 1");
+    if (st == 1 && !dgrad) {
+      PHX_G(1, 1)
+    } else if (st == 2 && !fwd) {
+      PHX_G(1, 2)
+    } else {
+      throw std::logic_error("gemm: storage variant does not match the mode");
+    }
+    return;
+  }
   switch (nt) {
-    PHX_G(1) PHX_G(2) PHX_G(3) PHX_G(4) PHX_G(5) PHX_G(6) PHX_G(7) PHX_G(8)
+    case 1: PHX_G(1, 0) break;
+    case 2: PHX_G(2, 0) break;
+    case 3: PHX_G(3, 0) break;
+    case 4: PHX_G(4, 0) break;
+    case 5: PHX_G(5, 0) break;
+    case 6: PHX_G(6, 0) break;
+    case 7: PHX_G(7, 0) break;
+    case 8: PHX_G(8, 0) break;
     default: throw std::runtime_error("gemm: bad NT");
   }
 #undef PHX_G
 }
 
 template <int MODE, int SK>
-static void gemm_dispatch(int wm, int nt, dim3 g, hipStream_t s, const GemmCall& a) {
-  if (wm == 4) gemm_dispatch_nt<4, MODE, SK>(nt, g, s, a);
-  else if (wm == 2) gemm_dispatch_nt<2, MODE, SK>(nt, g, s, a);
-  else gemm_dispatch_nt<1, MODE, SK>(nt, g, s, a);
+static void gemm_dispatch(int wm, int nt, dim3 g, hipStream_t s, const GemmCall& a, int st) {
+  if (wm == 4) gemm_dispatch_nt<4, MODE, SK>(nt, g, s, a, st);
+  else if (wm == 2) gemm_dispatch_nt<2, MODE, SK>(nt, g, s, a, st);
+  else gemm_dispatch_nt<1, MODE, SK>(nt, g, s, a, st);
 }
 
 GemmPlan plan_gemm(int M, int N, int K) {
@@ -856,18 +896,26 @@ int gemm_stat_partials(int M, int N, int K, bool bf16) {
 // reduce the split-K partial slabs into C (+ bias, + C when acc); with a StatSink the BN column
 // statistics of the result come out of the same pass.  Returns the StatSink partial rows.
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
-                       bool acc, StatSink sink, hipStream_t s) {
+                       bool acc, StatSink sink, hipStream_t s, bool cbf) {
   if (sink.part) {
     const int rb = splitk_stats_rb(M, N);
     sink.P = cdiv(M, rb);
-    hipLaunchKernelGGL(k_gemm_splitk_reduce_stats, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
-                       M, N, rb, bias, C, sink);
+    if (cbf)
+      hipLaunchKernelGGL(k_gemm_splitk_reduce_stats<true>, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
+                         M, N, rb, bias, C, sink);
+    else
+      hipLaunchKernelGGL(k_gemm_splitk_reduce_stats<false>, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
+                         M, N, rb, bias, C, sink);
     PHX_LAUNCH_CHECK();
     return sink.P;
   }
   long mn = (long)M * N;
-  hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
-                     bias, C, acc ? 1 : 0);
+  if (cbf)
+    hipLaunchKernelGGL(k_gemm_splitk_reduce<true>, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
+                       bias, C, acc ? 1 : 0);
+  else
+    hipLaunchKernelGGL(k_gemm_splitk_reduce<false>, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
+                       bias, C, acc ? 1 : 0);
   PHX_LAUNCH_CHECK();
   return 0;
 }
@@ -890,15 +938,16 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   dim3 g(p.gx, p.gy, p.splits);
   GemmCall a{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
              p.kslice, part, sink, gsk};
+  const int st = A.bf ? 1 : ((G.y && G.ybf) || (gs && gsk.ybf)) ? 2 : 0;
   switch (mode) {
     case 0:
-      if (kstats) gemm_dispatch<0, 1>(p.wm, p.nt, g, s, a);
-      else if (gs) gemm_dispatch<0, 2>(p.wm, p.nt, g, s, a);
-      else gemm_dispatch<0, 0>(p.wm, p.nt, g, s, a);
+      if (kstats) gemm_dispatch<0, 1>(p.wm, p.nt, g, s, a, st);
+      else if (gs) gemm_dispatch<0, 2>(p.wm, p.nt, g, s, a, st);
+      else gemm_dispatch<0, 0>(p.wm, p.nt, g, s, a, st);
       break;
-    case 1: kstats ? gemm_dispatch<1, 1>(p.wm, p.nt, g, s, a) : gemm_dispatch<1, 0>(p.wm, p.nt, g, s, a); break;
-    case 2: kstats ? gemm_dispatch<2, 1>(p.wm, p.nt, g, s, a) : gemm_dispatch<2, 0>(p.wm, p.nt, g, s, a); break;
-    default: gs ? gemm_dispatch<3, 2>(p.wm, p.nt, g, s, a) : gemm_dispatch<3, 0>(p.wm, p.nt, g, s, a); break;
+    case 1: kstats ? gemm_dispatch<1, 1>(p.wm, p.nt, g, s, a, st) : gemm_dispatch<1, 0>(p.wm, p.nt, g, s, a, st); break;
+    case 2: kstats ? gemm_dispatch<2, 1>(p.wm, p.nt, g, s, a, st) : gemm_dispatch<2, 0>(p.wm, p.nt, g, s, a, st); break;
+    default: gs ? gemm_dispatch<3, 2>(p.wm, p.nt, g, s, a, st) : gemm_dispatch<3, 0>(p.wm, p.nt, g, s, a, st); break;
   }
   if (gs) {
     PHX_LAUNCH_CHECK();
@@ -906,17 +955,8 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   }
   PHX_LAUNCH_CHECK();
   if (p.splits > 1) {
-    if (stats) {
-      const int rb = splitk_stats_rb(M, N);
-      hipLaunchKernelGGL(k_gemm_splitk_reduce_stats, dim3(cdiv(M, rb)), dim3(256), 0, s, partial,
-                         p.splits, M, N, rb, bias, C, sink);
-      PHX_LAUNCH_CHECK();
-      return cdiv(M, rb);
-    }
-    long mn = (long)M * N;
-    hipLaunchKernelGGL(k_gemm_splitk_reduce, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, p.splits, mn,
-                       N, bias, C, a.accf);
-    PHX_LAUNCH_CHECK();
+    const int np = gemm_splitk_finish(partial, p.splits, M, N, bias, C, acc, sink, s, st == 1);
+    if (stats) return np;
   }
   return p.gx;
 }

@@ -83,7 +83,8 @@ __device__ __forceinline__ bool dw_block_map(int L, int per, int ncg, int nwork,
   return true;
 }
 
-// ---- staging sources ---------------------------------------------------------------------
+// ---- staging sources (BF: the activation tensors hold bf16) --------------------------------
+template <bool BF>
 struct StageInX {
   using Raw = float4;
   InX v;
@@ -95,9 +96,7 @@ struct StageInX {
     if (f) k = inx_chan4(x, c);
   }
   __device__ __forceinline__ Raw zero() const { return make_float4(0.f, 0.f, 0.f, 0.f); }
-  __device__ __forceinline__ Raw load(long e) const {
-    return *reinterpret_cast<const float4*>(v.p + e);
-  }
+  __device__ __forceinline__ Raw load(long e) const { return ald4<BF>(v.p, e); }
   __device__ __forceinline__ float4 finish(const Raw& x) const {
     return f ? inx_apply4(v, k, x) : x;
   }
@@ -112,6 +111,7 @@ struct StageInX {
   }
 };
 
+template <bool BF>
 struct StageFuse {
   struct Raw {
     float4 v[3];
@@ -132,9 +132,9 @@ struct StageFuse {
   }
   __device__ __forceinline__ Raw load(long e) const {
     Raw r;
-    r.v[0] = *reinterpret_cast<const float4*>(f.x[0].p + e);
-    r.v[1] = *reinterpret_cast<const float4*>(f.x[1].p + e);
-    r.v[2] = f.nin > 2 ? *reinterpret_cast<const float4*>(f.x[2].p + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    r.v[0] = ald4<BF>(f.x[0].p, e);
+    r.v[1] = ald4<BF>(f.x[1].p, e);
+    r.v[2] = f.nin > 2 ? ald4<BF>(f.x[2].p, e) : make_float4(0.f, 0.f, 0.f, 0.f);
     return r;
   }
   __device__ __forceinline__ float4 finish(const Raw& r) const {
@@ -152,6 +152,7 @@ struct StageFuse {
   __device__ __forceinline__ float4 finish_t(const Raw& r) const { return finish(r); }
 };
 
+template <bool BF>
 struct StageGradX {
   struct Raw {
     float4 d, y;
@@ -168,7 +169,7 @@ struct StageGradX {
   __device__ __forceinline__ Raw load(long e) const {
     Raw r;
     r.d = *reinterpret_cast<const float4*>(g.da + e);
-    if (g.y) r.y = *reinterpret_cast<const float4*>(g.y + e);
+    if (g.y) r.y = ald4<BF>(g.y, e);
     return r;
   }
   __device__ __forceinline__ float4 finish(const Raw& r) const {
@@ -337,9 +338,10 @@ __device__ __forceinline__ void dw_stats(const float4 (&acc)[RPT], unsigned vmas
 }
 
 // ---- forward: y[oy][ox] = sum_ij a[oy*S - pt + i][ox*S - pl + j] * w[i][j] ----------------
-template <int K, int S, int RPT, bool STATS, int NS, class XV, int SU = 4>
+// BF: input and output activations in bf16 storage (statistics of the stored values)
+template <int K, int S, int RPT, bool STATS, int NS, class XV, int SU = 4, bool BF = false>
 __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
-  using Stage = std::conditional_t<std::is_same<XV, InX>::value, StageInX, StageFuse>;
+  using Stage = std::conditional_t<std::is_same<XV, InX>::value, StageInX<BF>, StageFuse<BF>>;
   const DwFwdSegT<XV> sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
   const XV& xv = sg.x;
   const DwGeom& g = sg.g;
@@ -396,8 +398,10 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
     const int oy = oy0 + row0 + r;
     if (active && oy < g.Ho) {
       vmask |= 1u << r;
-      *reinterpret_cast<float4*>(y + (((long)b * g.Ho + oy) * g.Wo + ox) * g.C + c) = acc[r];
+      ast4<BF>(y, (((long)b * g.Ho + oy) * g.Wo + ox) * g.C + c, acc[r]);
     }
+    if constexpr (BF && STATS)
+      acc[r] = make_float4(round_bf16(acc[r].x), round_bf16(acc[r].y), round_bf16(acc[r].z), round_bf16(acc[r].w));
   }
   if constexpr (STATS) dw_stats<RPT>(acc, vmask, g.lcg, c, (long)b * g.ntiles + tl, sink);
 }
@@ -432,7 +436,8 @@ __device__ __forceinline__ void dw_gsums(float4 s1, float4 s2, int lcg, int c, l
   }
 }
 
-template <int K, int S, int RPT, bool GS, int NS, int SU = 4>
+// YBF: the BN input y (gradient view, GradSink) in bf16 storage; dy and dx stay fp32
+template <int K, int S, int RPT, bool GS, int NS, int SU = 4, bool YBF = false>
 __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   const DwBwdSeg sg = pick_seg(grp.s, NS == 1 ? 0 : (int)blockIdx.y);
   const GradX& gv = sg.gv;
@@ -456,12 +461,12 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   const int oy_lo = S == 1 ? ay : (ay >= 0 ? ay / S : -((-ay + S - 1) / S));
   const int ox_lo = S == 1 ? ax : (ax >= 0 ? ax / S : -((-ax + S - 1) / S));
 
-  StageGradX src;
+  StageGradX<YBF> src;
   src.init(gv, c);
   float4* wt = tile + g.rin * g.cin * CG;
   Taps<K> wr;
   wr.stage(wt, w, g.C, cgi, g.lcg);
-  dw_stage<StageGradX, SU>(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
+  dw_stage<StageGradX<YBF>, SU>(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
   __syncthreads();
 
   const int ix = ix0 + col;
@@ -522,7 +527,7 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   for (int r = 0; r < RPT; ++r) {
     const long e = (((long)b * g.H + min(iy0 + row0 + r, g.H - 1)) * g.W + ixc) * g.C + c;
     if (acc_flag) old[r] = *reinterpret_cast<const float4*>(dx + e);
-    if constexpr (GS) yv[r] = *reinterpret_cast<const float4*>(gsk.y + e);
+    if constexpr (GS) yv[r] = ald4<YBF>(gsk.y, e);
   }
 #pragma unroll
   for (int r = 0; r < RPT; ++r) {
@@ -618,8 +623,18 @@ static size_t dw_lds(const DwGeom& g, int k) {
   return ((size_t)g.rin * g.cin + (lds_taps ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
 }
 
+static bool xv_bf(const InX& x) { return x.bf != 0; }
+static bool xv_bf(const FuseView& f) { return f.x[0].bf != 0; }
+
+template <int K, int S, int RPT, int NS, class XV, int SU, bool BF>
+static void dw_fwd_launch(dim3 grid, size_t lds, const DwFwdGroup<NS, XV>& grp, bool stats, hipStream_t s) {
+  if (stats) hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV, SU, BF>), grid, dim3(256), lds, s, grp);
+  else hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS, XV, SU, BF>), grid, dim3(256), lds, s, grp);
+}
+
 template <int K, int S, int RPT, int NS, class XV>
 static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, hipStream_t s) {
+  const bool bf = xv_bf(grp.s[0].x);
   int gx = 1;
   size_t lds = 0;
   for (int i = 0; i < n; ++i) {
@@ -632,18 +647,13 @@ static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, h
   if constexpr (S == 1 && std::is_same<XV, InX>::value) su8 = dw_s1_su() == 8;
   if constexpr (S == 2 || std::is_same<XV, InX>::value) {
     if (su8) {
-      if (stats)
-        hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV, 8>), grid, dim3(256), lds, s, grp);
-      else
-        hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS, XV, 8>), grid, dim3(256), lds, s, grp);
+      if (bf) dw_fwd_launch<K, S, RPT, NS, XV, 8, true>(grid, lds, grp, stats, s);
+      else dw_fwd_launch<K, S, RPT, NS, XV, 8, false>(grid, lds, grp, stats, s);
       return;
     }
   }
-  if (stats) {
-    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, true, NS, XV>), grid, dim3(256), lds, s, grp);
-  } else {
-    hipLaunchKernelGGL((k_dw_fwd<K, S, RPT, false, NS, XV>), grid, dim3(256), lds, s, grp);
-  }
+  if (bf) dw_fwd_launch<K, S, RPT, NS, XV, 4, true>(grid, lds, grp, stats, s);
+  else dw_fwd_launch<K, S, RPT, NS, XV, 4, false>(grid, lds, grp, stats, s);
 }
 
 template <int NS, class XV>
@@ -724,11 +734,20 @@ static void dw_bwd_go(const DwBwdGroup<NS>& grp, int n, int B, bool gsums, hipSt
     const char* e = std::getenv("PHX_DW_BSU");
     return e && atoi(e) == 8;
   }();
-  if (su8) {
+  // the BN input y of every member shares the context's storage type
+  const bool ybf = (grp.s[0].gv.y && grp.s[0].gv.ybf) || (gsums && grp.s[0].gs.ybf);
+  if (su8 && !ybf) {  // (A/B knob; the bf16-storage variant stages 4 deep)
     if (gsums)
       hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS, 8>), grid, dim3(256), lds, s, grp);
     else
       hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false, NS, 8>), grid, dim3(256), lds, s, grp);
+    return;
+  }
+  if (ybf) {
+    if (gsums)
+      hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS, 4, true>), grid, dim3(256), lds, s, grp);
+    else
+      hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false, NS, 4, true>), grid, dim3(256), lds, s, grp);
     return;
   }
   if (gsums)

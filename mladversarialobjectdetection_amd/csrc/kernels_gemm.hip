@@ -99,7 +99,10 @@ struct G2Regs {
 // A load under an exec-mask branch makes hipcc's wait counting conservative (vmcnt(0) right
 // after the first conditional load), which exposed a full HBM round trip per K step before the
 // MFMAs of the staged chunk could issue.
-template <int WM, int TM, int TN, int MODE, bool BF>
+// ST (activation storage, PHX_DTYPE_BF16): 0 every tensor fp32; 1 forward — A and C are bf16
+// activations; 2 data gradient — A and C are fp32 gradients, the BN input y (gradient view,
+// GradSink) a bf16 activation
+template <int WM, int TM, int TN, int MODE, bool BF, int ST>
 __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, int m0, int n0,
                                         int k0, int kend) {
   using P = G2<WM, TM, TN, MODE, BF>;
@@ -116,9 +119,9 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const G
     const long e = (long)min(row, a.M - 1) * a.K + kc;
     if (MODE == 3) {
       r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
-      r.y[u] = *reinterpret_cast<const float4*>(a.G.y + e);
+      r.y[u] = ald4<ST == 2>(a.G.y, e);
     } else {
-      r.a[u] = *reinterpret_cast<const float4*>(a.A.p + e);
+      r.a[u] = ald4<ST == 1>(a.A.p, e);
       if (MODE == 2)
         r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(min(row, a.M - 1) / a.rpi) * a.K + kc);
     }
@@ -214,8 +217,9 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, 
 #ifndef PHX_GEMM_PF2
 #define PHX_GEMM_PF2 0
 #endif
-template <int WM, int TM, int TN, int MODE, int SK, int NS, bool BF>
+template <int WM, int TM, int TN, int MODE, int SK, int NS, bool BF, int ST>
 __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
+  constexpr bool CBF = ST == 1;  // C holds bf16 activations (split-K partial slabs stay fp32)
   // two-deep prefetch for the fp32 forward GEMMs (the dgrad's gradient view and the bf16 chunks
   // hold twice the staging registers: one set keeps them clear of spills)
   constexpr bool PF2 = PHX_GEMM_PF2 && !BF && MODE != 3;
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
     // written to LDS at the end of step s+1 (two steps of latency cover; the HBM bytes a
     // workgroup keeps in flight double).  PF1: one set, loads one step ahead.
     G2Regs<WM, TM, TN, MODE, BF> rgA, rgB;
-    g2_load<WM, TM, TN, MODE, BF>(rgA, a, tile * BM, n0, kbeg, kend);
+    g2_load<WM, TM, TN, MODE, BF, ST>(rgA, a, tile * BM, n0, kbeg, kend);
     g2_store<WM, TM, TN, MODE, BF>(rgA, a, sm, 0, tile * BM, n0, kbeg, kend);
     int buf = 0, kc = 0;
     // the chunk after (tile, kc): the following chunk of this tile, or the first of the next
@@ -273,7 +277,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
     int t1, k1;
     advance(tile, 0, t1, k1);
     bool h1 = t1 < a.mtiles;
-    if constexpr (PF2) g2_load<WM, TM, TN, MODE, BF>(rgB, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : 0) * BK, kend);
+    if constexpr (PF2) g2_load<WM, TM, TN, MODE, BF, ST>(rgB, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : 0) * BK, kend);
     __syncthreads();
     floatx16 acc[TM][TN];
 #pragma unroll
@@ -291,9 +295,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       if constexpr (PF2) {
         advance(t1, k1, t2, k2);
         h2 = h1 && t2 < a.mtiles;
-        g2_load<WM, TM, TN, MODE, BF>(L, a, (h2 ? t2 : tile) * BM, n0, kbeg + (h2 ? k2 : kc) * BK, kend);
+        g2_load<WM, TM, TN, MODE, BF, ST>(L, a, (h2 ? t2 : tile) * BM, n0, kbeg + (h2 ? k2 : kc) * BK, kend);
       } else {
-        g2_load<WM, TM, TN, MODE, BF>(L, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : kc) * BK, kend);
+        g2_load<WM, TM, TN, MODE, BF, ST>(L, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : kc) * BK, kend);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs
       // MFMAs on the staged chunk
@@ -347,6 +351,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
         const int ncol0 = n0 + wn * TN * 32;
         const bool full = mrow0 + TM * 32 <= a.M && ncol0 + TN * 32 <= a.N;
         const bool accum = !split && a.acc;
+        const bool cbf = CBF && !split;  // split-K partial slabs stay fp32
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int col = ncol0 + j * 32 + r32;
@@ -354,20 +359,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
           const float bv = bias[j];
 #pragma unroll
           for (int i = 0; i < TM; ++i) {
-            float* cbase = out + (long)(mrow0 + i * 32 + 4 * h) * a.N + col;
+            const long cbase = (long)(mrow0 + i * 32 + 4 * h) * a.N + col;
             if (full) {
               float old[16];
               if (accum) {
 #pragma unroll
-                for (int e = 0; e < 16; ++e) old[e] = cbase[(long)((e & 3) + 8 * (e >> 2)) * a.N];
+                for (int e = 0; e < 16; ++e) {
+                  const long ce = cbase + (long)((e & 3) + 8 * (e >> 2)) * a.N;
+                  old[e] = cbf ? ald1<true>(out, ce) : out[ce];
+                }
               }
 #pragma unroll
               for (int e = 0; e < 16; ++e) {
                 float v = acc[i][j][e] + bv;
                 acc[i][j][e] = v;
                 if (accum) v += old[e];
-                cbase[(long)((e & 3) + 8 * (e >> 2)) * a.N] = v;
+                const long ce = cbase + (long)((e & 3) + 8 * (e >> 2)) * a.N;
+                if (cbf) ast1<true>(out, ce, v);
+                else out[ce] = v;
                 if (SK == 2) acc[i][j][e] = v;
+                if (CBF && STATS) acc[i][j][e] = round_bf16(v);  // statistics of the stored values
               }
             } else {
 #pragma unroll
@@ -376,11 +387,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
                 float v = acc[i][j][e] + bv;
                 acc[i][j][e] = v;
                 if (cok && row < a.M) {
-                  float* cp = out + (long)row * a.N + col;
-                  if (accum) v += *cp;
-                  *cp = v;
+                  const long ce = (long)row * a.N + col;
+                  if (accum) v += cbf ? ald1<true>(out, ce) : out[ce];
+                  if (cbf) ast1<true>(out, ce, v);
+                  else out[ce] = v;
                   if (SK == 2) acc[i][j][e] = v;
                 }
+                if (CBF && STATS) acc[i][j][e] = round_bf16(v);
               }
             }
           }
@@ -431,7 +444,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
                   const int row = min(mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h, a.M - 1);
-                  yv[e] = a.gsk.y[(long)row * a.N + cc];
+                  yv[e] = ald1<ST == 2>(a.gsk.y, (long)row * a.N + cc);
                 }
 #pragma unroll
                 for (int e = 0; e < 16; ++e) {
@@ -610,25 +623,51 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
   return p;
 }
 
+// st: activation storage variant (ST of k_gemm2).  A bf16 context stores bf16 activations, so its
+// forward modes run ST 1 and its gradient views ST 2; an fp32 context always ST 0.
 template <int WM, int TM, int TN, int MODE, int SK, int NS>
-static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf) {
-  if (bf) hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true>), g, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, false>), g, dim3(256), 0, s, a);
+static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st) {
+  if (!bf) {
+    if (st) throw std::logic_error("gemm2: bf16 storage needs the bf16 compute type");
+    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, false, 0>), g, dim3(256), 0, s, a);
+    return;
+  }
+  constexpr bool fwd_only = MODE == 1 || MODE == 2 || SK == 1;
+  constexpr bool dgrad_only = MODE == 3 || SK == 2;
+  if constexpr (fwd_only) {
+    if (st != 1) throw std::logic_error("gemm2: bf16 forward without bf16 activations");
+    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), 0, s, a);
+  } else if constexpr (dgrad_only) {
+    if (st != 2) throw std::logic_error("gemm2: bf16 gradient view without bf16 activations");
+    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 2>), g, dim3(256), 0, s, a);
+  } else {  // raw A: a forward activation (ST 1) or a plain gradient (ST 0)
+    if (st == 1) hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), 0, s, a);
+    else if (st == 0) hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 0>), g, dim3(256), 0, s, a);
+    else throw std::logic_error("gemm2: raw dgrad with a bf16 y");
+  }
 }
 
 // sk: 1 forward statistics (modes 0-2), 2 BN-backward sums (dgrad modes 0, 3)
 template <int WM, int TM, int TN, int NS>
-static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf) {
+static void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st) {
   switch (mode) {
     case 0:
-      if (sk == 1) g2_go<WM, TM, TN, 0, 1, NS>(g, s, a, bf);
-      else if (sk == 2) g2_go<WM, TM, TN, 0, 2, NS>(g, s, a, bf);
-      else g2_go<WM, TM, TN, 0, 0, NS>(g, s, a, bf);
+      if (sk == 1) g2_go<WM, TM, TN, 0, 1, NS>(g, s, a, bf, st);
+      else if (sk == 2) g2_go<WM, TM, TN, 0, 2, NS>(g, s, a, bf, st);
+      else g2_go<WM, TM, TN, 0, 0, NS>(g, s, a, bf, st);
       break;
-    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1, NS>(g, s, a, bf) : g2_go<WM, TM, TN, 1, 0, NS>(g, s, a, bf); break;
-    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1, NS>(g, s, a, bf) : g2_go<WM, TM, TN, 2, 0, NS>(g, s, a, bf); break;
-    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2, NS>(g, s, a, bf) : g2_go<WM, TM, TN, 3, 0, NS>(g, s, a, bf); break;
+    case 1: sk == 1 ? g2_go<WM, TM, TN, 1, 1, NS>(g, s, a, bf, st) : g2_go<WM, TM, TN, 1, 0, NS>(g, s, a, bf, st); break;
+    case 2: sk == 1 ? g2_go<WM, TM, TN, 2, 1, NS>(g, s, a, bf, st) : g2_go<WM, TM, TN, 2, 0, NS>(g, s, a, bf, st); break;
+    default: sk == 2 ? g2_go<WM, TM, TN, 3, 2, NS>(g, s, a, bf, st) : g2_go<WM, TM, TN, 3, 0, NS>(g, s, a, bf, st); break;
   }
+}
+
+// storage variant of a launch (see g2_go): A (raw / BN view) bf16 -> 1; a bf16 y (gradient view or
+// GradSink) -> 2
+static int g2_storage(const InX& A, const GradX& G, const GradSink& gsk) {
+  if (A.bf) return 1;
+  if ((G.y && G.ybf) || (gsk.part && gsk.ybf)) return 2;
+  return 0;
 }
 
 int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
@@ -651,20 +690,21 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   a.a[0] = Gemm2Args{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
                      p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles, gsk};
   dim3 g(p.gx, p.gy, p.splits);
+  const int st = g2_storage(A, G, gsk);
   const int key = p.wm * 100 + p.tm * 10 + p.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a, bf16); break;
-    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a, bf16); break;
-    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a, bf16); break;
-    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a, bf16); break;
-    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a, bf16); break;
-    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a, bf16); break;
-    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a, bf16); break;
-    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a, bf16); break;
+    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a, bf16, st); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
-  if (p.splits > 1) return gemm_splitk_finish(partial, p.splits, M, N, bias, C, acc, sink, s);
+  if (p.splits > 1) return gemm_splitk_finish(partial, p.splits, M, N, bias, C, acc, sink, s, st == 1);
   return p.gx;
 }
 
@@ -705,17 +745,18 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
                        cdiv(g.M, p0.wm * p0.tm * 32), gsk};
   }
   const int sk = stats ? 1 : gs ? 2 : 0;
+  const int st = g2_storage(segs[0].A, segs[0].G, segs[0].gsk);
   dim3 grid(gx, p0.gy, n);
   const int key = p0.wm * 100 + p0.tm * 10 + p0.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
-    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16); break;
+    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();

@@ -206,7 +206,8 @@ static void colred(F f, E e, long seg_rows, int C, int nseg, double* scratch, hi
 // rpi-th row of its chunk, computes and stores the float4 result (functor F::out), and folds it
 // into the BN-backward sums of its channels; the rpi lanes of a channel quad meet in LDS and the
 // block writes partial (seg * chunks + chunk) of the GradSink.
-template <class F, int D>
+// YBF: the GradSink's BN input y in bf16 storage
+template <class F, int D, bool YBF>
 __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, long rpc,
                                                    GradSink g) {
   const int tpr_total = C >> 2;
@@ -233,7 +234,7 @@ __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, lo
 #pragma unroll
       for (int u = 0; u < D; ++u) {
         v[u] = f.load(base + m + u * rpi, c4);
-        if (g.part) yv[u] = *reinterpret_cast<const float4*>(g.y + (base + m + u * rpi) * C + c4 * 4);
+        if (g.part) yv[u] = ald4<YBF>(g.y, (base + m + u * rpi) * C + c4 * 4);
       }
 #pragma unroll
       for (int u = 0; u < D; ++u) {
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, lo
     }
     for (; m < m1; m += rpi) {
       const float4 o = f.out(f.load(base + m, c4), base + m, c4);
-      if (g.part) gs_acc4(g, k, o, *reinterpret_cast<const float4*>(g.y + (base + m) * C + c4 * 4), s1, s2);
+      if (g.part) gs_acc4(g, k, o, ald4<YBF>(g.y, (base + m) * C + c4 * 4), s1, s2);
     }
   }
   if (!g.part) return;
@@ -270,8 +271,12 @@ static int ew_gstats(F f, long seg_rows, int C, int nseg, GradSink g, hipStream_
   if (C % 4) throw std::runtime_error("ew_gstats: C % 4 != 0");
   RedPlan p = red_plan(seg_rows, C, nseg);
   g.P = nseg * p.chunks;
-  hipLaunchKernelGGL((k_ew_gstats<F, 4>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows, C,
-                     p.rpc, g);
+  if (g.part && g.ybf)
+    hipLaunchKernelGGL((k_ew_gstats<F, 4, true>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+                       C, p.rpc, g);
+  else
+    hipLaunchKernelGGL((k_ew_gstats<F, 4, false>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+                       C, p.rpc, g);
   PHX_LAUNCH_CHECK();
   return g.P;
 }
@@ -279,16 +284,17 @@ static int ew_gstats(F f, long seg_rows, int C, int nseg, GradSink g, hipStream_
 int ew_gstats_partials(long seg_rows, int C, int nseg) { return nseg * red_plan(seg_rows, C, nseg).chunks; }
 
 // ---- BN forward statistics ------------------------------------------------------------------
+template <bool BF>
 struct StatsAcc {
   const float* y;
   int C;
   float ref[4];
   __device__ void init(int, int c4, long base) {
-    float4 r = *reinterpret_cast<const float4*>(y + base * C + c4 * 4);
+    float4 r = ald4<BF>(y, base * C + c4 * 4);
     ref[0] = r.x; ref[1] = r.y; ref[2] = r.z; ref[3] = r.w;
   }
   using Raw = float4;
-  __device__ Raw load(long m, int c4) const { return *reinterpret_cast<const float4*>(y + m * C + c4 * 4); }
+  __device__ Raw load(long m, int c4) const { return ald4<BF>(y, m * C + c4 * 4); }
   __device__ void add(const Raw& v, float* a0, float* a1) const {
     float d[4] = {v.x - ref[0], v.y - ref[1], v.z - ref[2], v.w - ref[3]};
 #pragma unroll
@@ -309,8 +315,9 @@ struct StatsEpi {
   float* mmean;
   float* mvar;
   float eps;
+  int ybf = 0;  // y in bf16 storage
   __device__ void operator()(int, int c, double s0, double s1) const {
-    const double ref = y ? (double)y[c] : 0.0;
+    const double ref = !y ? 0.0 : ybf ? (double)ald1<true>(y, c) : (double)y[c];
     const double dm = s0 / (double)M;            // mean - ref
     double var = s1 / (double)M - dm * dm;
     if (var < 0.0) var = 0.0;
@@ -331,10 +338,10 @@ struct StatsEpi {
 
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
                      const float* gamma, float* sc, float* mmean, float* mvar, float eps,
-                     hipStream_t s) {
-  StatsAcc f{y, C, {0, 0, 0, 0}};
-  StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps};
-  colred(f, e, M, C, 1, part, s);
+                     hipStream_t s, bool ybf) {
+  StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps, ybf ? 1 : 0};
+  if (ybf) colred(StatsAcc<true>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
+  else colred(StatsAcc<false>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
 }
 
 // ---- BN statistics from producer partials (StatSink / GradSink) ---------------------------
@@ -472,6 +479,7 @@ void launch_bn_apply(const float* y, const float* mean, const float* rstd, const
 }
 
 // ---- BN backward ----------------------------------------------------------------------------
+template <bool BF>
 struct BwdAcc {
   const float* da;
   const float* y;
@@ -494,8 +502,7 @@ struct BwdAcc {
     float4 y, g;
   };
   __device__ Raw load(long m, int c4) const {
-    return Raw{*reinterpret_cast<const float4*>(y + m * C + c4 * 4),
-               *reinterpret_cast<const float4*>(da + m * C + c4 * 4)};
+    return Raw{ald4<BF>(y, m * C + c4 * 4), *reinterpret_cast<const float4*>(da + m * C + c4 * 4)};
   }
   __device__ void add(const Raw& r, float* a0, float* a1) const {
     float ys[4] = {r.y.x, r.y.y, r.y.z, r.y.w};
@@ -587,24 +594,28 @@ void launch_bn_bwd_finalize_group(const BnFinSeg* segs, int n, int C, hipStream_
   PHX_LAUNCH_CHECK();
 }
 
+template <bool BF>
 __global__ __launch_bounds__(256) void k_gx_materialize(GradX g, float4* __restrict__ out, long n4,
                                                         int C) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  out[i] = gx_load4(g, i * 4, (int)((i * 4) % C));
+  out[i] = gx_load4<BF>(g, i * 4, (int)((i * 4) % C));
 }
 
 void launch_bn_bwd_apply2(GradX g, float* out, long M, int C, hipStream_t s) {
   long n4 = M * C / 4;
-  hipLaunchKernelGGL(k_gx_materialize, dim3(cdiv(n4, 256)), dim3(256), 0, s, g, (float4*)out, n4, C);
+  if (g.y && g.ybf)
+    hipLaunchKernelGGL(k_gx_materialize<true>, dim3(cdiv(n4, 256)), dim3(256), 0, s, g, (float4*)out, n4, C);
+  else
+    hipLaunchKernelGGL(k_gx_materialize<false>, dim3(cdiv(n4, 256)), dim3(256), 0, s, g, (float4*)out, n4, C);
   PHX_LAUNCH_CHECK();
 }
 
 void launch_bn_bwd_reduce(const float* da, const float* y, const float* mean, const float* rstd,
                           const float* gamma, const float* beta, long M, int C, int act,
-                          double* part, float* mdz, float* mdzx, hipStream_t s) {
-  BwdAcc f{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}};
-  colred(f, BwdEpi2{M, mdz, mdzx}, M, C, 1, part, s);
+                          double* part, float* mdz, float* mdzx, hipStream_t s, bool ybf) {
+  if (ybf) colred(BwdAcc<true>{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}}, BwdEpi2{M, mdz, mdzx}, M, C, 1, part, s);
+  else colred(BwdAcc<false>{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}}, BwdEpi2{M, mdz, mdzx}, M, C, 1, part, s);
 }
 
 void launch_bn_bwd(const float* da, const float* y, const float* mean, const float* rstd,
@@ -612,7 +623,7 @@ void launch_bn_bwd(const float* da, const float* y, const float* mean, const flo
                    bool frozen, bool acc, double* part, float* coef, hipStream_t s) {
   if (C % 4) throw std::runtime_error("bn_bwd: C % 4");
   if (!frozen) {
-    BwdAcc f{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}};
+    BwdAcc<false> f{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}};
     BwdEpi e{M, rstd, gamma, coef};
     colred(f, e, M, C, 1, part, s);
   }
@@ -626,6 +637,7 @@ void launch_bn_bwd(const float* da, const float* y, const float* mean, const flo
 // squeeze-excite (efficientnet_model.py:184-196)
 // ------------------------------------------------------------------------------------------
 // per-image channel sums: pool (sum x) and backward (sum dy*x) through the column reduction
+template <bool BF>
 struct SumAcc {
   InX x;
   const float* g;  // optional second factor
@@ -639,7 +651,7 @@ struct SumAcc {
   };
   __device__ Raw load(long m, int c4) const {
     Raw r;
-    r.v = *reinterpret_cast<const float4*>(x.p + m * C + c4 * 4);
+    r.v = ald4<BF>(x.p, m * C + c4 * 4);
     if (g) r.w = *reinterpret_cast<const float4*>(g + m * C + c4 * 4);
     return r;
   }
@@ -857,7 +869,8 @@ static void se_mlp(const double* scratch, int chunks, int B, int C, int N, float
 void launch_se_fwd(InX x, float* y, int B, int HW, int C, int Cse, const float* w1,
                    const float* b1, const float* w2, const float* b2, int act, float* pool,
                    float* hidden, float* scale, hipStream_t s, double* scratch) {
-  const int chunks = colred_parts(SumAcc{x, nullptr, C, {}}, HW, C, B, scratch, s);
+  const int chunks = x.bf ? colred_parts(SumAcc<true>{x, nullptr, C, {}}, HW, C, B, scratch, s)
+                          : colred_parts(SumAcc<false>{x, nullptr, C, {}}, HW, C, B, scratch, s);
   se_mlp<0>(scratch, chunks, B, C, Cse, 1.0f / (float)HW, w1, b1, w2, b2, act, nullptr, pool, hidden, scale, s);
   (void)y;  // the excitation is folded into the consuming GEMM's A load (rowscale)
 }
@@ -896,7 +909,8 @@ int launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int C
                   bool acc, hipStream_t s, double* scratch, GradSink gs) {
   (void)b1; (void)b2; (void)pool;
   // gsum[0 .. B*C): dpool
-  const int chunks = colred_parts(SumAcc{x, dy, C, {}}, HW, C, B, scratch, s);
+  const int chunks = x.bf ? colred_parts(SumAcc<true>{x, dy, C, {}}, HW, C, B, scratch, s)
+                          : colred_parts(SumAcc<false>{x, dy, C, {}}, HW, C, B, scratch, s);
   se_mlp<1>(scratch, chunks, B, C, Cse, 1.f, w2t, nullptr, w1, nullptr, act, scale, nullptr,
             const_cast<float*>(hidden), gsum, s);
   return ew_gstats(SeBwdApply{dy, scale, gsum, dx, C, acc ? 1 : 0, 1.0f / (float)HW, {}, {}}, HW, C, B, gs, s);
@@ -914,18 +928,32 @@ __device__ __forceinline__ float4 drop_bwd4(const DropView& dv, long row, float4
   return make_float4((g.x * k) / dv.p, (g.y * k) / dv.p, (g.z * k) / dv.p, (g.w * k) / dv.p);
 }
 
-__global__ void k_add(InX a, InX b, float4* __restrict__ y, long n4, int C, DropView dv) {
+template <bool BF>
+__global__ void k_add(InX a, InX b, float* __restrict__ y, long n4, int C, DropView dv) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
   const int c = (int)((i * 4) % C);
-  float4 u = inx_load4(a, i * 4, c), v = inx_load4(b, i * 4, c);
+  float4 u = inx_load4<BF>(a, i * 4, c), v = inx_load4<BF>(b, i * 4, c);
   if (dv.keep) u = drop_fwd4(dv, i * 4 / C, u);
-  y[i] = make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w);
+  ast4<BF>(y, i * 4, make_float4(u.x + v.x, u.y + v.y, u.z + v.z, u.w + v.w));
 }
 
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s, DropView dv) {
   long n4 = n / 4;
-  hipLaunchKernelGGL(k_add, dim3(cdiv(n4, 256)), dim3(256), 0, s, a, b, (float4*)y, n4, C, dv);
+  if (a.bf != b.bf) throw std::runtime_error("add: operands differ in storage type");
+  if (a.bf) hipLaunchKernelGGL(k_add<true>, dim3(cdiv(n4, 256)), dim3(256), 0, s, a, b, y, n4, C, dv);
+  else hipLaunchKernelGGL(k_add<false>, dim3(cdiv(n4, 256)), dim3(256), 0, s, a, b, y, n4, C, dv);
+  PHX_LAUNCH_CHECK();
+}
+
+// widening copy of a bf16 activation (phx_debug_tap of a PHX_DTYPE_BF16 context)
+__global__ void k_bf16_to_f32(const float* __restrict__ src, float* __restrict__ dst, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = ald1<true>(src, i);
+}
+
+void launch_bf16_to_f32(const float* src, float* dst, long n, hipStream_t s) {
+  hipLaunchKernelGGL(k_bf16_to_f32, dim3(cdiv(n, 256)), dim3(256), 0, s, src, dst, n);
   PHX_LAUNCH_CHECK();
 }
 
@@ -1012,6 +1040,7 @@ int launch_copy_grad(const float* src, float* dst, long n, bool acc, hipStream_t
 // output element, which window tap held the maximum (first in row-major scan order, the element
 // TF's MaxPoolGrad routes the gradient to), so the backward is a gather of at most
 // ceil(k/s)^2 dy values per input element with no window re-scan.
+template <bool BF>
 __global__ void k_maxpool_fwd(InX x, float* __restrict__ y, uint8_t* __restrict__ amax, int B, int H,
                               int W, int C, int Ho, int Wo, int k, int st, int pt, int pl) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1031,14 +1060,14 @@ __global__ void k_maxpool_fwd(InX x, float* __restrict__ y, uint8_t* __restrict_
     for (int j = 0; j < k; ++j) {
       int ix = ox * st - pl + j;
       if (ix < 0 || ix >= W) continue;
-      const float v = inx_load1(x, (((long)b * H + iy) * W + ix) * C + c, c);
+      const float v = inx_load1<BF>(x, (((long)b * H + iy) * W + ix) * C + c, c);
       if (v > m || am == 0 && m == -INFINITY) {
         if (v > m) m = v;
         am = i * k + j + 1;
       }
     }
   }
-  y[idx] = m;
+  ast1<BF>(y, idx, m);
   amax[idx] = (uint8_t)(am - 1);
 }
 
@@ -1086,7 +1115,8 @@ __device__ __forceinline__ void quad_pos(int idx, int C4, int Wd, int Hd, int& c
 }
 
 // max-pool: TF MaxPool picks the first maximum of the window (strict > after the first element)
-__global__ __launch_bounds__(256) void k_maxpool_fwd4(InX x, float4* __restrict__ y, uint32_t* __restrict__ amax,
+template <bool BF>
+__global__ __launch_bounds__(256) void k_maxpool_fwd4(InX x, float* __restrict__ y, uint32_t* __restrict__ amax,
                                                       int H, int W, int C4, int Ho, int Wo, int k, int st, int pt,
                                                       int pl, int total4) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -1104,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd4(InX x, float4* __restrict_
     for (int j = 0; j < k; ++j) {
       const int ix = ox * st - pl + j;
       if (ix < 0 || ix >= W) continue;
-      float4 v4 = *reinterpret_cast<const float4*>(x.p + ((long)(b * H + iy) * W + ix) * C + c4 * 4);
+      float4 v4 = ald4<BF>(x.p, ((long)(b * H + iy) * W + ix) * C + c4 * 4);
       if (x.mu) v4 = inx_apply4(x, ck, v4);
       const float v[4] = {v4.x, v4.y, v4.z, v4.w};
 #pragma unroll
@@ -1115,7 +1145,7 @@ __global__ __launch_bounds__(256) void k_maxpool_fwd4(InX x, float4* __restrict_
         }
     }
   }
-  y[idx] = make_float4(m[0], m[1], m[2], m[3]);
+  ast4<BF>(y, (long)idx * 4, make_float4(m[0], m[1], m[2], m[3]));
   amax[idx] = (uint32_t)(am[0] & 255) | ((uint32_t)(am[1] & 255) << 8) | ((uint32_t)(am[2] & 255) << 16) |
               ((uint32_t)(am[3] & 255) << 24);
 }
@@ -1161,10 +1191,17 @@ void launch_maxpool_fwd(InX x, float* y, uint8_t* amax, int B, int H, int W, int
   long total = (long)B * Ho * Wo * C;
   if (quad_ok(total, C)) {
     const int t4 = (int)(total / 4);
-    hipLaunchKernelGGL(k_maxpool_fwd4, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, (float4*)y, (uint32_t*)amax, H, W,
-                       C / 4, Ho, Wo, k, stride, pt, pl, t4);
+    if (x.bf)
+      hipLaunchKernelGGL(k_maxpool_fwd4<true>, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, y, (uint32_t*)amax, H, W,
+                         C / 4, Ho, Wo, k, stride, pt, pl, t4);
+    else
+      hipLaunchKernelGGL(k_maxpool_fwd4<false>, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, y, (uint32_t*)amax, H, W,
+                         C / 4, Ho, Wo, k, stride, pt, pl, t4);
+  } else if (x.bf) {
+    hipLaunchKernelGGL(k_maxpool_fwd<true>, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, amax, B, H, W, C, Ho,
+                       Wo, k, stride, pt, pl);
   } else {
-    hipLaunchKernelGGL(k_maxpool_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, amax, B, H, W, C, Ho,
+    hipLaunchKernelGGL(k_maxpool_fwd<false>, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, amax, B, H, W, C, Ho,
                        Wo, k, stride, pt, pl);
   }
   PHX_LAUNCH_CHECK();
@@ -1192,6 +1229,7 @@ __device__ __forceinline__ int nn_src(int d, float scale, int in) {
   return s < in - 1 ? s : in - 1;
 }
 
+template <bool BF>
 __global__ void k_upsample_fwd(InX x, float* __restrict__ y, int B, int H,
                                int W, int C, int Ho, int Wo) {
   long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1205,7 +1243,7 @@ __global__ void k_upsample_fwd(InX x, float* __restrict__ y, int B, int H,
   int b = (int)(t / Ho);
   int sy = nn_src(oy, (float)H / (float)Ho, H);
   int sx = nn_src(ox, (float)W / (float)Wo, W);
-  y[idx] = inx_load1(x, (((long)b * H + sy) * W + sx) * C + c, c);
+  ast1<BF>(y, idx, inx_load1<BF>(x, (((long)b * H + sy) * W + sx) * C + c, c));
 }
 
 __global__ void k_upsample_bwd(const float* __restrict__ dy, float* __restrict__ dx, int B, int H,
@@ -1236,7 +1274,8 @@ __global__ void k_upsample_bwd(const float* __restrict__ dy, float* __restrict__
   dx[idx] = g;
 }
 
-__global__ __launch_bounds__(256) void k_upsample_fwd4(InX x, float4* __restrict__ y, int H, int W, int C4, int Ho,
+template <bool BF>
+__global__ __launch_bounds__(256) void k_upsample_fwd4(InX x, float* __restrict__ y, int H, int W, int C4, int Ho,
                                                        int Wo, int total4) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= total4) return;
@@ -1244,7 +1283,7 @@ __global__ __launch_bounds__(256) void k_upsample_fwd4(InX x, float4* __restrict
   quad_pos(idx, C4, Wo, Ho, c4, ox, oy, b);
   const int sy = nn_src(oy, (float)H / (float)Ho, H);
   const int sx = nn_src(ox, (float)W / (float)Wo, W);
-  y[idx] = inx_load4(x, ((long)(b * H + sy) * W + sx) * (C4 * 4) + c4 * 4, c4 * 4);
+  ast4<BF>(y, (long)idx * 4, inx_load4<BF>(x, ((long)(b * H + sy) * W + sx) * (C4 * 4) + c4 * 4, c4 * 4));
 }
 
 __global__ __launch_bounds__(256) void k_upsample_bwd4(const float4* __restrict__ dy, float4* __restrict__ dx, int H,
@@ -1278,10 +1317,14 @@ void launch_upsample_fwd(InX x, float* y, int B, int H, int W, int C, int Ho, in
   long total = (long)B * Ho * Wo * C;
   if (quad_ok(total, C)) {
     const int t4 = (int)(total / 4);
-    hipLaunchKernelGGL(k_upsample_fwd4, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, (float4*)y, H, W, C / 4, Ho, Wo, t4);
+    if (x.bf)
+      hipLaunchKernelGGL(k_upsample_fwd4<true>, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, y, H, W, C / 4, Ho, Wo, t4);
+    else
+      hipLaunchKernelGGL(k_upsample_fwd4<false>, dim3(cdiv(t4, 256)), dim3(256), 0, s, x, y, H, W, C / 4, Ho, Wo, t4);
+  } else if (x.bf) {
+    hipLaunchKernelGGL(k_upsample_fwd<true>, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo);
   } else {
-    hipLaunchKernelGGL(k_upsample_fwd, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho,
-                       Wo);
+    hipLaunchKernelGGL(k_upsample_fwd<false>, dim3(cdiv(total, 256)), dim3(256), 0, s, x, y, B, H, W, C, Ho, Wo);
   }
   PHX_LAUNCH_CHECK();
 }
@@ -1310,6 +1353,7 @@ struct FuseArgs {
 };
 
 
+template <bool BF>
 __global__ void k_fuse_fwd(FuseArgs fa, int nin, const float* __restrict__ w0,
                            const float* __restrict__ w1, const float* __restrict__ w2, int method,
                            int act, float* __restrict__ y, long n, int C) {
@@ -1318,11 +1362,12 @@ __global__ void k_fuse_fwd(FuseArgs fa, int nin, const float* __restrict__ w0,
   float wv[3], den;
   fuse_weights(w0, w1, w2, nin, method, wv, &den);
   const int c = (int)(i % C);
-  const float x0 = inx_load1(fa.x[0], i, c), x1 = inx_load1(fa.x[1], i, c);
-  const float x2 = nin > 2 ? inx_load1(fa.x[2], i, c) : 0.f;
-  y[i] = fuse_combine(x0, x1, x2, nin, method, wv, den, act);
+  const float x0 = inx_load1<BF>(fa.x[0], i, c), x1 = inx_load1<BF>(fa.x[1], i, c);
+  const float x2 = nin > 2 ? inx_load1<BF>(fa.x[2], i, c) : 0.f;
+  ast1<BF>(y, i, fuse_combine(x0, x1, x2, nin, method, wv, den, act));
 }
 
+template <bool BF>
 __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
                            const float* __restrict__ w1, const float* __restrict__ w2, int method,
                            int act, const float* __restrict__ dy, long n, int C) {
@@ -1331,8 +1376,8 @@ __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
   float wv[3], den;
   fuse_weights(w0, w1, w2, nin, method, wv, &den);
   const int c = (int)(i % C);
-  const float x0 = inx_load1(fa.x[0], i, c), x1 = inx_load1(fa.x[1], i, c);
-  const float x2 = nin > 2 ? inx_load1(fa.x[2], i, c) : 0.f;
+  const float x0 = inx_load1<BF>(fa.x[0], i, c), x1 = inx_load1<BF>(fa.x[1], i, c);
+  const float x2 = nin > 2 ? inx_load1<BF>(fa.x[2], i, c) : 0.f;
   float v;
   if (method == 0) {
     v = x0 * wv[0] / den;
@@ -1352,6 +1397,7 @@ __global__ void k_fuse_bwd(FuseArgs fa, int nin, const float* __restrict__ w0,
 }
 
 // channel-quad form of k_fuse_bwd (C % 4 == 0): identical per-element arithmetic, 16-B accesses
+template <bool BF>
 __global__ __launch_bounds__(256) void k_fuse_bwd4(FuseArgs fa, int nin, const float* __restrict__ w0,
                                                    const float* __restrict__ w1, const float* __restrict__ w2,
                                                    int method, int act, const float4* __restrict__ dy, long n4,
@@ -1361,8 +1407,8 @@ __global__ __launch_bounds__(256) void k_fuse_bwd4(FuseArgs fa, int nin, const f
   float wv[3], den;
   fuse_weights(w0, w1, w2, nin, method, wv, &den);
   const int c = (int)((i * 4) % C);
-  const float4 a0 = inx_load4(fa.x[0], i * 4, c), a1 = inx_load4(fa.x[1], i * 4, c);
-  const float4 a2 = nin > 2 ? inx_load4(fa.x[2], i * 4, c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 a0 = inx_load4<BF>(fa.x[0], i * 4, c), a1 = inx_load4<BF>(fa.x[1], i * 4, c);
+  const float4 a2 = nin > 2 ? inx_load4<BF>(fa.x[2], i * 4, c) : make_float4(0.f, 0.f, 0.f, 0.f);
   const float4 d4 = dy[i];
   const float x0[4] = {a0.x, a0.y, a0.z, a0.w}, x1[4] = {a1.x, a1.y, a1.z, a1.w}, x2[4] = {a2.x, a2.y, a2.z, a2.w};
   const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
@@ -1400,8 +1446,12 @@ void launch_fuse_fwd(const InX* xs, int nin, const float* wsm0, const float* wsm
                      hipStream_t s) {
   FuseArgs fa{};
   for (int i = 0; i < nin; ++i) fa.x[i] = xs[i];
-  hipLaunchKernelGGL(k_fuse_fwd, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
-                     method, act, y, n, C);
+  if (xs[0].bf)
+    hipLaunchKernelGGL(k_fuse_fwd<true>, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+                       method, act, y, n, C);
+  else
+    hipLaunchKernelGGL(k_fuse_fwd<false>, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+                       method, act, y, n, C);
   PHX_LAUNCH_CHECK();
 }
 
@@ -1414,11 +1464,17 @@ void launch_fuse_bwd(const InX* xs, int nin, const float* wsm0, const float* wsm
     fa.dx[i] = dxs[i];
     fa.acc[i] = acc[i] ? 1 : 0;
   }
-  if (C % 4 == 0)
-    hipLaunchKernelGGL(k_fuse_bwd4, dim3(cdiv(n / 4, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+  if (C % 4 == 0 && xs[0].bf)
+    hipLaunchKernelGGL(k_fuse_bwd4<true>, dim3(cdiv(n / 4, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
                        method, act, (const float4*)dy, n / 4, C);
+  else if (C % 4 == 0)
+    hipLaunchKernelGGL(k_fuse_bwd4<false>, dim3(cdiv(n / 4, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+                       method, act, (const float4*)dy, n / 4, C);
+  else if (xs[0].bf)
+    hipLaunchKernelGGL(k_fuse_bwd<true>, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+                       method, act, dy, n, C);
   else
-    hipLaunchKernelGGL(k_fuse_bwd, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
+    hipLaunchKernelGGL(k_fuse_bwd<false>, dim3(cdiv(n, 256)), dim3(256), 0, s, fa, nin, wsm0, wsm1, wsm2,
                        method, act, dy, n, C);
   PHX_LAUNCH_CHECK();
 }

@@ -55,6 +55,8 @@ __device__ __forceinline__ void nms_cand_append(const NmsCand& c, int b, int A, 
 // ------------------------------------------------------------------------------------------
 constexpr int kPreTile = 128;
 
+// BF: the class / box outputs are bf16 activations (PHX_DTYPE_BF16); widened to fp32 when staged
+template <bool BF>
 __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_base,
                                                  const float* __restrict__ box_base,
                                                  const LevelDesc* __restrict__ lev, int nlev,
@@ -73,10 +75,29 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
   const int nloc = L.h * L.w * na;                      // anchors of this level per image
   const int a0 = ((int)blockIdx.x - L.tile0) * kPreTile;  // first local anchor of the tile
   const int n = min(kPreTile, nloc - a0);
-  const long run = ((long)b * nloc + a0) * nclass;      // float offset of the tile's logits
-  const float* src = cls_base + L.cls_off + run;
+  const long run = ((long)b * nloc + a0) * nclass;      // element offset of the tile's logits
   const int nf = n * nclass;
   const int nf4 = nf >> 2;
+  if constexpr (BF) {
+    const long e0 = L.cls_off + run;
+    const uint16_t* src = reinterpret_cast<const uint16_t*>(cls_base) + e0;
+    if ((e0 & 3) == 0) {
+      const uint2* src4 = reinterpret_cast<const uint2*>(src);
+      int i = threadIdx.x;
+      for (; i + 768 < nf4; i += 1024) {
+        uint2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = unpack_bf16x4(v[u]);
+      }
+      for (; i < nf4; i += blockDim.x) smem4[i] = unpack_bf16x4(src4[i]);
+      for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = ald1<true>(cls_base, e0 + j);
+    } else {
+      for (int j = threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = ald1<true>(cls_base, e0 + j);
+    }
+  } else {
+  const float* src = cls_base + L.cls_off + run;
   const float4* src4 = reinterpret_cast<const float4*>(src);
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
     // staging: four 16-B loads in flight per lane before any LDS store
@@ -94,6 +115,7 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     // a run that starts off a 16-B boundary (an image of a level with an odd pixel count, e.g. a
     // 1x1 or 5x5 P7: h*w*9*90 floats per image): scalar staging
     for (int j = threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
+  }
   }
   __syncthreads();
   // two lanes per anchor (lanes t and t + 128 of the block are in different waves, so the halves
@@ -130,7 +152,7 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     am = ha_[t];
   }
   const long idx = (long)b * A + a;
-  const float4 bx = *reinterpret_cast<const float4*>(box_base + L.box_off + ((long)b * nloc + a0 + t) * 4);
+  const float4 bx = ald4<BF>(box_base, L.box_off + ((long)b * nloc + a0 + t) * 4);
   const float4 an = *reinterpret_cast<const float4*>(anchors + (long)a * 4);
   float yca = (an.x + an.z) / 2.0f;
   float xca = (an.y + an.w) / 2.0f;
@@ -164,10 +186,14 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
 void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDesc* lev_dev,
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
-                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand) {
+                    float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand, bool bf) {
   size_t shm = (size_t)kPreTile * nclass * sizeof(float);
-  hipLaunchKernelGGL(k_pre_nms, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,
-                     anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes, keep, cand);
+  if (bf)
+    hipLaunchKernelGGL(k_pre_nms<true>, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,
+                       anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes, keep, cand);
+  else
+    hipLaunchKernelGGL(k_pre_nms<false>, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,
+                       anchors, A, B, nclass, na, img_h, img_w, thresh, scores, classes, boxes, keep, cand);
   PHX_LAUNCH_CHECK();
 }
 
@@ -676,6 +702,7 @@ void launch_loss(const float* mraw, int B, const float* params, float* dm, float
 // dL/dm through sigmoid and the class reduce_max (ties split, TF _MaxGrad) into the input of
 // the class-predict pointwise conv: dx[pixel, :] += W[:, k*ncls + c] * dlogit
 // ------------------------------------------------------------------------------------------
+template <bool BF>
 __global__ __launch_bounds__(256) void k_cls_scatter(
     const float* __restrict__ scores, const uint8_t* __restrict__ keep,
     const float* __restrict__ mraw, const int* __restrict__ nties, const float* __restrict__ dm,
@@ -697,16 +724,16 @@ __global__ __launch_bounds__(256) void k_cls_scatter(
   const int local = a - L.anchor0;
   const int pix = local / na, k = local % na;
   const long prow = (long)b * L.h * L.w + pix;
-  const float* lg = cls_base + L.cls_off + prow * (na * nclass) + (long)k * nclass;
-  float m = lg[0];
-  for (int c = 1; c < nclass; ++c) m = fmaxf(m, lg[c]);
+  const long lg = L.cls_off + prow * (na * nclass) + (long)k * nclass;  // element offset (BF: bf16)
+  float m = ald1<BF>(cls_base, lg);
+  for (int c = 1; c < nclass; ++c) m = fmaxf(m, ald1<BF>(cls_base, lg + c));
   int nt = 0;
-  for (int c = 0; c < nclass; ++c) nt += (lg[c] == m);
+  for (int c = 0; c < nclass; ++c) nt += (ald1<BF>(cls_base, lg + c) == m);
   const float dlc = dl / (float)nt;
   float* dx = dx_base + dx_off[l] + prow * K;
   const int N = na * nclass;
   for (int c = 0; c < nclass; ++c) {
-    if (lg[c] != m) continue;
+    if (ald1<BF>(cls_base, lg + c) != m) continue;
     const int col = k * nclass + c;
     for (int j = 0; j < K; ++j) atomicAdd(dx + j, wpred[(long)j * N + col] * dlc);
   }
@@ -716,10 +743,14 @@ void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* m
                         const int* nties, const float* dm, const float* cls_base,
                         const LevelDesc* lev, int nlev, int A, int B, int nclass, int na,
                         const float* wpred, int K, float* dx_base, const long* dx_off,
-                        hipStream_t s) {
+                        hipStream_t s, bool bf) {
   long n = (long)B * A;
-  hipLaunchKernelGGL(k_cls_scatter, dim3(cdiv(n, 256)), dim3(256), 0, s, scores, keep, mraw, nties,
-                     dm, cls_base, lev, nlev, A, B, nclass, na, wpred, K, dx_base, dx_off);
+  if (bf)
+    hipLaunchKernelGGL(k_cls_scatter<true>, dim3(cdiv(n, 256)), dim3(256), 0, s, scores, keep, mraw, nties,
+                       dm, cls_base, lev, nlev, A, B, nclass, na, wpred, K, dx_base, dx_off);
+  else
+    hipLaunchKernelGGL(k_cls_scatter<false>, dim3(cdiv(n, 256)), dim3(256), 0, s, scores, keep, mraw, nties,
+                       dm, cls_base, lev, nlev, A, B, nclass, na, wpred, K, dx_base, dx_off);
   PHX_LAUNCH_CHECK();
 }
 

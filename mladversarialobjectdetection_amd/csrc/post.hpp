@@ -21,7 +21,7 @@ void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* m
                         const int* nties, const float* dm, const float* cls_base,
                         const LevelDesc* lev, int nlev, int A, int B, int nclass, int na,
                         const float* wpred, int K, float* dx_base, const long* dx_off,
-                        hipStream_t s);
+                        hipStream_t s, bool bf = false);  // bf: cls_base holds bf16 logits
 void launch_count_ge(const float* sc, const int* cnt, int B, int maxo, float th, float* out,
                      hipStream_t s);
 

@@ -149,6 +149,21 @@ def _rbf16(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+class Bf16Store(torch.autograd.Function):
+    """A tensor as a PHX_DTYPE_BF16 context stores it (SURVEY.md 8a R4 "C4: bf16 act"): every
+    activation the library writes — conv / depthwise / stem outputs (BN inputs), fuse, add and
+    resample outputs, the class / box head outputs — is rounded to bf16; BN outputs are computed on
+    load in fp32 and never stored.  Gradients stay fp32, so the backward is the identity."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _rbf16(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 class Bf16Conv1x1(torch.autograd.Function):
     """A 1x1 convolution as the library's bf16 GEMM computes it (PHX_DTYPE_BF16, SURVEY.md 8a R4
     "C4: bf16 act, fp32 acc"): operands rounded to bf16, products accumulated in full precision.
@@ -199,7 +214,8 @@ class Detector:
         # trainable=False (attack_detection.py:46-47; the library's bn=frozen mode); drop connect
         # still follows `training`
         self.bn_frozen = bn_frozen
-        # bf16: emulate the library's PHX_DTYPE_BF16 1x1-conv arithmetic (Bf16Conv1x1)
+        # bf16: emulate the library's PHX_DTYPE_BF16 arithmetic — bf16 1x1-conv operands
+        # (Bf16Conv1x1) and bf16 activation storage (Bf16Store)
         self.bf16 = False
         # drop-connect draws: dict(seed, step, gimg0, pass) — pass 0 first, 1 second, 2 detect
         self.drop = drop
@@ -232,7 +248,13 @@ class Detector:
             y = F.conv2d(x, wt, stride=stride)
         if bias is not None:
             y = y + self.w(bias).view(1, -1, 1, 1)
-        return y
+        if "/se/" in kname:  # the SE MLP runs on pooled vectors, nothing is stored
+            return y
+        return self.store(y)
+
+    def store(self, t):
+        """a tensor the library writes to its activation arena (bf16 storage in bf16 mode)"""
+        return Bf16Store.apply(t) if self.bf16 else t
 
     def dwconv(self, x, kname, stride=1):
         k = self.w(kname)  # [k,k,C,1]
@@ -241,7 +263,7 @@ class Detector:
         pt, pb = same_pads(x.shape[2], kk, stride)
         pl, pr = same_pads(x.shape[3], kk, stride)
         x = F.pad(x, (pl, pr, pt, pb))
-        return F.conv2d(x, wt, stride=stride, groups=x.shape[1])
+        return self.store(F.conv2d(x, wt, stride=stride, groups=x.shape[1]))
 
     def bn(self, x, pfx, act=False):
         """BatchNormalization (+ the activation that follows it when act=True).  With
@@ -357,7 +379,7 @@ class Detector:
             if s == 1 and inf == outf:
                 if self.training and "b0" not in bb:
                     x = self.drop_connect(x, idx, len(blocks))
-                x = x + inputs
+                x = self.store(x + inputs)
             if idx == len(blocks) - 1 or blocks[idx + 1][1] > 1:
                 reductions.append(x)
         return reductions[MIN_LEVEL - 1:MIN_LEVEL + 2]  # P3..P5 = reduction_3..5
@@ -392,11 +414,11 @@ class Detector:
         if h > th and w > tw:
             x = maybe_1x1(x)
             sh = (h - 1) // th + 1
-            x = self._tap(pfx + "/max_pool", self.maxpool(x, sh + 1, sh))
+            x = self._tap(pfx + "/max_pool", self.store(self.maxpool(x, sh + 1, sh)))
         else:
             x = maybe_1x1(x)
             if h < th or w < tw:
-                x = self._tap(pfx + "/upsample", self.upsample(x, th, tw))
+                x = self._tap(pfx + "/upsample", self.store(self.upsample(x, th, tw)))
         return x
 
     # ---- full network ---------------------------------------------------------------------------
@@ -424,7 +446,7 @@ class Detector:
                     wsm = [self.w(f"{npfx}/WSM" + ("" if i == 0 else f"_{i}")).reshape(()) for i in range(len(ins))]
                 nd_out = fuse_nodes(ins, wsm, self.cfg["fuse"])
                 oac = f"{npfx}/op_after_combine{len(allf)}"
-                v = self._tap(f"{npfx}/fuse", self.act(nd_out))
+                v = self._tap(f"{npfx}/fuse", self.store(self.act(nd_out)))
                 v = self.sepconv(v, oac + "/conv")
                 v = self.bn(v, oac + "/bn")
                 allf.append(v)

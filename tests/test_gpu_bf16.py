@@ -1,19 +1,25 @@
-"""GPU parity of the bf16 compute mode (PHX_DTYPE_BF16, BASELINE config 4 "bf16"): every 1x1 conv
-with more than 16 output channels (and every data gradient with more than 16 input channels) runs on
-v_mfma_f32_32x32x16_bf16 with its operands rounded to bf16 and fp32 accumulation; BN statistics,
-depthwise convs, EOT, loss and the patch gradient stay fp32.
+"""GPU parity of the bf16 compute mode (PHX_DTYPE_BF16, BASELINE config 4 "bf16"; SURVEY.md 8a R4
+"C4: bf16 act, fp32 acc"): every activation the library stores (conv / depthwise / stem outputs,
+fuse, add, resample and head outputs) is bf16 in HBM; every 1x1 conv with more than 16 output
+channels (and every data gradient with more than 16 input channels) runs on
+v_mfma_f32_32x32x16_bf16 with its operands rounded to bf16 and fp32 accumulation; BN statistics
+(taken over the stored values), gradients, EOT, loss and the patch gradient stay fp32.
 
 Two references:
   * the fp64 oracle (the reference's arithmetic): SURVEY.md 8c's C4 tolerance — loss rel <= 1e-2,
     d patch cosine >= 0.99;
-  * the fp64 oracle with the same bf16 rounding points (oracle.detector.Bf16Conv1x1).  Layer by
-    layer, where both sides still have fp32-exact inputs (the first bf16 convs), the GPU's outputs
-    must equal the emulation 20x more closely than the emulation equals fp64 — this pins which
-    operands are rounded.  Deeper, bf16 noise (~2^-9) is amplified like any perturbation of this
+  * the fp64 oracle with the same bf16 rounding points (oracle.detector.Bf16Conv1x1 for the GEMM
+    operands, Bf16Store for the stored activations).  Layer by layer, in the first layers, the GPU's
+    outputs must equal the emulation 20x more closely than the emulation equals fp64 — this pins
+    which values are rounded.  Deeper, bf16 noise (~2^-9) is amplified like any perturbation of this
     synthetic-weight net (training-mode BN over a 2-image batch, P7 over 2 rows; max-pool and class
-    maxima whose top taps are that close resolve differently in any two bf16 evaluations), so the
-    end results are held to the same order as the bf16 arithmetic's own deviation from fp64: loss
-    rel <= 1e-4, ||d - d_emul|| <= 2 ||d_emul - d_fp64||, cosine >= 0.99.
+    maxima whose top taps are that close resolve differently in any two bf16 evaluations; with bf16
+    storage every stored activation is a rounding point, and an element whose fp32 and fp64
+    pre-rounding values straddle a rounding boundary lands a bf16 quantum apart), so the end results
+    are held to the same order as the bf16 arithmetic's own deviation from fp64:
+    |loss - loss_emul| <= max(1e-4 |loss_emul|, 3 |loss_emul - loss_fp64|) (a scalar: in the deep
+    layers the GPU's and the emulation's roundings become independent draws of the same noise),
+    ||d - d_emul|| <= 2 ||d_emul - d_fp64||, cosine >= 0.99.
 """
 import numpy as np
 import pytest
@@ -35,10 +41,10 @@ def _cos(a, b):
 
 
 def test_bf16_gemm_rounding_points_match_emulation():
-    """The first 1x1 convs of the second pass, whose inputs are still fp32-exact on both sides: the
-    GPU's conv outputs (BN inputs, read back through phx_debug_tap) equal the emulated bf16
-    arithmetic far more closely than that arithmetic equals fp64.  blocks_0's project conv (16
-    outputs) runs on the fp32 register kernel, so there GPU and fp64 agree to fp32 precision."""
+    """The first convs of the second pass: the GPU's stored conv outputs (BN inputs, bf16, read back
+    widened through phx_debug_tap) equal the emulated bf16 arithmetic far more closely than that
+    arithmetic equals fp64.  blocks_0's project conv (16 outputs) runs on the fp32 register kernel:
+    there only its bf16 input and output storage are rounding points."""
     from mladversarialobjectdetection_amd import weights as W
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
     from oracle import detector as D
@@ -66,8 +72,8 @@ def test_bf16_gemm_rounding_points_match_emulation():
             D.Detector.__init__ = orig
         taps[bf] = r["det"].taps
     b0 = "efficientnet-b0/blocks_0/tpu_batch_normalization_1"
-    for name, bf_layer in ((b0, False), ("efficientnet-b0/blocks_1/tpu_batch_normalization", True),
-                           ("efficientnet-b0/blocks_1/tpu_batch_normalization_2", True)):
+    for name in (b0, "efficientnet-b0/blocks_1/tpu_batch_normalization",
+                 "efficientnet-b0/blocks_1/tpu_batch_normalization_2"):
         x_emul = taps[True][name][0].detach().permute(0, 2, 3, 1).numpy()
         x_64 = taps[False][name][0].detach().permute(0, 2, 3, 1).numpy()
         buf = torch.empty(x_emul.size, device="cuda")
@@ -75,11 +81,18 @@ def test_bf16_gemm_rounding_points_match_emulation():
                    torch.cuda.current_stream().cuda_stream)
         x_gpu = buf.cpu().numpy().reshape(x_emul.shape).astype(np.float64)
         e_gpu, e_emul = _rel(x_gpu, x_emul), _rel(x_emul, x_64)
-        if bf_layer:
-            assert e_emul > 1e-4, (name, e_emul)  # visibly bf16
-            assert e_gpu <= 0.05 * e_emul, (name, e_gpu, e_emul)
-        else:
-            assert e_emul == 0.0 and e_gpu <= 1e-5, (name, e_gpu)
+        exact = float(np.mean(x_gpu == x_emul))
+        print(f"{name}: gpu vs emulation {e_gpu:.3e}, emulation vs fp64 {e_emul:.3e}, bit-equal {exact:.5f}")
+        assert e_emul > 1e-4, (name, e_emul)  # visibly bf16
+        # Both sides store the same bf16 values except where the fp32 and fp64 pre-rounding values
+        # fall on either side of a rounding boundary; each such flip moves one element by a bf16
+        # quantum, which BN (channels with |mean| >> std) and the next layers amplify.  A wrong
+        # rounding point would leave almost no element bit-equal.
+        assert exact >= 0.9, (name, exact)
+        assert e_gpu <= 0.25 * e_emul, (name, e_gpu, e_emul)
+        # the stored values are bf16: the widened tap has no bits below bf16's 8-bit significand
+        assert np.array_equal(x_gpu, x_gpu.astype(np.float32).view(np.uint32).__and__(0xFFFF0000)
+                              .view(np.float32).astype(np.float64)), name
 
 
 def test_bf16_step_matches_oracle():
@@ -107,7 +120,9 @@ def test_bf16_step_matches_oracle():
     assert abs(loss - r64["loss"]) <= 1e-2 * abs(r64["loss"])
     assert _cos(gp, r64["grad"][:-1]) >= 0.99
     # against the same bf16 rounding points
-    assert abs(loss - rem["loss"]) <= 1e-4 * abs(rem["loss"])
+    # the same order as the bf16 arithmetic's own deviation from fp64 (see the module docstring)
+    assert abs(loss - rem["loss"]) <= max(1e-4 * abs(rem["loss"]), 3 * abs(rem["loss"] - r64["loss"])), \
+        (loss, rem["loss"], r64["loss"])
     e_gpu, e_emul = _rel(gp, rem["grad"][:-1]), _rel(rem["grad"][:-1], r64["grad"][:-1])
     assert e_gpu <= 2 * e_emul, (e_gpu, e_emul)
     assert _cos(gp, rem["grad"][:-1]) >= 0.99
@@ -156,7 +171,9 @@ def test_bf16_d4_256_matches_emulation_oracle():
     gp = g[:-1]
     assert abs(loss - r64["loss"]) <= 1e-2 * abs(r64["loss"])
     assert _cos(gp, r64["grad"][:-1]) >= 0.99
-    assert abs(loss - rem["loss"]) <= 1e-4 * abs(rem["loss"])
+    # the same order as the bf16 arithmetic's own deviation from fp64 (see the module docstring)
+    assert abs(loss - rem["loss"]) <= max(1e-4 * abs(rem["loss"]), 3 * abs(rem["loss"] - r64["loss"])), \
+        (loss, rem["loss"], r64["loss"])
     e_gpu, e_emul = _rel(gp, rem["grad"][:-1]), _rel(rem["grad"][:-1], r64["grad"][:-1])
     assert e_gpu <= 2 * e_emul, (e_gpu, e_emul)
     assert _cos(gp, rem["grad"][:-1]) >= 0.99
@@ -165,13 +182,20 @@ def test_bf16_d4_256_matches_emulation_oracle():
 @pytest.mark.timeout(600)
 def test_bf16_d4_1024_four_images():
     """C4's model, size and per-GPU batch (D4 1024^2, 4 images, bf16): finite and non-trivial,
-    bit-identical on rerun (step and detector), and the step agrees with the fp32 build of the same
-    victim within SURVEY 8c's C4 tolerance (loss rel <= 1e-2, d patch cosine >= 0.99; per-image max
-    scores within 2e-2), at the well-conditioned weight draw above.  The fp64 oracle at this size
-    would need ~100 GB of host memory, so the fp32 build (parity-tested against it at 256^2 in
-    test_gpu_deep.py) is the reference here.  (D4's drop connect keys its draws by batch position,
-    so a permuted batch is not expected to give permuted outputs; D0's equivariance is tested in
-    test_gpu_fullsize.py.)"""
+    bit-identical on rerun (step and detector), and against the fp32 build of the same victim, at
+    the well-conditioned weight draw above:
+      * the step within SURVEY 8c's C4 tolerance (loss rel <= 1e-2, d patch cosine >= 0.99);
+      * the detector anchor by anchor: |score difference| <= 3e-2 everywhere, median <= 3e-3,
+        classes agree on >= 99 % of the anchors and every image's top person anchor is the same;
+      * the step's per-image max scores within 0.1.  They are maxima over the anchors that pass
+        filter_valid_boxes (attacker.py:69-89), and the decoded boxes come from bf16 box outputs: an
+        anchor whose box height or width is within bf16 precision of the image side is valid in one
+        build and not in the other (measured: every anchor's score within 0.017, one image's max
+        0.794 in fp32 against 0.745 in bf16 through such a flip).
+    The fp64 oracle at this size would need ~100 GB of host memory, so the fp32 build (parity-tested
+    against it at 256^2 in test_gpu_deep.py) is the reference here.  (D4's drop connect keys its
+    draws by batch position, so a permuted batch is not expected to give permuted outputs; D0's
+    equivariance is tested in test_gpu_fullsize.py.)"""
     from mladversarialobjectdetection_amd import _lib
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
     B4 = 4
@@ -188,20 +212,27 @@ def test_bf16_d4_1024_four_images():
         met = att.metrics_buf.cpu().numpy().copy()
         m = torch.empty(B4, device="cuda")
         v.ctx.call("phx_debug_last_maxscores", m.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        _, s0, c0 = v.detect(imgs)
         if dt == "bf16":
             att.call(imgs, boxes=boxes)
             torch.cuda.synchronize()
             assert torch.isfinite(g1).all()
             assert g1[:-1].abs().sum() > 0
             assert torch.equal(att.grad, g1)
-            _, s0, c0 = v.detect(imgs)
             _, s1, c1 = v.detect(imgs)
             assert torch.equal(s0, s1) and torch.equal(c0, c1)
-        res[dt] = (g1.cpu().numpy().astype(np.float64), met, m.cpu().numpy())
+        res[dt] = (g1.cpu().numpy().astype(np.float64), met, m.cpu().numpy(), s0.cpu().numpy(), c0.cpu().numpy())
         del att, v
         torch.cuda.empty_cache()
-    (gb, mb, sb), (gf, mf, sf) = res["bf16"], res["f32"]
+    (gb, mb, sb, db, cb), (gf, mf, sf, df, cf) = res["bf16"], res["f32"]
+    print(f"loss bf16 {mb[_lib.M_LOSS]:.6f} f32 {mf[_lib.M_LOSS]:.6f}; max scores {sb} vs {sf}; "
+          f"d patch cosine {_cos(gb[:-1], gf[:-1]):.6f}, rel {_rel(gb[:-1], gf[:-1]):.3e}")
     assert abs(mb[_lib.M_LOSS] - mf[_lib.M_LOSS]) <= 1e-2 * abs(mf[_lib.M_LOSS])
-    assert np.abs(sb - sf).max() <= 2e-2, (sb, sf)
     assert _cos(gb[:-1], gf[:-1]) >= 0.99, _cos(gb[:-1], gf[:-1])
+    d = np.abs(db - df)
+    assert d.max() <= 3e-2 and np.median(d) <= 3e-3, (d.max(), np.median(d))
+    assert np.mean(cb == cf) >= 0.99
+    for b in range(B4):
+        assert np.argmax(db[b] * (cb[b] == 0)) == np.argmax(df[b] * (cf[b] == 0)), b
+    assert np.abs(sb - sf).max() <= 0.1, (sb, sf)
     assert mb[_lib.M_NBOX] == mf[_lib.M_NBOX] and mb[_lib.M_NIMG] == B4
