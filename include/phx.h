@@ -202,6 +202,19 @@ int phx_letterbox(phx_ctx* ctx, const uint8_t* src, const int64_t* offsets, cons
 int phx_augment(phx_ctx* ctx, const float* in, int B, int H, int W, int64_t step, int global_image_offset,
                 float* out, void* stream);
 
+/* Inference-time patch compositor: AdversarialPatch.add_adv_to_img (adv_patch.py:16-201) for a batch
+ * of uint8 RGB images [B,H,W,3] on the device, modified in place.  boxes / count are HOST arrays:
+ * boxes [B][max_boxes][4] (ymin, xmin, ymax, xmax in pixels), count [B].  patch [P,P,3] uint8
+ * (device) is the unprinted patch (patch.png); the library prints it (print_patch, :40-58).  Boxes
+ * are pasted in order, each brightness-matched (cv2 YUV, :110-131) against the image as patched so
+ * far rescaled into out_h x out_w (:93-108), resized to the box's patch (cv2 INTER_AREA down,
+ * INTER_CUBIC up, :151-164), with U(-0.01, 0.01) noise (:140-149; Philox keyed by ctx seed, step,
+ * global image index, box slot).  A patch side below 1 or beyond the image is PHX_EINVAL (the
+ * reference's cv2 / numpy raise there).  The first call allocates a small scratch (synchronous). */
+int phx_adv_patch(phx_ctx* ctx, uint8_t* images, int B, int H, int W, const float* boxes, const int32_t* count,
+                  int max_boxes, const uint8_t* patch, int patch_size, double scale, int out_h, int out_w,
+                  int64_t step, int global_image_offset, void* stream);
+
 /* Per-launch-group device timing (HIP events on the launch stream).  enable=1 clears and
  * starts recording; phx_profile_report synchronises and writes JSON
  * {kind: {count, ms, flops, bytes}} with the algorithmic FLOPs / bytes of the launches. */

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import json
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int, c_int64, c_size_t, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_uint64, c_void_p
 
 ABI_VERSION = 2
 PATCH_SIZE = 640
@@ -82,6 +82,9 @@ _SIGS = [
     ("phx_letterbox", c_int,
      [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("phx_augment", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int64, c_int, c_void_p, c_void_p]),
+    ("phx_adv_patch", c_int,
+     [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_double, c_int, c_int,
+      c_int64, c_int, c_void_p]),
     ("phx_profile", c_int, [c_void_p, c_int]),
     ("phx_profile_report", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
     ("phx_debug_last_patched", c_int, [c_void_p, c_void_p, c_void_p]),

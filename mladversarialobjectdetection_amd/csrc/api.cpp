@@ -211,6 +211,8 @@ struct phx_ctx {
   // scratch for phx_augment (per-image channel-sum partials)
   DPtr aug_ws;
   size_t aug_cap = 0;
+  DPtr ap_ws;          // inference compositor scratch (phx_adv_patch)
+  size_t ap_cap = 0;
   // scratch for phx_brightness_match (Y-mean partials), grown on demand
   DPtr bm_ws;
   size_t bm_cap = 0;
@@ -1635,6 +1637,69 @@ int phx_augment(phx_ctx* ctx, const float* in, int B, int H, int W, int64_t step
   }
   launch_augment(in, out, B, H, W, ctx->seed, step, global_image_offset,
                  reinterpret_cast<double*>(ctx->aug_ws.get()), (hipStream_t)stream);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_adv_patch(phx_ctx* ctx, uint8_t* images, int B, int H, int W, const float* boxes, const int32_t* count,
+                  int max_boxes, const uint8_t* patch, int patch_size, double scale, int out_h, int out_w,
+                  int64_t step, int global_image_offset, void* stream) {
+  if (!ctx) return PHX_EINVAL;
+  if (!images || !boxes || !count || !patch || B <= 0 || H <= 0 || W <= 0 || max_boxes < 0 || patch_size <= 0 ||
+      out_h <= 0 || out_w <= 0)
+    return fail(ctx, PHX_EINVAL, "adv_patch: null pointer or empty shape");
+  PHX_TRY(ctx)
+  PHX_HIP(hipSetDevice(ctx->device));
+  hipStream_t s = (hipStream_t)stream;
+  const int P = patch_size;
+  // placements (AdversarialPatch._create, adv_patch.py:60-91), in double as Python computes them
+  int rounds = 0;
+  std::vector<ApBox> tab;
+  for (int b = 0; b < B; ++b) {
+    if (count[b] < 0 || count[b] > max_boxes) throw std::invalid_argument("adv_patch: box count out of range");
+    rounds = std::max(rounds, (int)count[b]);
+  }
+  tab.assign((size_t)std::max(rounds, 1) * B, ApBox{0, 0, 0, 0, 0});
+  std::vector<int> round_pix(std::max(rounds, 1), 0);
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < count[b]; ++k) {
+      const float* q = boxes + ((size_t)b * max_boxes + k) * 4;
+      // float32 boxes (the detector's dtype) under numpy's promotion: h, w in float32, then float64
+      const double ymin = q[0], xmin = q[1];
+      const double h = (float)(q[2] - q[0]), w = (float)(q[3] - q[1]);
+      const double long_side = std::max(h, w);
+      const int pw = (int)(long_side * scale), ph = pw;
+      if (ph < 1) throw std::invalid_argument("adv_patch: patch side below 1 pixel (cv2.resize to an empty size)");
+      if (ph > H || pw > W) throw std::invalid_argument("adv_patch: patch larger than the image");
+      double ymp = std::max((ymin + h / 2.0) - ph / 2.0, 0.0), xmp = std::max((xmin + w / 2.0) - pw / 2.0, 0.0);
+      if (ymp + ph > H) ymp = H - ph;
+      if (xmp + pw > W) xmp = W - pw;
+      tab[(size_t)k * B + b] = ApBox{1, (int)ymp, (int)xmp, ph, pw};
+      round_pix[k] = std::max(round_pix[k], ph * pw);
+    }
+  // the rescale of AdversarialPatch.rescale (adv_patch.py:93-108)
+  const double sc = std::min((double)out_w / W, (double)out_h / H);
+  const int sh = (int)(H * sc), sw = (int)(W * sc);
+  if (sh < 1 || sw < 1) throw std::invalid_argument("adv_patch: the rescaled image is empty");
+  const size_t need = (size_t)P * P * 3 + sizeof(unsigned long long) * (1 + (size_t)B) + sizeof(ApBox) * tab.size() + 64;
+  if (need > ctx->ap_cap) {
+    ctx->ap_ws.reset(dalloc<char>(need));
+    ctx->ap_cap = need;
+  }
+  char* ws = static_cast<char*>(ctx->ap_ws.get());
+  auto* ysum = reinterpret_cast<unsigned long long*>(ws);
+  auto* ysrc = ysum + B;
+  auto* dtab = reinterpret_cast<ApBox*>(ysrc + 1);
+  uint8_t* printed = reinterpret_cast<uint8_t*>(dtab + tab.size());
+  PHX_HIP(hipMemcpyAsync(dtab, tab.data(), sizeof(ApBox) * tab.size(), hipMemcpyHostToDevice, s));
+  launch_ap_print(patch, printed, P, ysrc, s);
+  for (int k = 0; k < rounds; ++k) {
+    launch_ap_ysum(images, B, H, W, out_h, out_w, sh, sw, ysum, s);
+    launch_ap_paste(images, B, H, W, printed, P, dtab + (size_t)k * B, round_pix[k], k, ysum, ysrc, out_h, out_w,
+                    ctx->seed, step, global_image_offset, s);
+  }
+  // the host table must outlive its (pageable, staged) copy
+  PHX_HIP(hipStreamSynchronize(s));
   return PHX_OK;
   PHX_CATCH(ctx)
 }

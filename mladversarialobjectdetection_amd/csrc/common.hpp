@@ -401,6 +401,8 @@ enum RngStream : uint32_t {
   RNG_DSHUF = 7,      // defender Masker: per image shuffle key (attack_detection.py:487)
   RNG_DFLIP = 8,      // defender Masker: per image left-right / up-down flips (:488-489)
   RNG_DROPOUT = 9,    // defender U-Net: per (layer, image, element) Dropout(0.2) uniform
+  RNG_APNOISE = 10,   // inference compositor: per (image, box slot, element pair) U(-.01, .01)
+                      // (adv_patch.py:144-149)
 };
 
 }  // namespace phx

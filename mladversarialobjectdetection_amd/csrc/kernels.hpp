@@ -250,4 +250,19 @@ void launch_letterbox(const uint8_t* src, const int64_t* offsets, const int32_t*
 size_t augment_scratch_doubles(int B);
 void launch_augment(const float* in, float* out, int B, int H, int W, uint64_t seed, int64_t step,
                     int gimg0, double* scratch, hipStream_t s);
+// ---- inference compositor (kernels_advpatch.hip, adv_patch.py) ------------------------------
+struct ApBox {
+  int valid;      // this image has a box in this round
+  int y, x;       // patch origin (AdversarialPatch._create)
+  int ph, pw;     // patch size (square)
+};
+// printed = (raw + 127) >> 1 per byte ([P,P,3]); *ysum = sum of its Y (zeroed first)
+void launch_ap_print(const uint8_t* raw, uint8_t* printed, int P, unsigned long long* ysum, hipStream_t s);
+// ysum[b] = sum of Y over the out_h x out_w rescale of image b (its sh x sw content + grey letterbox)
+void launch_ap_ysum(const uint8_t* img, int B, int H, int W, int out_h, int out_w, int sh, int sw,
+                    unsigned long long* ysum, hipStream_t s);
+// paste round `slot`: boxes[b] for every image (device), max_pix = largest ph * pw of the round
+void launch_ap_paste(uint8_t* img, int B, int H, int W, const uint8_t* printed, int P, const ApBox* boxes,
+                     int max_pix, int slot, const unsigned long long* ysum, const unsigned long long* ysrc, int out_h,
+                     int out_w, uint64_t seed, int64_t step, int gimg0, hipStream_t s);
 }  // namespace phx

@@ -1061,7 +1061,7 @@ __global__ void k_maxpool_fwd(InX x, float* __restrict__ y, uint8_t* __restrict_
       int ix = ox * st - pl + j;
       if (ix < 0 || ix >= W) continue;
       const float v = inx_load1<BF>(x, (((long)b * H + iy) * W + ix) * C + c, c);
-      if (v > m || am == 0 && m == -INFINITY) {
+      if (v > m || (am == 0 && m == -INFINITY)) {
         if (v > m) m = v;
         am = i * k + j + 1;
       }
