@@ -45,8 +45,11 @@ enum {
 
 /* BN modes.  LOCAL = training-mode batch statistics over the rank's batch, as
  * the reference's attack step (victim inherits training=True, attacker.py:172); FROZEN =
- * inference BN with moving statistics (attacker.py:325 test_step). */
-enum { PHX_BN_LOCAL = 0, PHX_BN_FROZEN = 1 };
+ * inference BN with moving statistics (attacker.py:325 test_step); SYNC = training-mode
+ * statistics over the global batch of all ranks (SyncBN: the per-channel [n, sum x, sum x^2]
+ * of every BN forward and [n, sum dz, sum dz*xhat] of every BN backward are SUM-reduced through
+ * the caller's collective, phx_set_allreduce), equal to one reference step on the whole batch. */
+enum { PHX_BN_LOCAL = 0, PHX_BN_FROZEN = 1, PHX_BN_SYNC = 2 };
 
 /* Arithmetic of the victim's 1x1 convolutions ("C4: bf16 act, fp32 acc").
  * F32: fp32 matrix cores (the reference's precision, BASELINE configs 1-3).  BF16: bf16 matrix
@@ -58,7 +61,7 @@ typedef struct phx_config {
                                (hparams_config.py:301-467)                                  */
   int image_size;           /* 0 = model default; square images only                         */
   int max_batch;            /* per-rank batch capacity (workspace is sized for it)            */
-  int bn_mode;              /* PHX_BN_LOCAL / PHX_BN_FROZEN                                   */
+  int bn_mode;              /* PHX_BN_LOCAL / PHX_BN_FROZEN / PHX_BN_SYNC                     */
   float score_thresh;       /* nms_configs.score_thresh (hparams_config.py:258-266 default 0;
                                attacker_train.py:31 override 0.5).  As the reference: the first
                                pass keeps scores >= it (attacker.py:83-84) and gaussian soft-NMS
@@ -68,6 +71,15 @@ typedef struct phx_config {
 } phx_config;
 
 typedef struct phx_ctx phx_ctx;
+
+/* bn=sync's collective: SUM-reduce n doubles at device address buf across the ranks, in place,
+ * ordered on `stream` after the library's work so far and before its next launch (an RCCL
+ * all-reduce enqueued on the stream, or a blocking one).  Returns 0 on success.  The library calls
+ * it from phx_step_grad / phx_detect / phx_first_pass of a PHX_BN_SYNC context, once per BN (per
+ * head group) and pass; every rank must run the same steps.  Replaces the cross-replica sums of
+ * the reference's SyncBatchNormalization (automl/efficientdet/utils.py:205-241). */
+typedef int (*phx_allreduce_fn)(void* user, double* buf, size_t n, void* stream);
+int phx_set_allreduce(phx_ctx* ctx, phx_allreduce_fn fn, void* user);
 
 /* Per-step metrics written by phx_step_grad (host-readable device or host memory, PHX_NMETRIC
  * floats), the reference's add_metric set, attacker.py:196-207. */

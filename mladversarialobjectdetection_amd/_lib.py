@@ -22,7 +22,7 @@ MAX_OUT = 100
 M_LOSS, M_SCALE_LOSS, M_TV, M_SUM_M, M_SUM_M2, M_ASR_NUM, M_ASR_DEN, M_NBOX, M_NIMG = range(9)
 NMETRIC = 9
 
-BN_LOCAL, BN_FROZEN = 0, 1
+BN_LOCAL, BN_FROZEN, BN_SYNC = 0, 1, 2
 DTYPE_F32, DTYPE_BF16 = 0, 1
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -82,6 +82,7 @@ _SIGS = [
     ("phx_letterbox", c_int,
      [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     ("phx_augment", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int64, c_int, c_void_p, c_void_p]),
+    ("phx_set_allreduce", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_adv_patch", c_int,
      [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int, c_double, c_int, c_int,
       c_int64, c_int, c_void_p]),

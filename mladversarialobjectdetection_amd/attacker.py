@@ -16,6 +16,7 @@ GPU, each holding B/world images; the [patch | scale] gradient is SUM-all-reduce
 """
 from __future__ import annotations
 
+import ctypes
 import math
 import os
 from collections.abc import Mapping
@@ -98,10 +99,17 @@ class EfficientDetVictim:
         self.device = device
         if dtype not in ("f32", "bf16"):
             raise ValueError("dtype must be 'f32' (the reference's precision) or 'bf16'")
-        self.ctx = _lib.Context(model_name, image_size, max_batch,
-                                _lib.BN_FROZEN if bn_mode == "frozen" else _lib.BN_LOCAL,
-                                score_thresh, rng_seed, device,
+        modes = {"local": _lib.BN_LOCAL, "frozen": _lib.BN_FROZEN, "sync": _lib.BN_SYNC}
+        if bn_mode not in modes:
+            raise ValueError("bn_mode must be 'local', 'frozen' or 'sync'")
+        self.ctx = _lib.Context(model_name, image_size, max_batch, modes[bn_mode], score_thresh, rng_seed, device,
                                 _lib.DTYPE_BF16 if dtype == "bf16" else _lib.DTYPE_F32)
+        self.bn_mode = bn_mode
+        if bn_mode == "sync":
+            # SyncBN: the library hands every BN's per-channel sums to this collective
+            from .distributed import bn_sync_callback
+            self._ar = bn_sync_callback()
+            self.ctx.call("phx_set_allreduce", ctypes.cast(self._ar, ctypes.c_void_p), None)
         self.dtype = dtype
         self.manifest = self.ctx.manifest()
         if isinstance(weights, str) and weights == "synthetic":

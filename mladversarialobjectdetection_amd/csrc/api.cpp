@@ -126,6 +126,7 @@ struct Exec {
   float* inj_boxes = nullptr;
   int* inj_count = nullptr;
   float* dscale_scratch = nullptr;  // dL/dscale of a gradient-free (eval) step
+  double* sync_sums = nullptr;      // bn=sync: [member][C][3] per-channel sums to all-reduce
 
   bool bf16 = false;  // the context's compute dtype (GEMM plans depend on it)
   // activations (the arena tensors) stored as bf16: PHX_DTYPE_BF16, SURVEY.md 8a R4 "C4: bf16 act";
@@ -187,6 +188,10 @@ struct phx_ctx {
   int device = 0;
   int max_batch = 0;
   int bn_mode = PHX_BN_LOCAL;
+  // bn=sync: the caller's SUM all-reduce of the BN sums (phx_set_allreduce)
+  phx_allreduce_fn ar_fn = nullptr;
+  void* ar_user = nullptr;
+  bool batch_bn() const { return bn_mode != PHX_BN_FROZEN; }  // training-mode batch statistics
   bool bf16 = false;  // PHX_DTYPE_BF16: bf16 matrix cores for the 1x1 convs
   // nms_configs.score_thresh: the first pass keeps scores >= filter_thresh (attacker.py:83-84);
   // gaussian soft-NMS keeps scores > nms_thresh = score_thresh or 0.001 (postprocess.py:186-188)
@@ -449,7 +454,7 @@ Exec& phx_ctx::exec_for(int B) {
   E.B = B;
   E.bf16 = bf16;
   E.abf = bf16;
-  NetBuilder nb(mc, B, bn_mode == PHX_BN_LOCAL);
+  NetBuilder nb(mc, B, batch_bn());
   nb.build();
   E.prog = nb.program();
   Program& P = E.prog;
@@ -494,7 +499,7 @@ Exec& phx_ctx::exec_for(int B) {
   E.fused_bn.assign(P.ops.size(), 0);
   E.stat_P.assign(P.tensors.size(), 0);
   size_t sp_need = 1, sc_need = 1;
-  if (bn_mode == PHX_BN_LOCAL) {
+  if (batch_bn()) {
     for (size_t i = 1; i < P.ops.size(); ++i) {
       const Op& op = P.ops[i];
       const Op& pr = P.ops[i - 1];
@@ -513,7 +518,7 @@ Exec& phx_ctx::exec_for(int B) {
   }
   E.gfused_bn.assign(P.ops.size(), 0);
   E.gstat_P.assign(P.ops.size(), 0);
-  if (bn_mode == PHX_BN_LOCAL) {
+  if (batch_bn()) {
     for (size_t i = 0; i + 1 < P.ops.size(); ++i) {
       const Op& bn = P.ops[i];
       const Op& L = P.ops[i + 1];
@@ -536,7 +541,12 @@ Exec& phx_ctx::exec_for(int B) {
       sp_need = std::max(sp_need, (size_t)np * tz.c);
     }
   }
-  plan_groups(E, bn_mode == PHX_BN_LOCAL);
+  plan_groups(E, batch_bn());
+  if (bn_mode == PHX_BN_SYNC) {
+    int cmax = 1;
+    for (const Tensor& t : P.tensors) cmax = std::max(cmax, t.c);
+    E.sync_sums = E.alloc<double>((size_t)kMaxSeg * cmax * 3);
+  }
   E.fuse_folded.assign(P.ops.size(), 0);
   {
     static const bool fold = [] {
@@ -822,6 +832,21 @@ void plan_groups(Exec& E, bool local_bn) {
   }
 }
 
+// bn=sync: the BN sums of `segs` (fold -> the caller's all-reduce -> statistics from the global sums)
+// bn=sync: all-reduce the sums of `n` members already in E.sync_sums, then their statistics
+void sync_reduce_apply(phx_ctx* ctx, Exec& E, const BnFinSeg* segs, int n, int C, bool bwd, hipStream_t s) {
+  if (!ctx->ar_fn) throw std::logic_error("bn=sync: no collective registered (phx_set_allreduce)");
+  if (ctx->ar_fn(ctx->ar_user, E.sync_sums, (size_t)n * C * 3, s) != 0)
+    throw std::runtime_error("bn=sync: the all-reduce callback failed");
+  launch_bn_from_sums(segs, n, C, bwd, E.sync_sums, kBnEps, s);
+}
+
+void sync_finalize(phx_ctx* ctx, Exec& E, const BnFinSeg* segs, int n, int C, bool bwd, hipStream_t s) {
+  if (!ctx->ar_fn) throw std::logic_error("bn=sync: no collective registered (phx_set_allreduce)");
+  launch_bn_fold_sums(segs, n, C, bwd, E.sync_sums, s);
+  sync_reduce_apply(ctx, E, segs, n, C, bwd, s);
+}
+
 void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream_t s, bool frozen) {
   const Program& P = E.prog;
   const std::vector<int>& g = E.groups[gid];
@@ -899,7 +924,8 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            E.slot_b[op.slot], W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar,
                            nullptr, nullptr};
       }
-      launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
+      if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, false, s);
+      else launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
       break;
     }
     default:
@@ -986,7 +1012,8 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            (long)P.tensors[op.in[0]].rows(), nullptr, nullptr, nullptr, nullptr, nullptr,
                            nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
       }
-      launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
+      if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, true, s);
+      else launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
       break;
     }
     default:
@@ -1087,11 +1114,22 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         if (frozen)
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
                                  E.slot_c[op.slot], ti.c, kBnEps, s);
-        else if (E.fused_bn[i])
+        else if (E.fused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
+          const BnFinSeg sg{E.spart + E.stat_region[op.in[0]] * E.sp_region,
+                            E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]], (long)ti.rows(),
+                            mean, rstd, W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, nullptr, nullptr};
+          sync_finalize(ctx, E, &sg, 1, ti.c, false, s);
+        } else if (E.fused_bn[i])
           launch_bn_finalize(E.spart + E.stat_region[op.in[0]] * E.sp_region,
                              E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]],
                              (long)ti.rows(), ti.c, mean, rstd,
                              W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
+        else if (ctx->bn_mode == PHX_BN_SYNC) {
+          launch_bn_stats_sums(x, (long)ti.rows(), ti.c, E.red, E.sync_sums, s, E.tbf(op.in[0]) != 0);
+          const BnFinSeg sg{nullptr, nullptr, 0, (long)ti.rows(), mean, rstd, W + op.gamma, E.slot_c[op.slot],
+                            W + op.mmean, W + op.mvar, nullptr, nullptr};
+          sync_reduce_apply(ctx, E, &sg, 1, ti.c, false, s);
+        }
         else
           launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.gamma,
                           E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s, E.tbf(op.in[0]) != 0);
@@ -1226,10 +1264,22 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       case OP_BN:
         // reduction only; the apply half runs in the producer's dgrad (gview)
         if (op.acc[0]) throw std::runtime_error("BN input with several consumers");
-        if (!frozen && E.gfused_bn[i])
+        if (!frozen && E.gfused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
+          const BnFinSeg sg{E.spart + E.gstat_region[i] * E.sp_region, nullptr, E.gstat_P[i], (long)ti.rows(),
+                            nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
+          sync_finalize(ctx, E, &sg, 1, ti.c, true, s);
+        } else if (!frozen && E.gfused_bn[i])
           launch_bn_bwd_finalize(E.spart + E.gstat_region[i] * E.sp_region, E.gstat_P[i], (long)ti.rows(),
                                  ti.c, E.slot_d[op.slot],
                                  E.slot_e[op.slot], s);
+        else if (!frozen && ctx->bn_mode == PHX_BN_SYNC) {
+          launch_bn_bwd_reduce_sums(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot], W + op.gamma,
+                                    W + op.beta, (long)ti.rows(), ti.c, op.act, E.red, E.sync_sums, s,
+                                    E.tbf(op.in[0]) != 0);
+          const BnFinSeg sg{nullptr, nullptr, 0, (long)ti.rows(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                            E.slot_d[op.slot], E.slot_e[op.slot]};
+          sync_reduce_apply(ctx, E, &sg, 1, ti.c, true, s);
+        }
         else if (!frozen)
           launch_bn_bwd_reduce(dy, E.tptr(op.in[0], input), E.slot_a[op.slot], E.slot_b[op.slot],
                                W + op.gamma, W + op.beta, (long)ti.rows(), ti.c, op.act, E.red,
@@ -1403,7 +1453,8 @@ int phx_create(const phx_config* cfg, int device, phx_ctx** out) {
       return PHX_EINVAL;
     }
     if (cfg->image_size < 0 || cfg->max_batch < 0) throw std::invalid_argument("negative image_size / max_batch");
-    if (cfg->bn_mode != PHX_BN_LOCAL && cfg->bn_mode != PHX_BN_FROZEN) throw std::invalid_argument("unknown bn_mode");
+    if (cfg->bn_mode != PHX_BN_LOCAL && cfg->bn_mode != PHX_BN_FROZEN && cfg->bn_mode != PHX_BN_SYNC)
+      throw std::invalid_argument("unknown bn_mode");
     if (!(cfg->score_thresh >= 0.f && cfg->score_thresh <= 1.f)) throw std::invalid_argument("score_thresh outside [0, 1]");
     if (cfg->image_size > 0) ctx->mc.image_size = cfg->image_size;
     ctx->device = device;
@@ -1440,6 +1491,13 @@ int phx_create(const phx_config* cfg, int device, phx_ctx** out) {
     return PHX_EINVAL;
   }
   *out = ctx.release();
+  return PHX_OK;
+}
+
+int phx_set_allreduce(phx_ctx* ctx, phx_allreduce_fn fn, void* user) {
+  if (!ctx) return PHX_EINVAL;
+  ctx->ar_fn = fn;
+  ctx->ar_user = user;
   return PHX_OK;
 }
 

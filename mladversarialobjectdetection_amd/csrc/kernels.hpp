@@ -131,6 +131,16 @@ struct BnFinSeg {
   float *mdz, *mdzx;  // backward
 };
 void launch_bn_finalize_group(const BnFinSeg* segs, int n, int C, float eps, hipStream_t s);
+// bn=sync halves of a finalize: fold each member's partials into sums[i][C][3] = (rows, S1, S2) in
+// fp64 (forward: sum x, sum x^2; backward: sum dz, sum dz*xhat), then — after the caller's
+// all-reduce of the sums — the statistics / backward means from the global sums
+void launch_bn_fold_sums(const BnFinSeg* segs, int n, int C, bool bwd, double* sums, hipStream_t s);
+void launch_bn_from_sums(const BnFinSeg* segs, int n, int C, bool bwd, const double* sums, float eps,
+                         hipStream_t s);
+void launch_bn_stats_sums(const float* y, long M, int C, double* part, double* sums, hipStream_t s, bool ybf);
+void launch_bn_bwd_reduce_sums(const float* da, const float* y, const float* mean, const float* rstd,
+                               const float* gamma, const float* beta, long M, int C, int act, double* part,
+                               double* sums, hipStream_t s, bool ybf);
 void launch_bn_bwd_finalize_group(const BnFinSeg* segs, int n, int C, hipStream_t s);
 // frozen BN: mean/rstd from moving statistics
 void launch_bn_frozen_stats(const float* mmean, const float* mvar, float* mean, float* rstd,

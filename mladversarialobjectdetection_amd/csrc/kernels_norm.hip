@@ -594,6 +594,76 @@ void launch_bn_bwd_finalize_group(const BnFinSeg* segs, int n, int C, hipStream_
   PHX_LAUNCH_CHECK();
 }
 
+// bn=sync: the finalize's fold with an epilogue that keeps the fp64 sums (and the rows they cover)
+struct SumsEpi {
+  double* out;  // [C][3]
+  double rows;
+  const float* y = nullptr;  // StatsAcc's shift row (its sums are of x - y[c]): unshifted here
+  int ybf = 0;
+  __device__ void operator()(int, int c, double s0, double s1) const {
+    if (y) {
+      const double r = ybf ? (double)ald1<true>(y, c) : (double)y[c];
+      s1 += 2.0 * r * s0 + rows * r * r;
+      s0 += rows * r;
+    }
+    out[(long)c * 3 + 0] = rows;
+    out[(long)c * 3 + 1] = s0;
+    out[(long)c * 3 + 2] = s1;
+  }
+};
+
+// bn=sync halves of the unfused reductions: the sums of one BN (forward sum x, sum x^2 over its
+// input y; backward sum dz, sum dz*xhat) into sums[C][3], for the caller's all-reduce
+void launch_bn_stats_sums(const float* y, long M, int C, double* part, double* sums, hipStream_t s, bool ybf) {
+  const SumsEpi e{sums, (double)M, y, ybf ? 1 : 0};
+  if (ybf) colred(StatsAcc<true>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
+  else colred(StatsAcc<false>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
+}
+
+void launch_bn_fold_sums(const BnFinSeg* segs, int n, int C, bool bwd, double* sums, hipStream_t s) {
+  if (n < 1 || n > kMaxSeg) throw std::runtime_error("bn fold: bad member count");
+  FinGroup<SumsEpi, kMaxSeg> g{};
+  for (int i = 0; i < n; ++i)
+    g.s[i] = FinSeg<SumsEpi>{segs[i].part, segs[i].cnt, segs[i].P, SumsEpi{sums + (size_t)i * C * 3, (double)segs[i].M}};
+  if (bwd) hipLaunchKernelGGL((k_bn_finalize<true, SumsEpi, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
+  else hipLaunchKernelGGL((k_bn_finalize<false, SumsEpi, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
+  PHX_LAUNCH_CHECK();
+}
+
+// one lane per (channel, member): StatsEpi / BwdEpi2 over the all-reduced sums (global row count)
+template <bool BWD>
+__global__ __launch_bounds__(256) void k_bn_from_sums(FinGroup<StatsEpi, kMaxSeg> fg, FinGroup<BwdEpi2, kMaxSeg> bg,
+                                                      const double* __restrict__ sums, int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x, i = blockIdx.y;
+  if (c >= C) return;
+  const double* q = sums + ((size_t)i * C + c) * 3;
+  const double rows = q[0];
+  if constexpr (BWD) {
+    BwdEpi2 e = pick_seg(bg.s, i).e;
+    e.M = (long)rows;
+    e(0, c, q[1], q[2]);
+  } else {
+    StatsEpi e = pick_seg(fg.s, i).e;
+    e.M = (long)rows;
+    e(0, c, q[1], q[2]);
+  }
+}
+
+void launch_bn_from_sums(const BnFinSeg* segs, int n, int C, bool bwd, const double* sums, float eps,
+                         hipStream_t s) {
+  if (n < 1 || n > kMaxSeg) throw std::runtime_error("bn from sums: bad member count");
+  FinGroup<StatsEpi, kMaxSeg> fg{};
+  FinGroup<BwdEpi2, kMaxSeg> bg{};
+  for (int i = 0; i < n; ++i) {
+    const BnFinSeg& d = segs[i];
+    if (bwd) bg.s[i].e = BwdEpi2{0, d.mdz, d.mdzx};
+    else fg.s[i].e = StatsEpi{nullptr, 0, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps};
+  }
+  if (bwd) hipLaunchKernelGGL(k_bn_from_sums<true>, dim3(cdiv(C, 256), n), dim3(256), 0, s, fg, bg, sums, C);
+  else hipLaunchKernelGGL(k_bn_from_sums<false>, dim3(cdiv(C, 256), n), dim3(256), 0, s, fg, bg, sums, C);
+  PHX_LAUNCH_CHECK();
+}
+
 template <bool BF>
 __global__ __launch_bounds__(256) void k_gx_materialize(GradX g, float4* __restrict__ out, long n4,
                                                         int C) {
@@ -616,6 +686,14 @@ void launch_bn_bwd_reduce(const float* da, const float* y, const float* mean, co
                           double* part, float* mdz, float* mdzx, hipStream_t s, bool ybf) {
   if (ybf) colred(BwdAcc<true>{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}}, BwdEpi2{M, mdz, mdzx}, M, C, 1, part, s);
   else colred(BwdAcc<false>{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}}, BwdEpi2{M, mdz, mdzx}, M, C, 1, part, s);
+}
+
+void launch_bn_bwd_reduce_sums(const float* da, const float* y, const float* mean, const float* rstd,
+                               const float* gamma, const float* beta, long M, int C, int act, double* part,
+                               double* sums, hipStream_t s, bool ybf) {
+  const SumsEpi e{sums, (double)M};
+  if (ybf) colred(BwdAcc<true>{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}}, e, M, C, 1, part, s);
+  else colred(BwdAcc<false>{da, y, mean, rstd, gamma, beta, C, act, {}, {}, {}, {}}, e, M, C, 1, part, s);
 }
 
 void launch_bn_bwd(const float* da, const float* y, const float* mean, const float* rstd,

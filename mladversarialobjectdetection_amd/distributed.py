@@ -11,6 +11,7 @@ shard), and reading the metrics issues no further collective.  The defender redu
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 import torch
@@ -39,6 +40,37 @@ def allreduce_sum_(t: torch.Tensor) -> torch.Tensor:
     if is_dist():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
+
+
+class _CudaBuf:
+    """A device buffer of the library seen as a torch tensor (__cuda_array_interface__)."""
+
+    def __init__(self, ptr: int, n: int):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": "<f8", "data": (ptr, False), "version": 2,
+                                         "strides": None}
+
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
+def bn_sync_callback():
+    """The phx_allreduce_fn of bn=sync: SUM all-reduce of the library's fp64 BN sums over the process
+    group, issued on the library's stream (the caller's current stream; RCCL orders the collective on
+    it, gloo reduces through the host and returns when done).  A no-op at world size 1.  Errors are
+    reported to the library as a non-zero return (the step then fails with a message)."""
+
+    def fn(user, ptr, n, stream):
+        try:
+            if is_dist():
+                t = torch.as_tensor(_CudaBuf(int(ptr), int(n)), device="cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            return 0
+        except Exception as e:  # noqa: BLE001 — surfaced through the library's return code
+            import sys
+            print(f"bn=sync all-reduce failed: {e!r}", file=sys.stderr)
+            return 1
+
+    return ALLREDUCE_FN(fn)
 
 
 def init_from_env(backend: str | None = None):

@@ -257,10 +257,13 @@ def print_patch(patch_u8):
 
 
 def create(img_shape, bbox, scale):
-    """AdversarialPatch._create (adv_patch.py:60-91): (ymin, xmin, patch_h, patch_w).  numpy's own
-    promotion applies: float32 boxes (the detector's dtype) take h, w in float32, the rest in float64."""
+    """AdversarialPatch._create (adv_patch.py:60-91): (ymin, xmin, patch_h, patch_w).  The reference's
+    numpy 1.22 promotion: float32 boxes (the detector's dtype) take h, w in float32 (array-scalar
+    subtraction), every product / sum with a Python float is float64 (numpy >= 2 would keep float32
+    there, so the float64 steps are written out)."""
     ymin, xmin, ymax, xmax = bbox
     h, w = ymax - ymin, xmax - xmin
+    ymin, xmin, h, w = float(ymin), float(xmin), float(h), float(w)
     long_side = max(h, w)
     pw = int(long_side * scale)
     ph = pw
