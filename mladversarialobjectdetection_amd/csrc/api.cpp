@@ -128,6 +128,16 @@ struct Exec {
   float* dscale_scratch = nullptr;  // dL/dscale of a gradient-free (eval) step
   double* sync_sums = nullptr;      // bn=sync: [member][C][3] per-channel sums to all-reduce
 
+  int tag = 0;        // 0: the step's executor; 1: the concurrent first pass's (forward only)
+  // deferred moving statistics (a step whose first pass runs beside the second): while defer_mov
+  // the BN finalizes leave the moving statistics alone and write (batch mean, variance) of their
+  // slot to side + 2 * side_off[slot]; launch_bn_moving_apply then applies both passes in order
+  bool defer_mov = false;
+  double* side = nullptr;
+  std::vector<int> side_off;
+  MovEntry* mov_tab = nullptr;
+  int n_mov = 0, mov_cmax = 1;
+  double* side_for(int slot) const { return defer_mov ? side + 2 * (size_t)side_off[slot] : nullptr; }
   bool bf16 = false;  // the context's compute dtype (GEMM plans depend on it)
   // activations (the arena tensors) stored as bf16: PHX_DTYPE_BF16, SURVEY.md 8a R4 "C4: bf16 act";
   // the program input (the images) and every gradient stay fp32
@@ -236,8 +246,16 @@ struct phx_ctx {
       if (p.first == off) return reinterpret_cast<const float*>(d_wt.get()) + p.second;
     throw std::runtime_error("no transposed kernel for weight offset");
   }
-  Exec& exec_for(int B);
+  Exec& exec_for(int B, int tag = 0);
   std::string model_info() const;
+  // concurrent first pass (injected placement): its own stream and fork / join events
+  hipStream_t s1 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  ~phx_ctx() {
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    if (s1) (void)hipStreamDestroy(s1);
+  }
 };
 
 namespace {
@@ -432,12 +450,12 @@ bool is_cls_out(const Program& P, int t);
 // kMaxExecs stay alive: a new batch size evicts the least recently used one (after the device
 // has drained, so no queued kernel still reads its memory), which bounds the workspace of a
 // driver that mixes batch sizes (last partial batch, validation) to two executors.
-constexpr size_t kMaxExecs = 2;
+constexpr size_t kMaxExecs = 3;
 
-Exec& phx_ctx::exec_for(int B) {
+Exec& phx_ctx::exec_for(int B, int tag) {
   ++clock;
   for (auto& e : execs)
-    if (e->B == B) {
+    if (e->B == B && e->tag == tag) {
       e->used = clock;
       return *e;
     }
@@ -452,6 +470,7 @@ Exec& phx_ctx::exec_for(int B) {
   auto ex = std::make_unique<Exec>();
   Exec& E = *ex;
   E.B = B;
+  E.tag = tag;
   E.bf16 = bf16;
   E.abf = bf16;
   NetBuilder nb(mc, B, batch_bn());
@@ -493,6 +512,23 @@ Exec& phx_ctx::exec_for(int B) {
       red_need = std::max(red_need, colred_scratch_doubles((long)ti.h * ti.w, ti.c, B));
       E.se_of_tensor[op.out] = (int)i;
     }
+  }
+  {
+    std::vector<MovEntry> tab;
+    int off = 0;
+    E.side_off.assign(P.n_slots, 0);
+    for (const Op& op : P.ops)
+      if (op.t == OP_BN) {
+        const int C = P.tensors[op.in[0]].c;
+        E.side_off[op.slot] = off;
+        tab.push_back(MovEntry{op.mmean, op.mvar, C, off});
+        off += C;
+        E.mov_cmax = std::max(E.mov_cmax, C);
+      }
+    E.side = E.alloc<double>(2 * (size_t)std::max(off, 1));
+    E.n_mov = (int)tab.size();
+    E.mov_tab = E.alloc<MovEntry>(std::max<size_t>(tab.size(), 1));
+    if (!tab.empty()) PHX_HIP(hipMemcpy(E.mov_tab, tab.data(), sizeof(MovEntry) * tab.size(), hipMemcpyHostToDevice));
   }
   // fused statistics: a BN whose input is produced by the op right before it (stem, 1x1 conv,
   // depthwise conv) gets its batch statistics from that producer's epilogue
@@ -922,7 +958,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
         segs[r] = BnFinSeg{E.spart + (size_t)reg * E.sp_region, E.scnt + (size_t)reg * E.sc_region,
                            E.stat_P[op.in[0]], (long)P.tensors[op.in[0]].rows(), E.slot_a[op.slot],
                            E.slot_b[op.slot], W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar,
-                           nullptr, nullptr};
+                           nullptr, nullptr, E.side_for(op.slot)};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, false, s);
       else launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
@@ -1117,22 +1153,25 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         else if (E.fused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
           const BnFinSeg sg{E.spart + E.stat_region[op.in[0]] * E.sp_region,
                             E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]], (long)ti.rows(),
-                            mean, rstd, W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, nullptr, nullptr};
+                            mean, rstd, W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, nullptr, nullptr,
+                            E.side_for(op.slot)};
           sync_finalize(ctx, E, &sg, 1, ti.c, false, s);
         } else if (E.fused_bn[i])
           launch_bn_finalize(E.spart + E.stat_region[op.in[0]] * E.sp_region,
                              E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]],
                              (long)ti.rows(), ti.c, mean, rstd,
-                             W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s);
+                             W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s,
+                             E.side_for(op.slot));
         else if (ctx->bn_mode == PHX_BN_SYNC) {
           launch_bn_stats_sums(x, (long)ti.rows(), ti.c, E.red, E.sync_sums, s, E.tbf(op.in[0]) != 0);
           const BnFinSeg sg{nullptr, nullptr, 0, (long)ti.rows(), mean, rstd, W + op.gamma, E.slot_c[op.slot],
-                            W + op.mmean, W + op.mvar, nullptr, nullptr};
+                            W + op.mmean, W + op.mvar, nullptr, nullptr, E.side_for(op.slot)};
           sync_reduce_apply(ctx, E, &sg, 1, ti.c, false, s);
         }
         else
           launch_bn_stats(x, (long)ti.rows(), ti.c, E.red, mean, rstd, W + op.gamma,
-                          E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s, E.tbf(op.in[0]) != 0);
+                          E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s, E.tbf(op.in[0]) != 0,
+                          E.side_for(op.slot));
         (void)y;
         break;
       }
@@ -1545,7 +1584,10 @@ int phx_workspace_bytes(phx_ctx* ctx, int B, size_t* bytes) {
   if (B > ctx->max_batch) return fail(ctx, PHX_ECAP, "batch exceeds max_batch");
   PHX_TRY(ctx)
   PHX_HIP(hipSetDevice(ctx->device));
-  *bytes = ctx->exec_for(B).bytes;
+  size_t tot = ctx->exec_for(B).bytes;
+  for (const auto& e : ctx->execs)  // + the concurrent first pass's executor, once a step made it
+    if (e->B == B && e->tag != 0) tot += e->bytes;
+  *bytes = tot;
   return PHX_OK;
   PHX_CATCH(ctx)
 }
@@ -1819,6 +1861,13 @@ int phx_patch_images(phx_ctx* ctx, const float* images, int B, const float* boxe
   PHX_CATCH(ctx)
 }
 
+// the concurrent first pass of phx_step_grad (on unless PHX_CONC=0; read per call so a test can
+// compare both orders in one process)
+static bool concurrent_first_pass() {
+  const char* e = std::getenv("PHX_CONC");
+  return !(e && e[0] == '0');
+}
+
 int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
                   const int32_t* count, int maxb, const float* params, int64_t step, int gimg0,
                   int add_tv, float* grad, float* metrics, void* stream) {
@@ -1829,14 +1878,51 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   Exec& E = ctx->exec_for(B);
   ctx->last = &E;
   PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
-  // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
-  run_forward(ctx, E, images, s, 0, step, gimg0);
-  run_pre_nms(ctx, E, s, 2);
-  // (a second HIP stream for the NMS passes that only feed the ASR metric was measured: any
-  // multi-stream use slows the whole step by ~0.8 ms on this runtime, so everything stays on `s`)
-  run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
-  launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
   const bool inject = boxes != nullptr;
+  // Injected placement: the first pass only feeds the ASR denominator (and the moving statistics),
+  // so it runs on a second stream beside the second pass and the backward, on its own executor
+  // (its own activation arena).  Both passes defer their moving-statistics updates, applied in
+  // pass order after the join, so every result equals the one-stream order bit for bit.  Not with
+  // bn=sync: every rank must issue its collectives in one order.  PHX_CONC=0 turns it off.
+  Exec* E1p = nullptr;
+  // (a profiled step runs on one stream: its per-launch-group events time each kernel alone)
+  if (inject && concurrent_first_pass() && ctx->bn_mode == PHX_BN_LOCAL && !ctx->prof.on) {
+    if (!ctx->s1) {
+      PHX_HIP(hipStreamCreateWithFlags(&ctx->s1, hipStreamNonBlocking));
+      PHX_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+      PHX_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    }
+    E1p = &ctx->exec_for(B, 1);
+    ctx->last = &E;
+  }
+  const bool fork = E1p != nullptr;
+  // (an error part-way leaves neither executor deferring)
+  struct DeferReset {
+    Exec *a, *b;
+    ~DeferReset() {
+      a->defer_mov = false;
+      if (b) b->defer_mov = false;
+    }
+  } defer_reset{&E, E1p};
+  if (fork) {
+    Exec& E1 = *E1p;
+    hipStream_t s1 = ctx->s1;
+    E1.defer_mov = E.defer_mov = true;
+    PHX_HIP(hipEventRecord(ctx->ev_fork, s));
+    PHX_HIP(hipStreamWaitEvent(s1, ctx->ev_fork, 0));
+    run_forward(ctx, E1, images, s1, 0, step, gimg0);
+    E1.defer_mov = false;
+    run_pre_nms(ctx, E1, s1, 2);
+    run_nms(ctx, E1, 2, E1.nms1_boxes, E1.nms1_scores, E1.nms1_count, s1);
+    launch_count_ge(E1.nms1_scores, E1.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s1);
+    PHX_HIP(hipEventRecord(ctx->ev_join, s1));
+  } else {
+    // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
+    run_forward(ctx, E, images, s, 0, step, gimg0);
+    run_pre_nms(ctx, E, s, 2);
+    run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
+    launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
+  }
   if (inject) {
     if (!count) throw std::invalid_argument("boxes without count");
     stage_boxes(E, boxes, count, B, maxb, s);  // injected placement boxes
@@ -1847,6 +1933,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_count(E.ed, E.place, metrics, s);
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);
+  E.defer_mov = false;
   run_pre_nms(ctx, E, s, 1);
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, grad + PHX_NPATCH, metrics, s);
@@ -1864,6 +1951,10 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.rstore, E.dmatched, s);
   launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
+  if (fork) {
+    PHX_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+    launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), E1p->side, E.side, s);
+  }
   return PHX_OK;
   PHX_CATCH(ctx)
 }

@@ -112,13 +112,15 @@ void launch_transpose(const float* in, float* out, int rows, int cols, hipStream
 // Per-channel batch statistics of y [M,C]: writes mean/rstd (float) and updates moving stats
 // (momentum 0.99, util_keras.py:33-35) when mmean != nullptr.  part: scratch (doubles).
 size_t bn_stats_scratch_doubles(long M, int C);
+// side != nullptr: the moving statistics are not touched; (mean, Bessel-corrected variance) go to
+// side[2c], side[2c+1] in fp64 for launch_bn_moving_apply (a step whose two passes run concurrently)
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
                      const float* gamma, float* sc, float* mmean, float* mvar, float eps,
-                     hipStream_t s, bool ybf = false);
+                     hipStream_t s, bool ybf = false, double* side = nullptr);
 // training-mode BN statistics from the P producer partials of a StatSink (k_bn_finalize)
 void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
                         float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
-                        float eps, hipStream_t s);
+                        float eps, hipStream_t s, double* side = nullptr);
 // grouped finalize (one launch for the per-level BNs of a head conv, each its own partials)
 struct BnFinSeg {
   const float2* part;
@@ -129,7 +131,17 @@ struct BnFinSeg {
   const float* gamma;
   float *sc, *mmean, *mvar;
   float *mdz, *mdzx;  // backward
+  double* side = nullptr;  // forward: deferred moving statistics (see launch_bn_stats)
 };
+// The moving-statistics updates of two passes, in pass order (m <- m - (m - batch) * 0.01 twice,
+// each rounded to float as the in-finalize update does): for every entry, channels c < C of
+// W[mm + c] / W[mv + c] from side0 / side1 + off (fp64 (mean, var) pairs)
+struct MovEntry {
+  long mm, mv;
+  int C, off;
+};
+void launch_bn_moving_apply(const MovEntry* tab, int n, int cmax, float* W, const double* side0,
+                            const double* side1, hipStream_t s);
 void launch_bn_finalize_group(const BnFinSeg* segs, int n, int C, float eps, hipStream_t s);
 // bn=sync halves of a finalize: fold each member's partials into sums[i][C][3] = (rows, S1, S2) in
 // fp64 (forward: sum x, sum x^2; backward: sum dz, sum dz*xhat), then — after the caller's

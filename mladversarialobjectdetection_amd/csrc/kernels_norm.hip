@@ -305,6 +305,9 @@ struct StatsAcc {
   }
 };
 
+// one moving-average step, m - (m - batch) * (1 - momentum) in fp64 rounded to float
+__device__ __forceinline__ float moving_update(float m, double batch) { return (float)(m - (m - batch) * 0.01); }
+
 struct StatsEpi {
   const float* y;  // for the shift (row 0)
   long M;
@@ -316,6 +319,7 @@ struct StatsEpi {
   float* mvar;
   float eps;
   int ybf = 0;  // y in bf16 storage
+  double* side = nullptr;  // deferred moving statistics: (mean, uvar) pairs, moving stats untouched
   __device__ void operator()(int, int c, double s0, double s1) const {
     const double ref = !y ? 0.0 : ybf ? (double)ald1<true>(y, c) : (double)y[c];
     const double dm = s0 / (double)M;            // mean - ref
@@ -326,20 +330,41 @@ struct StatsEpi {
     const double rs = 1.0 / sqrt(var + (double)eps);
     rstd[c] = (float)rs;
     sc[c] = (float)(rs * (double)gamma[c]);
-    if (mmean) {
-      // Keras: moving -= (moving - batch) * (1 - momentum); the fused op reports the
-      // Bessel-corrected variance for the moving average [TF-recall].
-      double uvar = M > 1 ? var * (double)M / (double)(M - 1) : var;
-      mmean[c] = (float)(mmean[c] - (mmean[c] - mu) * 0.01);
-      mvar[c] = (float)(mvar[c] - (mvar[c] - uvar) * 0.01);
+    // Keras: moving -= (moving - batch) * (1 - momentum); the fused op reports the
+    // Bessel-corrected variance for the moving average [TF-recall].
+    const double uvar = M > 1 ? var * (double)M / (double)(M - 1) : var;
+    if (side) {
+      side[2 * c] = mu;
+      side[2 * c + 1] = uvar;
+    } else if (mmean) {
+      mmean[c] = moving_update(mmean[c], mu);
+      mvar[c] = moving_update(mvar[c], uvar);
     }
   }
 };
 
+__global__ __launch_bounds__(256) void k_bn_moving_apply(const MovEntry* __restrict__ tab, float* __restrict__ W,
+                                                         const double* __restrict__ s0,
+                                                         const double* __restrict__ s1) {
+  const MovEntry e = tab[blockIdx.x];
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= e.C) return;
+  const long o = 2L * (e.off + c);
+  W[e.mm + c] = moving_update(moving_update(W[e.mm + c], s0[o]), s1[o]);
+  W[e.mv + c] = moving_update(moving_update(W[e.mv + c], s0[o + 1]), s1[o + 1]);
+}
+
+void launch_bn_moving_apply(const MovEntry* tab, int n, int cmax, float* W, const double* side0,
+                            const double* side1, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_bn_moving_apply, dim3(n, cdiv(cmax, 256)), dim3(256), 0, s, tab, W, side0, side1);
+  PHX_LAUNCH_CHECK();
+}
+
 void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, float* rstd,
                      const float* gamma, float* sc, float* mmean, float* mvar, float eps,
-                     hipStream_t s, bool ybf) {
-  StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps, ybf ? 1 : 0};
+                     hipStream_t s, bool ybf, double* side) {
+  StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps, ybf ? 1 : 0, side};
   if (ybf) colred(StatsAcc<true>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
   else colred(StatsAcc<false>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
 }
@@ -411,10 +436,10 @@ __global__ __launch_bounds__(256) void k_bn_finalize(FinGroup<E, NS> grp) {
 
 void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
                         float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
-                        float eps, hipStream_t s) {
+                        float eps, hipStream_t s, double* side) {
   // StatsEpi's shift is 0 here: S1, S2 are plain sums of x and x^2 in fp64
   FinGroup<StatsEpi, 1> g{};
-  g.s[0] = FinSeg<StatsEpi>{part, cnt, P, StatsEpi{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps}};
+  g.s[0] = FinSeg<StatsEpi>{part, cnt, P, StatsEpi{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps, 0, side}};
   hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi, 1>), dim3(C), dim3(256), 0, s, g);
   PHX_LAUNCH_CHECK();
 }
@@ -425,7 +450,7 @@ void launch_bn_finalize_group(const BnFinSeg* segs, int n, int C, float eps, hip
   for (int i = 0; i < n; ++i) {
     const BnFinSeg& d = segs[i];
     g.s[i] = FinSeg<StatsEpi>{d.part, d.cnt, d.P,
-                              StatsEpi{nullptr, d.M, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps}};
+                              StatsEpi{nullptr, d.M, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps, 0, d.side}};
   }
   hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
   PHX_LAUNCH_CHECK();
@@ -657,7 +682,7 @@ void launch_bn_from_sums(const BnFinSeg* segs, int n, int C, bool bwd, const dou
   for (int i = 0; i < n; ++i) {
     const BnFinSeg& d = segs[i];
     if (bwd) bg.s[i].e = BwdEpi2{0, d.mdz, d.mdzx};
-    else fg.s[i].e = StatsEpi{nullptr, 0, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps};
+    else fg.s[i].e = StatsEpi{nullptr, 0, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps, 0, d.side};
   }
   if (bwd) hipLaunchKernelGGL(k_bn_from_sums<true>, dim3(cdiv(C, 256), n), dim3(256), 0, s, fg, bg, sums, C);
   else hipLaunchKernelGGL(k_bn_from_sums<false>, dim3(cdiv(C, 256), n), dim3(256), 0, s, fg, bg, sums, C);
