@@ -1885,13 +1885,13 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   // pass order after the join, so every result equals the one-stream order bit for bit.  Not with
   // bn=sync: every rank must issue its collectives in one order.  PHX_CONC=0 turns it off.
   Exec* E1p = nullptr;
+  if (concurrent_first_pass() && ctx->bn_mode != PHX_BN_SYNC && !ctx->s1) {
+    PHX_HIP(hipStreamCreateWithFlags(&ctx->s1, hipStreamNonBlocking));
+    PHX_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    PHX_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+  }
   // (a profiled step runs on one stream: its per-launch-group events time each kernel alone)
   if (inject && concurrent_first_pass() && ctx->bn_mode == PHX_BN_LOCAL && !ctx->prof.on) {
-    if (!ctx->s1) {
-      PHX_HIP(hipStreamCreateWithFlags(&ctx->s1, hipStreamNonBlocking));
-      PHX_HIP(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
-      PHX_HIP(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
-    }
     E1p = &ctx->exec_for(B, 1);
     ctx->last = &E;
   }
@@ -1935,13 +1935,25 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);
   E.defer_mov = false;
   run_pre_nms(ctx, E, s, 1);
+  // 5. ASR metric: soft-NMS over second-pass person boxes (attacker.py:203-205).  It reads the
+  // pre_nms outputs only (the backward reads them too, nothing writes them until the next step),
+  // so it runs on the side stream beside the backward and joins at the end of the step
+  const bool side_nms = ctx->s1 != nullptr && concurrent_first_pass() && ctx->bn_mode != PHX_BN_SYNC && !ctx->prof.on;
+  if (side_nms) {
+    PHX_HIP(hipEventRecord(ctx->ev_fork, s));
+    PHX_HIP(hipStreamWaitEvent(ctx->s1, ctx->ev_fork, 0));
+    run_nms(ctx, E, 1, E.nms2_boxes, E.nms2_scores, E.nms2_count, ctx->s1);
+    launch_count_ge(E.nms2_scores, E.nms2_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_NUM, ctx->s1);
+    PHX_HIP(hipEventRecord(ctx->ev_join, ctx->s1));
+  }
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, grad + PHX_NPATCH, metrics, s);
   // 4. victim data-gradient -> d(patched images)
   run_backward(ctx, E, E.patched, s);
-  // 5. ASR metric: soft-NMS over second-pass person boxes (attacker.py:203-205)
-  run_nms(ctx, E, 1, E.nms2_boxes, E.nms2_scores, E.nms2_count, s);
-  launch_count_ge(E.nms2_scores, E.nms2_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_NUM, s);
+  if (!side_nms) {
+    run_nms(ctx, E, 1, E.nms2_boxes, E.nms2_scores, E.nms2_count, s);
+    launch_count_ge(E.nms2_scores, E.nms2_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_NUM, s);
+  }
   // 6. EOT backward -> d patch (+ TV)
   EotDims d = E.ed;
   d.B = B;
@@ -1951,10 +1963,8 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.rstore, E.dmatched, s);
   launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
-  if (fork) {
-    PHX_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
-    launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), E1p->side, E.side, s);
-  }
+  if (fork || side_nms) PHX_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
+  if (fork) launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), E1p->side, E.side, s);
   return PHX_OK;
   PHX_CATCH(ctx)
 }

@@ -3,7 +3,8 @@ pass only feeds the ASR denominator and the moving statistics, so the library ru
 stream beside the second pass and the backward (its own executor), deferring both passes'
 moving-statistics updates and applying them in pass order after the join.  The result must equal
 the one-stream order (PHX_CONC=0) bit for bit: gradient, parameters after Adam, the metric row and
-the moving statistics after two steps — with and without drop connect (D1 draws per-pass masks)."""
+the moving statistics after two steps — with and without drop connect (D1 draws per-pass masks).
+The second pass's soft-NMS (ASR numerator) also runs on the side stream, in both placement flows."""
 import os
 
 import numpy as np
@@ -21,7 +22,7 @@ def _case(B, S):
     return imgs, boxes
 
 
-def _run(conc, model, B, S, person_bias=0.0):
+def _run(conc, model, B, S, person_bias=0.0, inject=True):
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker
     old = os.environ.get("PHX_CONC")
     os.environ["PHX_CONC"] = "1" if conc else "0"
@@ -33,7 +34,7 @@ def _run(conc, model, B, S, person_bias=0.0):
         x = torch.as_tensor(imgs).cuda()
         rows = []
         for _ in range(2):
-            att.train_step(x, boxes=boxes)
+            att.train_step(x, boxes=boxes if inject else None)
             torch.cuda.synchronize()
             rows.append(att.metrics_buf.cpu().numpy().copy())
         return (att.grad.cpu().numpy().copy(), att.params.cpu().numpy().copy(), np.stack(rows),
@@ -58,3 +59,14 @@ def test_concurrent_first_pass_equals_one_stream(model, S, B, pb):
     assert ws2 > ws1  # the first pass's own executor
     if pb:
         assert m2[:, _lib.M_ASR_DEN].min() > 0  # the first pass's metric (run on the side stream) is live
+
+
+def test_side_stream_soft_nms_with_first_pass_placement():
+    """boxes=None (the reference's flow): the first pass feeds the placement, so it stays on the
+    step's stream; only the second pass's soft-NMS (the ASR numerator) runs beside the backward."""
+    from mladversarialobjectdetection_amd import _lib
+    g1, p1, m1, w1, _ = _run(False, "efficientdet-d0", 4, 256, 4.0, inject=False)
+    g2, p2, m2, w2, _ = _run(True, "efficientdet-d0", 4, 256, 4.0, inject=False)
+    assert np.array_equal(g1, g2) and np.array_equal(p1, p2) and np.array_equal(w1, w2)
+    assert np.array_equal(m1, m2)
+    assert m2[:, _lib.M_NBOX].min() > 0 and m2[:, _lib.M_ASR_NUM].max() > 0
