@@ -12,6 +12,7 @@
 #include <memory>
 #include <sstream>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "common.hpp"
@@ -248,6 +249,10 @@ struct phx_ctx {
   }
   Exec& exec_for(int B, int tag = 0);
   std::string model_info() const;
+  // issued by run_forward once it has issued op fwd_hook_at (the second pass starts the concurrent
+  // first pass part-way through its own forward, §12 of DESIGN.md)
+  std::function<void()> fwd_hook;
+  size_t fwd_hook_at = 0;
   // concurrent first pass (injected placement): its own stream and fork / join events
   hipStream_t s1 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -1079,6 +1084,11 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
   if (E.ndrop && train)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   for (size_t i = 0; i < P.ops.size(); ++i) {
+    if (ctx->fwd_hook && i == ctx->fwd_hook_at) {
+      auto h = std::move(ctx->fwd_hook);
+      ctx->fwd_hook = nullptr;
+      h();
+    }
     if (E.grp_of[i] >= 0) {
       if (E.groups[E.grp_of[i]].front() == (int)i) run_group_fwd(ctx, E, E.grp_of[i], input, s, frozen);
       continue;
@@ -1898,16 +1908,27 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   const bool fork = E1p != nullptr;
   // (an error part-way leaves neither executor deferring)
   struct DeferReset {
+    phx_ctx* c;
     Exec *a, *b;
     ~DeferReset() {
+      c->fwd_hook = nullptr;  // never left armed (it refers to this call's frame)
       a->defer_mov = false;
       if (b) b->defer_mov = false;
     }
-  } defer_reset{&E, E1p};
-  if (fork) {
+  } defer_reset{ctx, &E, E1p};
+  // Where the side stream starts: when the second pass's forward reaches the backbone's stage 6
+  // (the first op at 1/32 of the image side), so the first pass's HBM-bound early layers run beside
+  // the second pass's latency-bound deep layers, BiFPN and heads rather than beside its own early
+  // layers (C2 12.06 -> 11.89 ms).  PHX_FORK_FRAC: 0 = at the step start, 0 < f < 1 = after that
+  // fraction of the ops (experiments).
+  static const double fork_frac = [] {
+    const char* e = std::getenv("PHX_FORK_FRAC");
+    return e ? atof(e) : -1.0;
+  }();
+  auto side = [&]() {
     Exec& E1 = *E1p;
     hipStream_t s1 = ctx->s1;
-    E1.defer_mov = E.defer_mov = true;
+    E1.defer_mov = true;
     PHX_HIP(hipEventRecord(ctx->ev_fork, s));
     PHX_HIP(hipStreamWaitEvent(s1, ctx->ev_fork, 0));
     run_forward(ctx, E1, images, s1, 0, step, gimg0);
@@ -1916,6 +1937,25 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
     run_nms(ctx, E1, 2, E1.nms1_boxes, E1.nms1_scores, E1.nms1_count, s1);
     launch_count_ge(E1.nms1_scores, E1.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s1);
     PHX_HIP(hipEventRecord(ctx->ev_join, s1));
+  };
+  if (fork) {
+    E.defer_mov = true;
+    if (fork_frac == 0.0) {
+      side();
+    } else {
+      ctx->fwd_hook = side;
+      if (fork_frac > 0.0) {
+        ctx->fwd_hook_at = (size_t)(fork_frac * (double)E.prog.ops.size());
+      } else {
+        // the first op at 1/32 of the image side (the backbone's stage 6)
+        ctx->fwd_hook_at = E.prog.ops.size();
+        for (size_t i = 0; i < E.prog.ops.size(); ++i)
+          if (E.prog.tensors[E.prog.ops[i].out].h * 32 <= ctx->mc.image_size) {
+            ctx->fwd_hook_at = i;
+            break;
+          }
+      }
+    }
   } else {
     // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
     run_forward(ctx, E, images, s, 0, step, gimg0);
@@ -1933,6 +1973,11 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_count(E.ed, E.place, metrics, s);
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);
+  if (ctx->fwd_hook) {
+    auto h = std::move(ctx->fwd_hook);
+    ctx->fwd_hook = nullptr;
+    h();
+  }
   E.defer_mov = false;
   run_pre_nms(ctx, E, s, 1);
   // 5. ASR metric: soft-NMS over second-pass person boxes (attacker.py:203-205).  It reads the

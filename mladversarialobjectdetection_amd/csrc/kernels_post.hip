@@ -700,7 +700,11 @@ void launch_loss(const float* mraw, int B, const float* params, float* dm, float
 // ------------------------------------------------------------------------------------------
 // sparse class-head backward: for every kept anchor whose score equals the image max, route
 // dL/dm through sigmoid and the class reduce_max (ties split, TF _MaxGrad) into the input of
-// the class-predict pointwise conv: dx[pixel, :] += W[:, k*ncls + c] * dlogit
+// the class-predict pointwise conv: dx[pixel, :] += W[:, k*ncls + c] * dlogit.
+// One lane per (image, pixel): it walks the pixel's anchors and their tied classes in a fixed
+// order and accumulates into its own dx row, so several contributions to one pixel (tied scores
+// of its anchors: frequent with bf16 logits) always add in the same order.  (Float atomics here
+// made the sum depend on the workgroup schedule, e.g. on work running on another stream.)
 // ------------------------------------------------------------------------------------------
 template <bool BF>
 __global__ __launch_bounds__(256) void k_cls_scatter(
@@ -709,33 +713,37 @@ __global__ __launch_bounds__(256) void k_cls_scatter(
     const float* __restrict__ cls_base, const LevelDesc* __restrict__ lev, int nlev, int A, int B,
     int nclass, int na, const float* __restrict__ wpred /*[K][na*ncls]*/, int K,
     float* __restrict__ dx_base, const long* __restrict__ dx_off) {
-  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (long)B * A) return;
-  const int b = (int)(idx / A), a = (int)(idx % A);
-  if (!(keep[idx] & 1)) return;
-  const float mx = mraw[b];
-  if (scores[idx] != mx || dm[b] == 0.0f) return;
-  const float ds = dm[b] / (float)nties[b];
-  const float s = scores[idx];
-  const float dl = ds * s * (1.0f - s);  // SigmoidGrad: y * (1 - y) * dy
+  const int PT = A / na;  // pixels per image over all levels
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * PT) return;
+  const int b = (int)(idx / PT), p = (int)(idx % PT);
+  if (dm[b] == 0.0f) return;
   int l = 0;
-  while (l + 1 < nlev && a >= lev[l + 1].anchor0) ++l;
+  while (l + 1 < nlev && p * na >= lev[l + 1].anchor0) ++l;
   const LevelDesc L = lev[l];
-  const int local = a - L.anchor0;
-  const int pix = local / na, k = local % na;
+  const int pix = p - L.anchor0 / na;
+  const float mx = mraw[b];
+  const float ds = dm[b] / (float)nties[b];
   const long prow = (long)b * L.h * L.w + pix;
-  const long lg = L.cls_off + prow * (na * nclass) + (long)k * nclass;  // element offset (BF: bf16)
-  float m = ald1<BF>(cls_base, lg);
-  for (int c = 1; c < nclass; ++c) m = fmaxf(m, ald1<BF>(cls_base, lg + c));
-  int nt = 0;
-  for (int c = 0; c < nclass; ++c) nt += (ald1<BF>(cls_base, lg + c) == m);
-  const float dlc = dl / (float)nt;
   float* dx = dx_base + dx_off[l] + prow * K;
   const int N = na * nclass;
-  for (int c = 0; c < nclass; ++c) {
-    if (ald1<BF>(cls_base, lg + c) != m) continue;
-    const int col = k * nclass + c;
-    for (int j = 0; j < K; ++j) atomicAdd(dx + j, wpred[(long)j * N + col] * dlc);
+  for (int k = 0; k < na; ++k) {
+    const long aidx = (long)b * A + L.anchor0 + (long)pix * na + k;
+    if (!(keep[aidx] & 1)) continue;
+    const float s = scores[aidx];
+    if (s != mx) continue;
+    const float dl = ds * s * (1.0f - s);  // SigmoidGrad: y * (1 - y) * dy
+    const long lg = L.cls_off + prow * (na * nclass) + (long)k * nclass;  // element offset (BF: bf16)
+    float m = ald1<BF>(cls_base, lg);
+    for (int c = 1; c < nclass; ++c) m = fmaxf(m, ald1<BF>(cls_base, lg + c));
+    int nt = 0;
+    for (int c = 0; c < nclass; ++c) nt += (ald1<BF>(cls_base, lg + c) == m);
+    const float dlc = dl / (float)nt;
+    for (int c = 0; c < nclass; ++c) {
+      if (ald1<BF>(cls_base, lg + c) != m) continue;
+      const int col = k * nclass + c;
+      for (int j = 0; j < K; ++j) dx[j] += wpred[(long)j * N + col] * dlc;
+    }
   }
 }
 
@@ -744,7 +752,8 @@ void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* m
                         const LevelDesc* lev, int nlev, int A, int B, int nclass, int na,
                         const float* wpred, int K, float* dx_base, const long* dx_off,
                         hipStream_t s, bool bf) {
-  long n = (long)B * A;
+  if (A % na) throw std::runtime_error("cls_scatter: anchors not a multiple of anchors per pixel");
+  const long n = (long)B * (A / na);
   if (bf)
     hipLaunchKernelGGL(k_cls_scatter<true>, dim3(cdiv(n, 256)), dim3(256), 0, s, scores, keep, mraw, nties,
                        dm, cls_base, lev, nlev, A, B, nclass, na, wpred, K, dx_base, dx_off);
