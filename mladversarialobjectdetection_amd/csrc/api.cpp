@@ -418,6 +418,7 @@ struct Scope {
   size_t idx;
   hipStream_t s;
   std::string dbg;
+  ExtTiming ext;  // GEMM groups: timed by the kernels' own dispatch timestamps (PHX_TLAUNCH)
   Scope(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t st, const std::string& tag = "")
       : p(ctx->prof.on ? &ctx->prof : nullptr), s(st) {
     if (debug_sync()) {
@@ -428,12 +429,19 @@ struct Scope {
     // GEMMs of a bf16 context run on the bf16 matrix cores; everything else at the fp32 rate
     const double peak = (ctx->bf16 && std::string(kind) == "gemm") ? 2500.0 : 157.3;
     Prof::Rec r{std::string(kind) + (prof_detail() ? tag : std::string()), p->ev(), p->ev(), flops, bytes, peak};
-    PHX_HIP(hipEventRecord(r.a, s));
+    PHX_HIP(hipEventRecord(r.a, s));  // (re-recorded by the group's first timed kernel)
     p->recs.push_back(r);
     idx = p->recs.size() - 1;
+    if (std::string(kind) == "gemm") {
+      ext = ExtTiming{r.a, r.b, false};
+      ext_timing() = &ext;
+    }
   }
   ~Scope() noexcept(false) {
-    if (p) (void)hipEventRecord(p->recs[idx].b, s);
+    if (p) {
+      if (ext_timing() == &ext) ext_timing() = nullptr;
+      if (!ext.used) (void)hipEventRecord(p->recs[idx].b, s);
+    }
     if (!dbg.empty() && std::uncaught_exceptions() == 0) {
       const hipError_t e = hipStreamSynchronize(s);
       if (e != hipSuccess) throw HipError(std::string("device error after ") + dbg + ": " + hipGetErrorString(e));
@@ -1420,6 +1428,11 @@ void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc
 }
 
 }  // namespace
+
+phx::ExtTiming*& phx::ext_timing() {
+  static ExtTiming* t = nullptr;
+  return t;
+}
 
 phx::ProfScope phx::prof_begin(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t s) {
   ProfScope r{nullptr, 0, s};

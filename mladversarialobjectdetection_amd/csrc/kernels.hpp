@@ -2,6 +2,7 @@
 // given stream and never allocate.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstddef>
 #include <cstdint>
@@ -9,6 +10,27 @@
 #include "common.hpp"
 
 namespace phx {
+
+// Launch-group timing by the kernels' own dispatch timestamps (the library profiler's GEMM
+// groups, so the live roofline times kernels as rocprofv3 does, without the gaps two
+// hipEventRecord packets add): while ext_timing() is set, a kernel launched through PHX_TLAUNCH
+// records its start event (the group's first kernel) and its stop event (every kernel; the last
+// one counts).
+struct ExtTiming {
+  hipEvent_t a = nullptr, b = nullptr;
+  bool used = false;
+};
+ExtTiming*& ext_timing();
+#define PHX_TLAUNCH(K, G, BL, SHM, S, ...)                                                              \
+  do {                                                                                                 \
+    if (::phx::ExtTiming* t_ = ::phx::ext_timing()) {                                                  \
+      hipExtLaunchKernelGGL(K, G, BL, SHM, S, t_->used ? nullptr : t_->a, t_->b, 0, __VA_ARGS__);      \
+      t_->used = true;                                                                                 \
+    } else {                                                                                           \
+      hipLaunchKernelGGL(K, G, BL, SHM, S, __VA_ARGS__);                                               \
+    }                                                                                                  \
+  } while (0)
+
 
 // ---- convolutions (kernels_conv.hip) ------------------------------------------------------
 // 3x3 stride-2 stem, Cin = 3: x [B,H,W,3] -> y [B,Ho,Wo,Co]; w [3,3,3,Co] (HWIO)

@@ -772,7 +772,7 @@ struct GemmCall {
 template <int WM, int MODE, int SK>
 static void gemm_dispatch_nt(int nt, dim3 g, hipStream_t s, const GemmCall& a, int st) {
 #define PHX_G(NT_, ST_)                                                                                \
-    hipLaunchKernelGGL((k_gemm<NT_, WM, MODE, SK, ST_>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias,   \
+    PHX_TLAUNCH((k_gemm<NT_, WM, MODE, SK, ST_>), g, dim3(256), 0, s, a.A, a.G, a.Bt, a.bias,   \
                        a.C, a.M, a.N, a.K, a.accf, a.rs, a.rpi, a.kslice, a.part, a.sink, a.gsk);
   if (st) {
     constexpr bool fwd = MODE == 1 || MODE == 2 || SK == 1, dgrad = MODE == 3 || SK == 2;
@@ -901,20 +901,20 @@ int gemm_splitk_finish(const float* partial, int splits, int M, int N, const flo
     const int rb = splitk_stats_rb(M, N);
     sink.P = cdiv(M, rb);
     if (cbf)
-      hipLaunchKernelGGL(k_gemm_splitk_reduce_stats<true>, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
+      PHX_TLAUNCH(k_gemm_splitk_reduce_stats<true>, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
                          M, N, rb, bias, C, sink);
     else
-      hipLaunchKernelGGL(k_gemm_splitk_reduce_stats<false>, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
+      PHX_TLAUNCH(k_gemm_splitk_reduce_stats<false>, dim3(cdiv(M, rb)), dim3(256), 0, s, partial, splits,
                          M, N, rb, bias, C, sink);
     PHX_LAUNCH_CHECK();
     return sink.P;
   }
   long mn = (long)M * N;
   if (cbf)
-    hipLaunchKernelGGL(k_gemm_splitk_reduce<true>, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
+    PHX_TLAUNCH(k_gemm_splitk_reduce<true>, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
                        bias, C, acc ? 1 : 0);
   else
-    hipLaunchKernelGGL(k_gemm_splitk_reduce<false>, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
+    PHX_TLAUNCH(k_gemm_splitk_reduce<false>, dim3(cdiv(mn, 256)), dim3(256), 0, s, partial, splits, mn, N,
                        bias, C, acc ? 1 : 0);
   PHX_LAUNCH_CHECK();
   return 0;

@@ -629,20 +629,20 @@ template <int WM, int TM, int TN, int MODE, int SK, int NS>
 static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st) {
   if (!bf) {
     if (st) throw std::logic_error("gemm2: bf16 storage needs the bf16 compute type");
-    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, false, 0>), g, dim3(256), 0, s, a);
+    PHX_TLAUNCH((k_gemm2<WM, TM, TN, MODE, SK, NS, false, 0>), g, dim3(256), 0, s, a);
     return;
   }
   constexpr bool fwd_only = MODE == 1 || MODE == 2 || SK == 1;
   constexpr bool dgrad_only = MODE == 3 || SK == 2;
   if constexpr (fwd_only) {
     if (st != 1) throw std::logic_error("gemm2: bf16 forward without bf16 activations");
-    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), 0, s, a);
+    PHX_TLAUNCH((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), 0, s, a);
   } else if constexpr (dgrad_only) {
     if (st != 2) throw std::logic_error("gemm2: bf16 gradient view without bf16 activations");
-    hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 2>), g, dim3(256), 0, s, a);
+    PHX_TLAUNCH((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 2>), g, dim3(256), 0, s, a);
   } else {  // raw A: a forward activation (ST 1) or a plain gradient (ST 0)
-    if (st == 1) hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), 0, s, a);
-    else if (st == 0) hipLaunchKernelGGL((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 0>), g, dim3(256), 0, s, a);
+    if (st == 1) PHX_TLAUNCH((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), 0, s, a);
+    else if (st == 0) PHX_TLAUNCH((k_gemm2<WM, TM, TN, MODE, SK, NS, true, 0>), g, dim3(256), 0, s, a);
     else throw std::logic_error("gemm2: raw dgrad with a bf16 y");
   }
 }
