@@ -1239,14 +1239,24 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
   // 1. sparse class-head gradient into the inputs of the class-predict pointwise convs
   int K = 0;
   long wpred = -1;
+  std::vector<std::pair<char*, size_t>> zero;  // the levels' gradient buffers, merged where adjacent
   for (int l = 0; l < (int)P.cls_out.size(); ++l) {
     for (const Op& op : P.ops) {
       if (op.out != P.cls_out[l]) continue;
       const Tensor& ti = P.tensors[op.in[0]];
-      PHX_HIP(hipMemsetAsync(E.gptr(op.in[0]), 0, ti.numel() * sizeof(float), s));
+      zero.emplace_back(reinterpret_cast<char*>(E.gptr(op.in[0])), ti.numel() * sizeof(float));
       K = ti.c;
       wpred = op.w;
     }
+  }
+  std::sort(zero.begin(), zero.end());
+  for (size_t i = 0; i < zero.size();) {
+    char* p0 = zero[i].first;
+    char* p1 = p0 + zero[i].second;
+    size_t j = i + 1;
+    for (; j < zero.size() && zero[j].first <= p1; ++j) p1 = std::max(p1, zero[j].first + zero[j].second);
+    PHX_HIP(hipMemsetAsync(p0, 0, (size_t)(p1 - p0), s));
+    i = j;
   }
   launch_cls_scatter(E.scores, E.keep, E.mraw, E.nties, E.dm, E.tptr(P.cls_out[0], input),
                      E.lev_dev, (int)E.lev.size(), ctx->A, E.B, ctx->mc.num_classes, na,

@@ -321,8 +321,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       } else {
         const float* As = reinterpret_cast<const float*>(g2_tile<P>(sm, buf, false, 0, 0));
         const float* Bs = As + BM * P::LD;
+        // k rows of this chunk that exist (a K of 24 or 40 leaves a last chunk of 8: its upper half
+        // is zero-filled and its MFMAs would add exact zeros)
+        const int kvalid = kend - (kbeg + kc * BK);
 #pragma unroll
         for (int s8 = 0; s8 < BK / 8; ++s8) {
+          if (s8 > 0 && 8 * s8 >= kvalid) break;  // wave-uniform
           float4 fa[TM], fb[TN];
 #pragma unroll
           for (int i = 0; i < TM; ++i)
