@@ -459,12 +459,23 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
         const float sim = tf_iou(cb, sbx);
         f1 = expf(scale * sim * sim);
       }
+      // sc = orig * f(newest) * f(next) * ... in that order.  TF stops at the first product
+      // <= thresh; every factor is in (0, 1], so the full product is <= thresh too and the outcome
+      // (removed: key 0, never selected) is the same — so the chain runs without the per-factor
+      // test, 16 factors at a time, padded with exact 1.0f: independent readlanes, then a
+      // dependent multiply chain with scalar operands.
       float sc = orig;
-      for (int k = 0; k < nf; ++k) {
-        const float f = __uint_as_float((uint32_t)__builtin_amdgcn_readlane(
-            (int)__float_as_uint(k < 64 ? f0 : f1), k & 63));
-        sc *= f;
-        if (sc <= score_thresh) break;
+      for (int k0 = 0; k0 < nf; k0 += 16) {
+        float fk[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = k0 + u;
+          const float v = k < 64 ? f0 : f1;  // k0 is wave-uniform: a uniform select
+          fk[u] = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(v), k & 63));
+          if (k >= nf) fk[u] = 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sc *= fk[u];
       }
       uint32_t nk;
       if (sc == orig) {
