@@ -21,7 +21,9 @@ bench.py's cpu_baseline import it).
 Keras semantics restated: Conv2D 'same' (3x3, stride 1: pad 1), Conv2DTranspose 3x3 stride 2
 'same' (TF pads the equivalent forward conv (0, 1): out[2i + k] += x[i] w[k], cropped to 2H),
 BatchNormalization training mode (batch statistics, eps 1e-3, moving statistics momentum 0.99 with
-the Bessel-corrected variance), leaky_relu alpha 0.2, MaxPooling2D 2x2 valid, Dropout 0.2
+the Bessel-corrected variance), leaky_relu alpha 0.2 [TF-recall: Keras 2.8 resolves the string
+Activation('leaky_relu') of generator.py:120,173,179 to tf.nn.leaky_relu, whose default alpha is
+0.2; no reference file pins the value], MaxPooling2D 2x2 valid, Dropout 0.2
 (x * 1.25 * [u >= 0.2]).  Random draws are the product's Philox streams (oracle/philox.py).
 """
 from __future__ import annotations
