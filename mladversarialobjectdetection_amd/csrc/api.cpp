@@ -1461,6 +1461,7 @@ void phx::prof_end(const ProfScope& r) {
 }
 
 int phx::ctx_image_size(const phx_ctx* ctx) { return ctx->mc.image_size; }
+bool phx::ctx_profiling(const phx_ctx* ctx) { return ctx->prof.on; }
 uint64_t phx::ctx_seed(const phx_ctx* ctx) { return ctx->seed; }
 int phx::ctx_device(const phx_ctx* ctx) { return ctx->device; }
 

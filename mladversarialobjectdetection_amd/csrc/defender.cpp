@@ -70,6 +70,15 @@ struct Lvl {
 
 struct phx_def {
   phx_ctx* victim = nullptr;
+  // backward: each 3x3 conv's weight gradient runs on a side stream beside its data gradient
+  // (independent given dy; disjoint scratch: wpart / cpart against col / gpart)
+  hipStream_t s1 = nullptr;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  ~phx_def() {
+    if (ev_a) (void)hipEventDestroy(ev_a);
+    if (ev_b) (void)hipEventDestroy(ev_b);
+    if (s1) (void)hipStreamDestroy(s1);
+  }
   int device = 0, max_batch = 0, S = 0;
   uint64_t seed = 0;
   std::string err;
@@ -468,17 +477,37 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   const long Mf = (long)B * S * S;
 
   // ---- backward ----
-  auto bias_grad = [&](const float* dy, long M, const UConv& c) { un_colsum(dy, M, c.co, G + c.b, cpart, s); };
+  // the side stream for weight gradients (PHX_DEF_CONC=1; never while profiling)
+  const bool side = std::getenv("PHX_DEF_CONC") && std::getenv("PHX_DEF_CONC")[0] == '1' && !ctx_profiling(victim);
+  if (side && !s1) {
+    PHX_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
+    PHX_HIP(hipEventCreateWithFlags(&ev_a, hipEventDisableTiming));
+    PHX_HIP(hipEventCreateWithFlags(&ev_b, hipEventDisableTiming));
+  }
+  hipStream_t sw = side ? s1 : s;  // where weight gradients run
+  auto fork = [&]() {
+    if (!side) return;
+    PHX_HIP(hipEventRecord(ev_a, s));
+    PHX_HIP(hipStreamWaitEvent(s1, ev_a, 0));
+  };
+  auto join = [&]() {
+    if (!side) return;
+    PHX_HIP(hipEventRecord(ev_b, s1));
+    PHX_HIP(hipStreamWaitEvent(s, ev_b, 0));
+  };
+  auto bias_grad = [&](const float* dy, long M, const UConv& c, hipStream_t st) {
+    un_colsum(dy, M, c.co, G + c.b, cpart, st);
+  };
   auto bn_bwd = [&](UBn& b, const float* da, const float* y, long M, int act, float* dy) {
     DScope g(victim, "unet_bn", 0.0, 12.0 * M * b.c, s);
     un_bn_bwd(da, y, M, b.c, b.mean, b.rstd, b.sc, W + b.beta, act, b.mdz, b.mdzx, G + b.gamma, G + b.beta, dy, cpart,
               s);
   };
-  auto conv3_wgrad = [&](const float* xin, int H, const UConv& c, const float* dy) {
+  auto conv3_wgrad = [&](const float* xin, int H, const UConv& c, const float* dy, hipStream_t st) {
     const long M = (long)B * H * H;
-    DScope g(victim, "unet_wgrad", 2.0 * M * c.co * 9 * c.ci, 4.0 * M * (c.co + c.ci), s);
-    un_wgrad(dy, c.co, xin, c.ci, 1, B, H, H, c.ci, M, c.co, c.kp_f, c.ci, 9, 0, wpart, G + c.w, s);
-    bias_grad(dy, M, c);
+    DScope g(victim, "unet_wgrad", 2.0 * M * c.co * 9 * c.ci, 4.0 * M * (c.co + c.ci), st);
+    un_wgrad(dy, c.co, xin, c.ci, 1, B, H, H, c.ci, M, c.co, c.kp_f, c.ci, 9, 0, wpart, G + c.w, st);
+    bias_grad(dy, M, c, st);
   };
   auto conv3_dgrad = [&](const float* dy, int H, const UConv& c, float* dx) {
     const long M = (long)B * H * H;
@@ -492,11 +521,15 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
                        float* da2, float* tmp, float* dx) {
     const long M = (long)B * H * H;
     bn_bwd(bns[k.b2], da2, y2, M, 1, tmp);
-    conv3_wgrad(a1, H, convs[k.c2], tmp);
+    fork();
+    conv3_wgrad(a1, H, convs[k.c2], tmp, sw);
     conv3_dgrad(tmp, H, convs[k.c2], da2);
+    join();  // tmp is rewritten next
     bn_bwd(bns[k.b1], da2, y1, M, 1, tmp);
-    conv3_wgrad(xin, H, convs[k.c1], tmp);
+    fork();
+    conv3_wgrad(xin, H, convs[k.c1], tmp, sw);
     if (dx) conv3_dgrad(tmp, H, convs[k.c1], dx);
+    join();
   };
   // output layer: dz [Mf,3]
   {
@@ -538,7 +571,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     {
       DScope g(victim, "unet_wgrad", 2.0 * M * n * n, 8.0 * M * n, s);
       un_wgrad(tmpT, n, d.up, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k1.w, s);
-      bias_grad(tmpT, M, k1);
+      bias_grad(tmpT, M, k1, s);
     }
     {
       DScope g(victim, "unet_gemm", 2.0 * M * n * n, 12.0 * M * n, s);
@@ -550,7 +583,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     {
       DScope g(victim, "unet_wgrad", 2.0 * M * n * n, 8.0 * M * n, s);
       un_wgrad(tmpT, n, skip, n, 0, 1, 1, 1, 1, M, n, n, n, 1, 4, wpart, G + k2.w, s);
-      bias_grad(tmpT, M, k2);
+      bias_grad(tmpT, M, k2, s);
     }
     {
       DScope g(victim, "unet_gemm", 2.0 * M * n * n, 12.0 * M * n, s);
@@ -559,10 +592,11 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     // transposed conv: input = the previous decoder's output (or the bottleneck's)
     const float* xin = i == 0 ? c4t.a2 : dt[i - 1].a2;
     const long Min = (long)B * hin * hin;
+    fork();
     {
-      DScope g(victim, "unet_wgrad", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
-      un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, s);
-      bias_grad(tmpX, M, up);
+      DScope g(victim, "unet_wgrad", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), sw);
+      un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, sw);
+      bias_grad(tmpX, M, up, sw);
     }
     {
       DScope g(victim, "unet_conv", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
@@ -571,6 +605,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
         gemm(col, bt + up.bt_d, nullptr, tmpY, Min, up.ci, up.kp_d, false, gpart, s);
       }
     }
+    join();  // tmpX is rewritten next
     std::swap(tmpX, tmpY);  // tmpX = gradient of the next (earlier) block's output
   }
   // bottleneck: tmpX = d c4 output

@@ -91,6 +91,7 @@ struct ProfScope {
 };
 ProfScope prof_begin(phx_ctx* ctx, const char* kind, double flops, double bytes, hipStream_t s);
 void prof_end(const ProfScope& r);
+bool ctx_profiling(const phx_ctx* ctx);  // phx_profile is on (launch groups timed one at a time)
 uint64_t ctx_seed(const phx_ctx* ctx);
 int ctx_device(const phx_ctx* ctx);
 
