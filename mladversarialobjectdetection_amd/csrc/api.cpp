@@ -491,7 +491,8 @@ Exec& phx_ctx::exec_for(int B, int tag) {
   E.prog = nb.program();
   Program& P = E.prog;
   E.act = E.alloc<float>(E.abf ? (P.act_floats + 1) / 2 : P.act_floats);
-  E.grad = E.alloc<float>(P.grad_floats);
+  // the concurrent first pass's executor (tag 1) runs forwards only: no gradient arena
+  E.grad = E.alloc<float>(tag == 1 ? 1 : P.grad_floats);
   // statistics slots and scratch
   E.slot_a.assign(P.n_slots, nullptr);
   E.slot_b.assign(P.n_slots, nullptr);
@@ -704,16 +705,18 @@ Exec& phx_ctx::exec_for(int B, int tag) {
   E.ymean = E.alloc<float>((size_t)B * 2);
   // the resized patches; reused by the resize adjoint's row buffer once the rotation backward
   // has consumed them
-  E.rstore = E.alloc<float>(std::max(E.ed.rcap, eot_resize_scratch_floats(E.ed)));
-  E.dstore = E.alloc<float>(E.ed.rcap);
+  // (the concurrent first pass's executor runs no EOT: its patch stores stay one element)
+  const bool eot = tag != 1;
+  E.rstore = E.alloc<float>(eot ? std::max(E.ed.rcap, eot_resize_scratch_floats(E.ed)) : 1);
+  E.dstore = E.alloc<float>(eot ? E.ed.rcap : 1);
   const size_t np = (size_t)PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3;
-  E.matched = E.alloc<float>(np * B);
-  E.dmatched = E.alloc<float>(np * B);
+  E.matched = E.alloc<float>(eot ? np * B : 1);
+  E.dmatched = E.alloc<float>(eot ? np * B : 1);
   E.dsum = E.alloc<double>((size_t)B * 64);
   E.tvs = E.alloc<double>(256);
   E.err = E.alloc<int>(1);
-  E.patched = E.alloc<float>((size_t)B * S * S * 3);
-  E.owner = E.alloc<int16_t>((size_t)B * S * S * 3);
+  E.patched = E.alloc<float>(eot ? (size_t)B * S * S * 3 : 1);
+  E.owner = E.alloc<int16_t>(eot ? (size_t)B * S * S * 3 : 1);
   {
     std::vector<int> blk;
     std::vector<float> pr;
