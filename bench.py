@@ -195,6 +195,33 @@ def main():
     images_per_s = world * B * args.steps / elapsed
 
     patches_headline = att.step_metrics()["patches"] if rank == 0 else 0
+
+    # the step's one collective timed alone (N>1): the same [d patch | d scale | metric row] payload,
+    # on a copy, between barriers, max over ranks — so a scaling curve separates the exchange from
+    # the per-rank compute
+    allreduce = None
+    if world > 1:
+        buf = att._red.clone()
+        n_ar = 20
+        ddp.allreduce_sum_(buf)  # warm the communicator
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        ta = time.perf_counter()
+        for _ in range(n_ar):
+            ddp.allreduce_sum_(buf)
+        torch.cuda.synchronize()
+        da = torch.tensor([time.perf_counter() - ta], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(da, op=torch.distributed.ReduceOp.MAX)
+        ar_ms = 1e3 * float(da.item()) / n_ar
+        nbytes = buf.numel() * buf.element_size()
+        allreduce = {"ms_per_call": round(ar_ms, 4), "bytes": nbytes, "calls_per_step": 1,
+                     "backend": str(torch.distributed.get_backend()),
+                     "algbw_GBps": round(nbytes / (ar_ms * 1e-3) / 1e9, 3),
+                     # ring all-reduce moves 2 (N-1)/N of the payload over each rank's links
+                     "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ar_ms * 1e-3) / 1e9, 3),
+                     "frac_of_step": round(ar_ms / (1e3 * elapsed / args.steps), 4)}
+        del buf
+
     roofline = None
     step_roof = None
     if not args.no_profile:
@@ -281,6 +308,7 @@ def main():
             "roofline": roofline,
             "step_roofline": step_roof,
             "cpu_baseline": cpu,
+            "allreduce": allreduce,
             "secondary": secondary,
         }
         print(json.dumps(line))

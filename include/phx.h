@@ -238,6 +238,11 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed);
 int phx_debug_last_patched(phx_ctx* ctx, float* out, void* stream);
 /* Last step's per-image max scores m_b [B] and loss-anchor index [B] (device->device). */
 int phx_debug_last_maxscores(phx_ctx* ctx, float* m, int32_t* anchor, void* stream);
+/* Last step's second-pass pre_nms outputs (postprocess.pre_nms, postprocess.py:119-156): per-anchor
+ * scores [B,A], classes [B,A] and decoded boxes [B,A,4] (ymin, xmin, ymax, xmax px) — the values
+ * the loss's person / validity masks read (attacker.py:118-141).  Any pointer may be NULL
+ * (device->device). */
+int phx_debug_last_detections(phx_ctx* ctx, float* scores, int32_t* classes, float* boxes, void* stream);
 /* Last step's d loss / d patched images [B,H,W,3] as the EOT backward reads it (the stem dgrad
  * writes it only at pixels a paste owns; elsewhere 0) (device->device). */
 int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream);

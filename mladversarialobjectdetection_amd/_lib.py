@@ -90,6 +90,7 @@ _SIGS = [
     ("phx_profile_report", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
     ("phx_debug_last_patched", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_maxscores", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("phx_debug_last_detections", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_image_grad", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_tap", c_int, [c_void_p, c_char_p, c_int, c_void_p, c_size_t, c_void_p]),
     # defender step

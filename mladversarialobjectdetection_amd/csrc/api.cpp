@@ -459,11 +459,14 @@ void plan_groups(Exec& E, bool local_bn);
 bool is_cls_out(const Program& P, int t);
 }  // namespace
 
-// One executor per batch size (the program and its arenas are shaped by B).  At most
-// kMaxExecs stay alive: a new batch size evicts the least recently used one (after the device
-// has drained, so no queued kernel still reads its memory), which bounds the workspace of a
-// driver that mixes batch sizes (last partial batch, validation) to two executors.
-constexpr size_t kMaxExecs = 3;
+// One executor per (batch size, tag) (the program and its arenas are shaped by B; tag 1 is the
+// concurrent first pass's forward-only executor, §12 of DESIGN.md).  At most kMaxExecs stay
+// alive, two per batch size for two batch sizes, so a driver that mixes batch sizes (a last
+// partial batch, validation) keeps both sizes' step and side executors without evicting at every
+// switch.  A third batch size evicts (after the device has drained, so no queued kernel still
+// reads its memory) a forward-only executor first — the smaller, cheaper one to rebuild — and
+// the least recently used among those.
+constexpr size_t kMaxExecs = 4;
 
 Exec& phx_ctx::exec_for(int B, int tag) {
   ++clock;
@@ -474,8 +477,12 @@ Exec& phx_ctx::exec_for(int B, int tag) {
     }
   if (execs.size() >= kMaxExecs) {
     size_t lru = 0;
+    auto older = [&](size_t i, size_t j) {
+      if (execs[i]->tag != execs[j]->tag) return execs[i]->tag > execs[j]->tag;
+      return execs[i]->used < execs[j]->used;
+    };
     for (size_t i = 1; i < execs.size(); ++i)
-      if (execs[i]->used < execs[lru]->used) lru = i;
+      if (older(i, lru)) lru = i;
     PHX_HIP(hipDeviceSynchronize());
     if (last == execs[lru].get()) last = nullptr;
     execs.erase(execs.begin() + (long)lru);
@@ -2181,6 +2188,20 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
     return PHX_OK;
   }
   throw std::invalid_argument(std::string("tap: no op named ") + op_name);
+  PHX_CATCH(ctx)
+}
+
+int phx_debug_last_detections(phx_ctx* ctx, float* scores, int32_t* classes, float* boxes, void* stream) {
+  if (!ctx || ctx->execs.empty()) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->last) throw std::logic_error("no step has run");
+  Exec& E = *ctx->last;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t n = (size_t)E.B * ctx->A;
+  if (scores) PHX_HIP(hipMemcpyAsync(scores, E.scores, n * 4, hipMemcpyDeviceToDevice, s));
+  if (classes) PHX_HIP(hipMemcpyAsync(classes, E.classes, n * 4, hipMemcpyDeviceToDevice, s));
+  if (boxes) PHX_HIP(hipMemcpyAsync(boxes, E.boxes, n * 16, hipMemcpyDeviceToDevice, s));
+  return PHX_OK;
   PHX_CATCH(ctx)
 }
 

@@ -215,7 +215,7 @@ struct phx_def {
     js << "]}";
     return js.str();
   }
-  // evaluation Masker (the attacker's 640^2 patch), allocated at the first evaluation
+  // evaluation Masker (the attacker's 640^2 patch), part of workspace(B)
   float *ematched = nullptr, *erstore = nullptr;
   int eB = 0;
 
@@ -350,6 +350,14 @@ void phx_def::workspace(int B) {
   count = alloc<int>(B);
   info = alloc<int>((size_t)B * 3);
   eerr = alloc<int>(1);
+  // evaluation Masker (the attacker's 640^2 patch): reserved here with the rest of the batch's
+  // workspace, so phx_def_workspace_bytes is the whole footprint before the first evaluation and a
+  // rebuild for another batch size never leaves them dangling.  Placement side <= floor(longer side
+  // * scale) <= S for scale in [0, 1] (the attacker's clip); soft-NMS may return 100 overlapping
+  // image-sized boxes, so the R store keeps the worst case.
+  ematched = F((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3);
+  erstore = F((size_t)B * PHX_MAX_OUT * S_ * S_ * 3);
+  eB = B;
 }
 
 // ---- U-Net forward (generator.py:17-101) + output layer and loss ----
@@ -637,13 +645,7 @@ void phx_def::eval(const float* images, int B, const float* boxes_in, const int*
   e2.P = PHX_PATCH_SIZE;
   // placement side <= floor(longer side * scale) <= S for scale in [0, 1] (the attacker's clip)
   e2.rcap = (long)B * PHX_MAX_OUT * S * S * 3;
-  if (eB != B) {
-    PHX_HIP(hipStreamSynchronize(s));
-    ematched = alloc<float>((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3);
-    erstore = alloc<float>(e2.rcap);
-    ws_bytes += ((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3 + e2.rcap) * 4;
-    eB = B;
-  }
+  if (eB != B || !ematched || !erstore) throw std::logic_error("defender evaluation buffers not reserved");
   prep_weights(W, s);
   const float* bx = boxes_in;
   const int* cn = count_in;

@@ -55,15 +55,21 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 
 def bn_sync_callback():
     """The phx_allreduce_fn of bn=sync: SUM all-reduce of the library's fp64 BN sums over the process
-    group, issued on the library's stream (the caller's current stream; RCCL orders the collective on
-    it, gloo reduces through the host and returns when done).  A no-op at world size 1.  Errors are
-    reported to the library as a non-zero return (the step then fails with a message)."""
+    group, issued on the library's stream `stream` (phx.h: the callback is ordered on it).  The
+    collective runs under that stream as torch's current stream, so RCCL orders it after the fold
+    kernel that wrote the sums and before the kernel that reads them, whatever stream the caller
+    made current; gloo reduces through the host and returns when done.  A no-op at world size 1.
+    Errors are reported to the library as a non-zero return (the step then fails with a message)."""
 
     def fn(user, ptr, n, stream):
         try:
             if is_dist():
                 t = torch.as_tensor(_CudaBuf(int(ptr), int(n)), device="cuda")
-                dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                if stream:
+                    with torch.cuda.stream(torch.cuda.ExternalStream(int(stream), device=t.device)):
+                        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+                else:
+                    dist.all_reduce(t, op=dist.ReduceOp.SUM)
             return 0
         except Exception as e:  # noqa: BLE001 — surfaced through the library's return code
             import sys

@@ -187,11 +187,15 @@ def test_bf16_d4_1024_four_images():
       * the step within SURVEY 8c's C4 tolerance (loss rel <= 1e-2, d patch cosine >= 0.99);
       * the detector anchor by anchor: |score difference| <= 3e-2 everywhere, median <= 3e-3,
         classes agree on >= 99 % of the anchors and every image's top person anchor is the same;
-      * the step's per-image max scores within 0.1.  They are maxima over the anchors that pass
-        filter_valid_boxes (attacker.py:69-89), and the decoded boxes come from bf16 box outputs: an
-        anchor whose box height or width is within bf16 precision of the image side is valid in one
-        build and not in the other (measured: every anchor's score within 0.017, one image's max
-        0.794 in fp32 against 0.745 in bf16 through such a flip).
+      * the step's per-image max scores within 3e-2, the per-anchor bound.  They are maxima over the
+        anchors that pass filter_valid_boxes (attacker.py:69-89: w/W <= 1, h/H <= 1, h*w > 100) on the
+        second pass's decoded boxes, and the box outputs are bf16 activations: an anchor whose decoded
+        side lies within bf16 precision of the image side (or whose area lies that close to 100) is
+        valid in one build and not in the other.  Such anchors are excluded explicitly — an anchor
+        is undecided when its fp32 height or width lies within one bf16 ulp of the image side plus
+        twice its own bf16-vs-fp32 deviation, and likewise for the area — and the maxima over the
+        remaining kept anchors of both builds are compared.  Each build's step maximum must be the maximum over its own
+        kept anchors (checked exactly), so the exclusion only ever removes undecided anchors.
     The fp64 oracle at this size would need ~100 GB of host memory, so the fp32 build (parity-tested
     against it at 256^2 in test_gpu_deep.py) is the reference here.  (D4's drop connect keys its
     draws by batch position, so a permuted batch is not expected to give permuted outputs; D0's
@@ -211,7 +215,14 @@ def test_bf16_d4_1024_four_images():
         g1 = att.grad.clone()
         met = att.metrics_buf.cpu().numpy().copy()
         m = torch.empty(B4, device="cuda")
-        v.ctx.call("phx_debug_last_maxscores", m.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        st = torch.cuda.current_stream().cuda_stream
+        v.ctx.call("phx_debug_last_maxscores", m.data_ptr(), None, st)
+        A = v.num_anchors
+        ds = torch.empty(B4, A, device="cuda")
+        dc = torch.empty(B4, A, dtype=torch.int32, device="cuda")
+        db_ = torch.empty(B4, A, 4, device="cuda")
+        v.ctx.call("phx_debug_last_detections", ds.data_ptr(), dc.data_ptr(), db_.data_ptr(), st)
+        second = (ds.cpu().numpy(), dc.cpu().numpy(), db_.cpu().numpy())
         _, s0, c0 = v.detect(imgs)
         if dt == "bf16":
             att.call(imgs, boxes=boxes)
@@ -221,10 +232,11 @@ def test_bf16_d4_1024_four_images():
             assert torch.equal(att.grad, g1)
             _, s1, c1 = v.detect(imgs)
             assert torch.equal(s0, s1) and torch.equal(c0, c1)
-        res[dt] = (g1.cpu().numpy().astype(np.float64), met, m.cpu().numpy(), s0.cpu().numpy(), c0.cpu().numpy())
+        res[dt] = (g1.cpu().numpy().astype(np.float64), met, m.cpu().numpy(), s0.cpu().numpy(), c0.cpu().numpy(),
+                   second)
         del att, v
         torch.cuda.empty_cache()
-    (gb, mb, sb, db, cb), (gf, mf, sf, df, cf) = res["bf16"], res["f32"]
+    (gb, mb, sb, db, cb, secb), (gf, mf, sf, df, cf, secf) = res["bf16"], res["f32"]
     print(f"loss bf16 {mb[_lib.M_LOSS]:.6f} f32 {mf[_lib.M_LOSS]:.6f}; max scores {sb} vs {sf}; "
           f"d patch cosine {_cos(gb[:-1], gf[:-1]):.6f}, rel {_rel(gb[:-1], gf[:-1]):.3e}")
     assert abs(mb[_lib.M_LOSS] - mf[_lib.M_LOSS]) <= 1e-2 * abs(mf[_lib.M_LOSS])
@@ -234,5 +246,32 @@ def test_bf16_d4_1024_four_images():
     assert np.mean(cb == cf) >= 0.99
     for b in range(B4):
         assert np.argmax(db[b] * (cb[b] == 0)) == np.argmax(df[b] * (cf[b] == 0)), b
-    assert np.abs(sb - sf).max() <= 0.1, (sb, sf)
+    # the step's per-image maxima over the kept anchors (person and valid), undecided anchors excluded
+    Sf = np.float32(1024)
+    (ssb, scb, sbb), (ssf, scf, sbf) = secb, secf
+
+    def sides(bx_):
+        return bx_[..., 2] - bx_[..., 0], bx_[..., 3] - bx_[..., 1]
+
+    def valid(bx_):
+        h, w = sides(bx_)
+        return (w / Sf <= 1) & (h / Sf <= 1) & (h * w > np.float32(100))
+
+    kb, kf = (scb == 0) & valid(sbb), (scf == 0) & valid(sbf)
+    for b in range(B4):  # each build's step maximum is the maximum over its own kept anchors
+        assert sb[b] == max(np.float32(0), ssb[b][kb[b]].max(initial=np.float32(0))), b
+        assert sf[b] == max(np.float32(0), ssf[b][kf[b]].max(initial=np.float32(0))), b
+    # undecided: the validity boundary lies within bf16 precision of the anchor's fp32 box — within
+    # one bf16 ulp of the image side (4 px; 1 % of the area bound) plus twice the anchor's own
+    # bf16-vs-fp32 deviation of that quantity
+    (hb, wb), (hf, wf) = sides(sbb), sides(sbf)
+    undecided = ((np.abs(hf - 1024.0) <= 4.0 + 2 * np.abs(hb - hf))
+                 | (np.abs(wf - 1024.0) <= 4.0 + 2 * np.abs(wb - wf))
+                 | (np.abs(hf * wf - 100.0) <= 1.0 + 2 * np.abs(hb * wb - hf * wf)))
+    agree = (valid(sbb) == valid(sbf)) | undecided
+    assert agree.all(), np.argwhere(~agree)[:5]  # validity differs only where it is undecided
+    for b in range(B4):
+        mb_ = ssb[b][kb[b] & ~undecided[b]].max(initial=np.float32(0))
+        mf_ = ssf[b][kf[b] & ~undecided[b]].max(initial=np.float32(0))
+        assert abs(float(mb_) - float(mf_)) <= 3e-2, (b, mb_, mf_)
     assert mb[_lib.M_NBOX] == mf[_lib.M_NBOX] and mb[_lib.M_NIMG] == B4
