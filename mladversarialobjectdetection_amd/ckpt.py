@@ -516,8 +516,8 @@ def checkpoint_to_blob(ckpt, manifest, ema_decay: float = 0.9998, skip_mismatch:
 def _object_graph_to_blob(reader, manifest) -> np.ndarray:
     """The object-graph branch of restore_ckpt (util_keras.py:131-152): every manifest variable whose
     full_name the object graph records gets its saved value (no EMA rule); the others keep 0 and
-    are listed in `.missing`; a restore that matches nothing raises (assert_nontrivial_match, whose
-    hub-checkpoint fallback, load_from_hub_checkpoint, is not built)."""
+    are listed in `.missing`; a restore that matches nothing (assert_nontrivial_match) falls back to
+    the hub-checkpoint loader, which fails on any missing key."""
     by_name = object_graph_keys(reader)
     shapes = reader.shape_map()
     n = max(p["offset"] + int(np.prod(p["shape"])) for p in manifest)
@@ -534,11 +534,65 @@ def _object_graph_to_blob(reader, manifest) -> np.ndarray:
         blob[p["offset"]:p["offset"] + val.size] = val.reshape(-1)
         matched += 1
     if not matched:
-        raise AssertionError(f"{reader.prefix}: the object graph matches no variable of the model "
-                             "(assert_nontrivial_match; the hub-checkpoint fallback is not built)")
+        # assert_nontrivial_match failed: restore_ckpt falls back to load_from_hub_checkpoint
+        # (util_keras.py:141-147)
+        return hub_checkpoint_to_blob(reader, manifest)
     out = blob.view(_Blob)
     out.missing = missing
     return out
+
+
+# util_keras.HUB_CPT_NAME (util_keras.py:24-26): variable-name prefix -> EfficientDetNetTrainHub
+# object, tried in this order ('' matches everything else)
+HUB_CPT_NAME = (("class_net/class-predict/", "classes"), ("box_net/box-predict/", "boxes"), ("", "base_model"))
+
+
+def hub_checkpoint_key(var_name: str) -> str:
+    """load_from_hub_checkpoint's _get_cpt_var_name (util_keras.py:86-96) for a Keras variable name
+    (with its ':0'): the prefix is replaced by the hub object's name, '/' becomes '.S' (the object
+    graph's escaping of a slash inside one path component), and ':0' is dropped except under
+    base_model, whose keys keep it."""
+    for prefix, hub in HUB_CPT_NAME:
+        if var_name.startswith(prefix):
+            key = hub + "/" + var_name[len(prefix):].replace("/", ".S")
+            if prefix:
+                key = key.replace(":0", "")
+            return key + "/.ATTRIBUTES/VARIABLE_VALUE"
+    raise AssertionError("unreachable: the '' prefix matches every name")
+
+
+def hub_checkpoint_to_blob(ckpt, manifest, verify: bool = True) -> np.ndarray:
+    """load_from_hub_checkpoint (util_keras.py:83-105): every variable of the model (model.weights:
+    the manifest, named '<name>:0') is assigned tf.train.load_variable(ckpt, hub key) — a missing key
+    or a mis-shaped value fails, as the reference's assign does."""
+    reader = ckpt if isinstance(ckpt, CheckpointReader) else CheckpointReader(ckpt, verify)
+    shapes = reader.shape_map()
+    n = max(p["offset"] + int(np.prod(p["shape"])) for p in manifest)
+    blob = np.zeros(n, np.float32)
+    for p in manifest:
+        key = hub_checkpoint_key(p["name"] + ":0")
+        if key not in shapes:
+            raise KeyError(f"Key {key} not found in checkpoint {reader.prefix} (load_from_hub_checkpoint)")
+        if tuple(shapes[key]) != tuple(p["shape"]):
+            raise ValueError(f"Shape mismatch: {key}, expected {tuple(p['shape'])}, but got {tuple(shapes[key])}")
+        val = reader.get_tensor(key)
+        blob[p["offset"]:p["offset"] + val.size] = val.reshape(-1)
+    out = blob.view(_Blob)
+    out.missing = []
+    return out
+
+
+def write_hub_checkpoint(prefix: str, manifest, blob: np.ndarray):
+    """An EfficientDetNetTrainHub-style object checkpoint of a weight blob: every variable under its
+    hub key (hub_checkpoint_key), with an object graph whose full names are the hub objects' own
+    (so it matches no EfficientDetNet variable, and restore_ckpt takes the hub fallback)."""
+    tensors, paths = {}, {}
+    for p in manifest:
+        v = np.asarray(blob[p["offset"]:p["offset"] + int(np.prod(p["shape"]))], np.float32).reshape(p["shape"])
+        path = hub_checkpoint_key(p["name"] + ":0")[: -len("/.ATTRIBUTES/VARIABLE_VALUE")]
+        tensors["hub/" + path] = v
+        paths["hub/" + path] = path
+    write_object_graph_checkpoint(prefix, tensors, paths)
 
 
 class _Blob(np.ndarray):

@@ -70,15 +70,6 @@ struct Lvl {
 
 struct phx_def {
   phx_ctx* victim = nullptr;
-  // backward: each 3x3 conv's weight gradient runs on a side stream beside its data gradient
-  // (independent given dy; disjoint scratch: wpart / cpart against col / gpart)
-  hipStream_t s1 = nullptr;
-  hipEvent_t ev_a = nullptr, ev_b = nullptr;
-  ~phx_def() {
-    if (ev_a) (void)hipEventDestroy(ev_a);
-    if (ev_b) (void)hipEventDestroy(ev_b);
-    if (s1) (void)hipStreamDestroy(s1);
-  }
   int device = 0, max_batch = 0, S = 0;
   uint64_t seed = 0;
   std::string err;
@@ -485,24 +476,6 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   const long Mf = (long)B * S * S;
 
   // ---- backward ----
-  // the side stream for weight gradients (PHX_DEF_CONC=1; never while profiling)
-  const bool side = std::getenv("PHX_DEF_CONC") && std::getenv("PHX_DEF_CONC")[0] == '1' && !ctx_profiling(victim);
-  if (side && !s1) {
-    PHX_HIP(hipStreamCreateWithFlags(&s1, hipStreamNonBlocking));
-    PHX_HIP(hipEventCreateWithFlags(&ev_a, hipEventDisableTiming));
-    PHX_HIP(hipEventCreateWithFlags(&ev_b, hipEventDisableTiming));
-  }
-  hipStream_t sw = side ? s1 : s;  // where weight gradients run
-  auto fork = [&]() {
-    if (!side) return;
-    PHX_HIP(hipEventRecord(ev_a, s));
-    PHX_HIP(hipStreamWaitEvent(s1, ev_a, 0));
-  };
-  auto join = [&]() {
-    if (!side) return;
-    PHX_HIP(hipEventRecord(ev_b, s1));
-    PHX_HIP(hipStreamWaitEvent(s, ev_b, 0));
-  };
   auto bias_grad = [&](const float* dy, long M, const UConv& c, hipStream_t st) {
     un_colsum(dy, M, c.co, G + c.b, cpart, st);
   };
@@ -529,15 +502,11 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
                        float* da2, float* tmp, float* dx) {
     const long M = (long)B * H * H;
     bn_bwd(bns[k.b2], da2, y2, M, 1, tmp);
-    fork();
-    conv3_wgrad(a1, H, convs[k.c2], tmp, sw);
+    conv3_wgrad(a1, H, convs[k.c2], tmp, s);
     conv3_dgrad(tmp, H, convs[k.c2], da2);
-    join();  // tmp is rewritten next
     bn_bwd(bns[k.b1], da2, y1, M, 1, tmp);
-    fork();
-    conv3_wgrad(xin, H, convs[k.c1], tmp, sw);
+    conv3_wgrad(xin, H, convs[k.c1], tmp, s);
     if (dx) conv3_dgrad(tmp, H, convs[k.c1], dx);
-    join();
   };
   // output layer: dz [Mf,3]
   {
@@ -600,11 +569,10 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     // transposed conv: input = the previous decoder's output (or the bottleneck's)
     const float* xin = i == 0 ? c4t.a2 : dt[i - 1].a2;
     const long Min = (long)B * hin * hin;
-    fork();
     {
-      DScope g(victim, "unet_wgrad", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), sw);
-      un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, sw);
-      bias_grad(tmpX, M, up, sw);
+      DScope g(victim, "unet_wgrad", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
+      un_wgrad(tmpX, n, xin, up.ci, 2, B, H, H, up.ci, M, n, up.kp_f, up.ci, 9, 2, wpart, G + up.w, s);
+      bias_grad(tmpX, M, up, s);
     }
     {
       DScope g(victim, "unet_conv", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
@@ -613,7 +581,6 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
         gemm(col, bt + up.bt_d, nullptr, tmpY, Min, up.ci, up.kp_d, false, gpart, s);
       }
     }
-    join();  // tmpX is rewritten next
     std::swap(tmpX, tmpY);  // tmpX = gradient of the next (earlier) block's output
   }
   // bottleneck: tmpX = d c4 output

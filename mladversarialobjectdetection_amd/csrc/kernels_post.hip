@@ -54,6 +54,8 @@ __device__ __forceinline__ void nms_cand_append(const NmsCand& c, int b, int A, 
 // lane t reduces anchor t's 90 classes (max, first argmax) and decodes its box.
 // ------------------------------------------------------------------------------------------
 constexpr int kPreTile = 128;
+constexpr int kPreMaxClass = 96;                                  // staging registers cover nclass <= 96
+constexpr int kPreU = (kPreTile * kPreMaxClass / 4 + 255) / 256;  // 16-B loads per lane per tile
 
 // BF: the class / box outputs are bf16 activations (PHX_DTYPE_BF16); widened to fp32 when staged
 template <bool BF>
@@ -82,16 +84,14 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     const long e0 = L.cls_off + run;
     const uint16_t* src = reinterpret_cast<const uint16_t*>(cls_base) + e0;
     if ((e0 & 3) == 0) {
+      // the whole tile in one round trip: every lane issues all of its 8-B loads before any LDS store
       const uint2* src4 = reinterpret_cast<const uint2*>(src);
-      int i = threadIdx.x;
-      for (; i + 768 < nf4; i += 1024) {
-        uint2 v[4];
+      uint2 v[kPreU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
+      for (int u = 0; u < kPreU; ++u) v[u] = src4[min((int)threadIdx.x + 256 * u, max(nf4 - 1, 0))];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = unpack_bf16x4(v[u]);
-      }
-      for (; i < nf4; i += blockDim.x) smem4[i] = unpack_bf16x4(src4[i]);
+      for (int u = 0; u < kPreU; ++u)
+        if ((int)threadIdx.x + 256 * u < nf4) smem4[threadIdx.x + 256 * u] = unpack_bf16x4(v[u]);
       for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = ald1<true>(cls_base, e0 + j);
     } else {
       for (int j = threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = ald1<true>(cls_base, e0 + j);
@@ -100,16 +100,14 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
   const float* src = cls_base + L.cls_off + run;
   const float4* src4 = reinterpret_cast<const float4*>(src);
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-    // staging: four 16-B loads in flight per lane before any LDS store
-    int i = threadIdx.x;
-    for (; i + 768 < nf4; i += 1024) {
-      float4 v[4];
+    // the whole tile in one round trip: every lane issues all of its 16-B loads (from clamped
+    // addresses, no branch between them) before any LDS store
+    float4 v[kPreU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
+    for (int u = 0; u < kPreU; ++u) v[u] = src4[min((int)threadIdx.x + 256 * u, max(nf4 - 1, 0))];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = v[u];
-    }
-    for (; i < nf4; i += blockDim.x) smem4[i] = src4[i];
+    for (int u = 0; u < kPreU; ++u)
+      if ((int)threadIdx.x + 256 * u < nf4) smem4[threadIdx.x + 256 * u] = v[u];
     for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
   } else {
     // a run that starts off a 16-B boundary (an image of a level with an odd pixel count, e.g. a
@@ -187,6 +185,7 @@ void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDes
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
                     float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand, bool bf) {
+  if (nclass > kPreMaxClass) throw std::runtime_error("pre_nms: more than 96 classes");
   size_t shm = (size_t)kPreTile * nclass * sizeof(float);
   if (bf)
     hipLaunchKernelGGL(k_pre_nms<true>, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,

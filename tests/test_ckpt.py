@@ -167,9 +167,9 @@ def test_object_graph_checkpoint_restores_by_full_name(tmp_path, d0):
     p0 = man[0]
     n0 = int(np.prod(p0["shape"]))
     np.testing.assert_array_equal(part[p0["offset"]:p0["offset"] + n0], blob[p0["offset"]:p0["offset"] + n0])
-    # nothing matches: assert_nontrivial_match
+    # nothing matches: assert_nontrivial_match fails and the hub fallback finds no hub key either
     C.write_object_graph_checkpoint(str(tmp_path / "og3" / "ckpt-1"), {"other/kernel": np.ones(2, np.float32)})
-    with pytest.raises(AssertionError):
+    with pytest.raises(KeyError):
         C.checkpoint_to_blob(str(tmp_path / "og3"), man)
     # the string tensor's checksums are verified
     data = bytearray(open(prefix + ".data-00000-of-00001", "rb").read())
@@ -178,3 +178,30 @@ def test_object_graph_checkpoint_restores_by_full_name(tmp_path, d0):
     open(prefix + ".data-00000-of-00001", "wb").write(bytes(data))
     with pytest.raises(ValueError):
         C.object_graph_keys(C.CheckpointReader(prefix))
+
+
+def test_hub_checkpoint_key_follows_util_keras():
+    """_get_cpt_var_name (util_keras.py:86-96): prefix -> hub object, '/' -> '.S', ':0' dropped except
+    under base_model."""
+    assert C.hub_checkpoint_key("class_net/class-predict/depthwise_kernel:0") == \
+        "classes/depthwise_kernel/.ATTRIBUTES/VARIABLE_VALUE"
+    assert C.hub_checkpoint_key("box_net/box-predict/bias:0") == "boxes/bias/.ATTRIBUTES/VARIABLE_VALUE"
+    assert C.hub_checkpoint_key("efficientnet-b0/stem/conv2d/kernel:0") == \
+        "base_model/efficientnet-b0.Sstem.Sconv2d.Skernel:0/.ATTRIBUTES/VARIABLE_VALUE"
+    assert C.hub_checkpoint_key("class_net/class-0/bias:0") == \
+        "base_model/class_net.Sclass-0.Sbias:0/.ATTRIBUTES/VARIABLE_VALUE"
+
+
+def test_hub_checkpoint_fallback_restores_every_variable(tmp_path, d0):
+    """restore_ckpt's AssertionError branch (util_keras.py:141-147): an EfficientDetNetTrainHub
+    checkpoint (object graph of the hub objects, matching no EfficientDetNet variable) is loaded by
+    load_from_hub_checkpoint bit for bit; a missing or mis-shaped hub key fails."""
+    man, blob = d0
+    prefix = str(tmp_path / "hub" / "ckpt-1")
+    C.write_hub_checkpoint(prefix, man, blob)
+    out = C.checkpoint_to_blob(str(tmp_path / "hub"), man)
+    assert np.array_equal(out.view(np.uint32), blob.view(np.uint32)) and out.missing == []
+    short = [p for p in man if p is not man[3]]
+    C.write_hub_checkpoint(str(tmp_path / "hub2" / "ckpt-1"), short, blob)
+    with pytest.raises(KeyError):
+        C.checkpoint_to_blob(str(tmp_path / "hub2"), man)
