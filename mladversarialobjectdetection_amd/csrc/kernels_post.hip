@@ -54,8 +54,6 @@ __device__ __forceinline__ void nms_cand_append(const NmsCand& c, int b, int A, 
 // lane t reduces anchor t's 90 classes (max, first argmax) and decodes its box.
 // ------------------------------------------------------------------------------------------
 constexpr int kPreTile = 128;
-constexpr int kPreMaxClass = 96;                                  // staging registers cover nclass <= 96
-constexpr int kPreU = (kPreTile * kPreMaxClass / 4 + 255) / 256;  // 16-B loads per lane per tile
 
 // BF: the class / box outputs are bf16 activations (PHX_DTYPE_BF16); widened to fp32 when staged
 template <bool BF>
@@ -84,14 +82,16 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
     const long e0 = L.cls_off + run;
     const uint16_t* src = reinterpret_cast<const uint16_t*>(cls_base) + e0;
     if ((e0 & 3) == 0) {
-      // the whole tile in one round trip: every lane issues all of its 8-B loads before any LDS store
       const uint2* src4 = reinterpret_cast<const uint2*>(src);
-      uint2 v[kPreU];
+      int i = threadIdx.x;
+      for (; i + 768 < nf4; i += 1024) {
+        uint2 v[4];
 #pragma unroll
-      for (int u = 0; u < kPreU; ++u) v[u] = src4[min((int)threadIdx.x + 256 * u, max(nf4 - 1, 0))];
+        for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
 #pragma unroll
-      for (int u = 0; u < kPreU; ++u)
-        if ((int)threadIdx.x + 256 * u < nf4) smem4[threadIdx.x + 256 * u] = unpack_bf16x4(v[u]);
+        for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = unpack_bf16x4(v[u]);
+      }
+      for (; i < nf4; i += blockDim.x) smem4[i] = unpack_bf16x4(src4[i]);
       for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = ald1<true>(cls_base, e0 + j);
     } else {
       for (int j = threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = ald1<true>(cls_base, e0 + j);
@@ -100,14 +100,17 @@ __global__ __launch_bounds__(256) void k_pre_nms(const float* __restrict__ cls_b
   const float* src = cls_base + L.cls_off + run;
   const float4* src4 = reinterpret_cast<const float4*>(src);
   if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-    // the whole tile in one round trip: every lane issues all of its 16-B loads (from clamped
-    // addresses, no branch between them) before any LDS store
-    float4 v[kPreU];
+    // staging: four 16-B loads in flight per lane before any LDS store (all of a lane's loads at
+    // once — 12 — measured slower: 99 -> 125 us, the staging registers cost occupancy)
+    int i = threadIdx.x;
+    for (; i + 768 < nf4; i += 1024) {
+      float4 v[4];
 #pragma unroll
-    for (int u = 0; u < kPreU; ++u) v[u] = src4[min((int)threadIdx.x + 256 * u, max(nf4 - 1, 0))];
+      for (int u = 0; u < 4; ++u) v[u] = src4[i + 256 * u];
 #pragma unroll
-    for (int u = 0; u < kPreU; ++u)
-      if ((int)threadIdx.x + 256 * u < nf4) smem4[threadIdx.x + 256 * u] = v[u];
+      for (int u = 0; u < 4; ++u) smem4[i + 256 * u] = v[u];
+    }
+    for (; i < nf4; i += blockDim.x) smem4[i] = src4[i];
     for (int j = (nf4 << 2) + threadIdx.x; j < nf; j += blockDim.x) lg_s[j] = src[j];
   } else {
     // a run that starts off a 16-B boundary (an image of a level with an odd pixel count, e.g. a
@@ -185,7 +188,6 @@ void launch_pre_nms(const float* cls_base, const float* box_base, const LevelDes
                     int nlev, const float* anchors, int A, int B, int nclass, int na,
                     float img_h, float img_w, float thresh, float* scores, int* classes,
                     float* boxes, uint8_t* keep, int ntiles, hipStream_t s, NmsCand cand, bool bf) {
-  if (nclass > kPreMaxClass) throw std::runtime_error("pre_nms: more than 96 classes");
   size_t shm = (size_t)kPreTile * nclass * sizeof(float);
   if (bf)
     hipLaunchKernelGGL(k_pre_nms<true>, dim3(ntiles, B), dim3(256), shm, s, cls_base, box_base, lev_dev, nlev,
@@ -239,7 +241,28 @@ struct NmsPlan {
   int ck_bytes; // chunk-key region (also the bitmap of N bits during compaction)
   int cap;      // positions whose key / visit count live in LDS
   int lds;      // dynamic LDS bytes
+  int lp;       // top-list sort size of the fast path (power of 2, <= kNmsTopMax)
+  int qrows;    // re-queue rows of the fast path (0: general queue only)
 };
+
+// Fast path (k_soft_nms phases F1-F4): batches of the highest-scoring unlisted candidates — at least
+// kNmsTopWant each, all of them when fewer are left — sorted by queue key, their boxes in LDS.  Every
+// candidate outside the batch scores below the batch, so a pop is exact whenever the batch or the
+// re-queue set holds the maximum; the next batch is built when neither does.  Wave 0 takes the batch
+// 64 candidates at a time (a "row", lane j = the row's j-th candidate) and visits all of them at
+// once, one per lane, against every selection so far (the per-lane product in TF's newest-first
+// order); a row candidate's visit stays exact until a later selection overlaps it (a decay factor
+// other than exactly 1 would come first in TF's product), which marks it for a fresh visit at its
+// pop.  Popping a fresh candidate is then a handful of scalar operations.  Visited candidates that
+// stay above the threshold are re-queued in place (the row's lanes); a used-up row moves its
+// re-queued entries to a free row of the re-queue set in LDS (qrows rows of 64, one max per row in a
+// lane of wave 0).  The general queue (phases 3-5) runs instead when a batch or the re-queue set
+// overflows its LDS capacity.
+constexpr int kNmsTopWant = 960;  // a batch of ~1000 sorts at 1024 entries
+constexpr int kNmsTopMax = 4096;
+constexpr int kNmsHistBins = 4096;
+constexpr int kNmsRowBytes = 64 * (8 + 16 + 4);  // a re-queue row: keys | boxes | last-visit counts
+constexpr int kNmsSelBytes = PHX_MAX_OUT_DEV * 16 + (PHX_MAX_OUT_DEV * 4 + 15) / 16 * 16;
 
 static NmsPlan nms_plan(int N) {
   NmsPlan p;
@@ -251,22 +274,134 @@ static NmsPlan nms_plan(int N) {
   int cap = (kNmsLdsBytes - fixed - p.ck_bytes) / 5 / 64 * 64;
   p.cap = std::max(0, std::min(cap, (N + 63) / 64 * 64));
   p.lds = fixed + p.ck_bytes + p.cap * 5;
+  // fast path scratch after the fixed region: sort keys (u64; the score histogram before) | sort
+  // payload (u32) | list boxes (float4) | normalised selected boxes + areas | re-queue rows
+  p.lp = 4;  // >= 4: the list boxes after the u32 payload stay 16-B aligned
+  while (p.lp < std::min(N, kNmsTopMax)) p.lp <<= 1;
+  const int fast = std::max(p.lp * 8, kNmsHistBins * 4) + p.lp * 4 + p.lp * 16 + kNmsSelBytes;
+  p.qrows = std::max(0, std::min(64, (kNmsLdsBytes - fixed - p.ck_bytes - fast) / kNmsRowBytes));
+  p.lds = std::max(p.lds, fixed + p.ck_bytes + fast + p.qrows * kNmsRowBytes);
   p.lds = (p.lds + 15) / 16 * 16;
   return p;
 }
 
+// Wave-wide max of a 64-bit key, on the queue's critical path (a dependent chain per pop): within
+// each 16-lane row by DPP moves (quad xor 1, xor 2, half-row mirror, row mirror — VALU latency), then
+// the four row maxima by readlane (scalar).  A shuffle (ds_bpermute) per step cost ~6x as much.
+template <int CTRL>
+__device__ __forceinline__ void dpp_max_step(uint32_t& hi, uint32_t& lo) {
+  const uint32_t oh = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xf, 0xf, false);
+  const uint32_t ol = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xf, 0xf, false);
+  const bool gt = oh > hi || (oh == hi && ol > lo);
+  hi = gt ? oh : hi;
+  lo = gt ? ol : lo;
+}
+
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+  uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  dpp_max_step<0xB1>(hi, lo);   // quad_perm [1,0,3,2]
+  dpp_max_step<0x4E>(hi, lo);   // quad_perm [2,3,0,1]
+  dpp_max_step<0x141>(hi, lo);  // row_half_mirror
+  dpp_max_step<0x140>(hi, lo);  // row_mirror
+  uint64_t m = 0;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t lo = __shfl_xor((uint32_t)v, o), hi = __shfl_xor((uint32_t)(v >> 32), o);
-    const uint64_t w = ((uint64_t)hi << 32) | lo;
-    v = w > v ? w : v;
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t w = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
+    m = w > m ? w : m;
   }
-  return v;
+  return m;
+}
+
+// sc = orig * f(newest) * f(next) * ... in that order (lane l holds the factor of selection
+// nsel-1-l in f0 and of nsel-65-l in f1; lanes past the visit's selections hold 1).  TF stops at the
+// first product <= thresh; every factor lies in (0, 1], so the full product is <= thresh as well and
+// the outcome is the same — the chain runs without a per-factor test.  A factor of exactly 1 (a
+// selected box that does not overlap: exp(0)) leaves the product unchanged, so only the lanes whose
+// factor differs from 1 are multiplied in, in lane order: a short dependent chain of scalar
+// multiplies instead of one per selection.
+__device__ __forceinline__ float decay_chain(float orig, float f0, float f1) {
+  float sc = orig;
+  unsigned long long m0 = __ballot(f0 != 1.f), m1 = __ballot(f1 != 1.f);
+  while (m0) {
+    const int l = __ffsll(m0) - 1;
+    m0 &= m0 - 1ull;
+    sc *= __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(f0), l));
+  }
+  while (m1) {
+    const int l = __ffsll(m1) - 1;
+    m1 &= m1 - 1ull;
+    sc *= __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(f1), l));
+  }
+  return sc;
 }
 
 __device__ __forceinline__ uint64_t nms_key(uint32_t sbits, int pos) {
   return sbits ? (((uint64_t)sbits << 32) | (uint32_t)~(uint32_t)pos) : 0ull;
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
+__device__ __forceinline__ float4 readlane_f4(float4 v, int l) {
+  return make_float4(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.x), l)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.y), l)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.z), l)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v.w), l)));
+}
+
+// A visit of one candidate (box cb4, queue score orig) by the whole wave: the decay factors of the
+// selections [from, nsel) — lane l computes selection nsel-1-l (and nsel-65-l) — and TF's product.
+__device__ __forceinline__ float nms_visit(float4 cb4, float orig, int from, int nsel, const float4* s_sel,
+                                           float scale, int lane) {
+  const float cb[4] = {cb4.x, cb4.y, cb4.z, cb4.w};
+  const int nf = nsel - from;
+  float f0 = 1.f, f1 = 1.f;
+  if (lane < nf) {
+    const float4 s4 = s_sel[nsel - 1 - lane];
+    const float sbx[4] = {s4.x, s4.y, s4.z, s4.w};
+    const float sim = tf_iou(cb, sbx);
+    f0 = expf(scale * sim * sim);
+  }
+  if (lane + 64 < nf) {
+    const float4 s4 = s_sel[nsel - 65 - lane];
+    const float sbx[4] = {s4.x, s4.y, s4.z, s4.w};
+    const float sim = tf_iou(cb, sbx);
+    f1 = expf(scale * sim * sim);
+  }
+  return decay_chain(orig, f0, f1);
+}
+
+// tf_iou's operands with the corners ordered and the area taken (the same operations in the same
+// order, so nms_factor(norm(i), norm(j)) == expf(scale * iou^2) of tf_iou(i, j) bit for bit)
+struct NmsNBox {
+  float y0, x0, y1, x1, a;
+};
+
+__device__ __forceinline__ NmsNBox nms_norm(float4 b) {
+  NmsNBox n;
+  n.y0 = fminf(b.x, b.z);
+  n.x0 = fminf(b.y, b.w);
+  n.y1 = fmaxf(b.x, b.z);
+  n.x1 = fmaxf(b.y, b.w);
+  n.a = (n.y1 - n.y0) * (n.x1 - n.x0);
+  return n;
+}
+
+// whether candidate c and selection s intersect; when not, their decay factor is exactly 1
+__device__ __forceinline__ bool nms_overlap(const NmsNBox& c, const NmsNBox& s) {
+  return fminf(c.y1, s.y1) > fmaxf(c.y0, s.y0) && fminf(c.x1, s.x1) > fmaxf(c.x0, s.x0);
+}
+
+__device__ __forceinline__ float nms_factor(const NmsNBox& c, const NmsNBox& s, float scale) {
+  if (c.a <= 0.f || s.a <= 0.f) return 1.f;
+  const float iy0 = fmaxf(c.y0, s.y0), ix0 = fmaxf(c.x0, s.x0);
+  const float iy1 = fminf(c.y1, s.y1), ix1 = fminf(c.x1, s.x1);
+  const float inter = fmaxf(iy1 - iy0, 0.f) * fmaxf(ix1 - ix0, 0.f);
+  const float sim = inter / (c.a + s.a - inter);
+  return expf(scale * sim * sim);
 }
 
 __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
@@ -275,7 +410,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     float score_thresh, float scale, int max_out, float clip_hi, float* __restrict__ out_boxes,
     float* __restrict__ out_scores, int* __restrict__ out_count, float4* __restrict__ cbox_all,
     uint32_t* __restrict__ gkey_all, int* __restrict__ gwi_all, uint8_t* __restrict__ gwb_all,
-    NmsCand cand, NmsPlan pl) {
+    NmsCand cand, NmsPlan pl, int dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char nms_smem[];
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -366,6 +501,304 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   const int n = s_scan[kNmsThreads - 1];
   __syncthreads();  // gwi complete (global writes of this workgroup, visible after the barrier)
 
+  // ---- fast path -------------------------------------------------------------------------
+  // Batches of the highest-scoring candidates not yet listed (>= kNmsTopWant each, or all that are
+  // left), sorted by queue key with their boxes in LDS; wave 0 pops from the batch's rows and from
+  // the re-queue set (rows of 64 in LDS) and asks for the next batch when the batch is used up while
+  // an unlisted candidate could be next.  The general queue below runs instead (from scratch) when a
+  // batch or the re-queue set overflows.
+  bool fast_done = false;
+  if (pl.qrows > 0) {
+    unsigned char* fbase = reinterpret_cast<unsigned char*>(s_key);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(fbase);                    // [kNmsHistBins]
+    uint64_t* lkey = reinterpret_cast<uint64_t*>(fbase);                    // [lp] (after the histograms)
+    uint32_t* lpay = reinterpret_cast<uint32_t*>(fbase + max(pl.lp * 8, kNmsHistBins * 4));  // [lp]
+    float4* lbox = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(lpay) + pl.lp * 4);  // [lp]
+    float4* s_seln = lbox + pl.lp;                                           // [PHX_MAX_OUT_DEV]
+    float* s_sela = reinterpret_cast<float*>(s_seln + PHX_MAX_OUT_DEV);      // [PHX_MAX_OUT_DEV]
+    unsigned char* qbase = reinterpret_cast<unsigned char*>(s_seln) + kNmsSelBytes;
+    uint64_t* qkey = reinterpret_cast<uint64_t*>(qbase);                     // [qrows][64]
+    float4* qbox = reinterpret_cast<float4*>(qkey + pl.qrows * 64);           // [qrows][64]
+    int* qfrom = reinterpret_cast<int*>(qbox + pl.qrows * 64);                // [qrows][64]
+    // F1. every candidate's score bits (positive floats: integer order = float order) to gkey,
+    //     eight gathers in flight per lane
+    for (int p0 = 0; p0 < n; p0 += 8 * kNmsThreads) {
+      int a[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a[u] = gwi[min(p0 + u * kNmsThreads + t, n - 1)];
+      uint32_t k[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) k[u] = __float_as_uint(sb[a[u]]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (p0 + u * kNmsThreads + t < n) gkey[p0 + u * kNmsThreads + t] = k[u];
+    }
+    __syncthreads();
+    // wave 0's queue state, kept across batches: the selections, and the re-queue rows' maxima
+    // (lane r: row r's largest key, 0 = a free row) with their overall maximum
+    int nsel = 0;
+    uint64_t rmax = 0ull, cmax = 0ull;
+    int crow = 0;
+    int npop = 0, nrq = 0, nbatch = 0;  // PHX_NMS_STATS counts
+    uint32_t hi = 0xffffffffu;  // candidates with score bits < hi are not listed yet
+    int rem = n;                // how many
+    int state = 0;              // 0 next batch, 1 done, 2 fall back
+    while (state == 0) {
+      // F2. the batch: unlisted keys with key >> 8 >= thr24, the largest 24-bit prefix whose count
+      //     reaches min(rem, kNmsTopWant) (two histogram passes: bits 31..20, then 19..8 inside the
+      //     crossing bin); thr24 = 0 lists every remaining candidate
+      uint32_t thr24 = 0;
+      if (rem > kNmsTopWant) {
+        uint32_t prefix = 0;
+        int need = kNmsTopWant;
+        for (int pass = 0; pass < 2; ++pass) {
+          for (int i = t; i < kNmsHistBins; i += kNmsThreads) hist[i] = 0u;
+          __syncthreads();
+          for (int p0 = 0; p0 < n; p0 += 8 * kNmsThreads) {
+            uint32_t k[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) k[u] = gkey[min(p0 + u * kNmsThreads + t, n - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              if (p0 + u * kNmsThreads + t >= n || k[u] >= hi) continue;
+              if (pass == 0) atomicAdd(&hist[k[u] >> 20], 1u);
+              else if ((k[u] >> 20) == prefix) atomicAdd(&hist[(k[u] >> 8) & 4095u], 1u);
+            }
+          }
+          __syncthreads();
+          // suffix counts from the top bin down: thread t owns bins [4095 - 16t - 15, 4095 - 16t]
+          int cnt = 0;
+          for (int i = 0; i < 16; ++i) cnt += (int)hist[4095 - 16 * t - i];
+          s_scan[t] = cnt;
+          __syncthreads();
+          for (int off = 1; off < kNmsThreads; off <<= 1) {
+            const int v = t >= off ? s_scan[t - off] : 0;
+            __syncthreads();
+            s_scan[t] += v;
+            __syncthreads();
+          }
+          const int before = s_scan[t] - cnt;  // candidates in higher bins
+          if (before < need && before + cnt >= need) {
+            int acc = before, bin = 4095 - 16 * t;
+            for (int i = 0; i < 16; ++i) {
+              acc += (int)hist[4095 - 16 * t - i];
+              bin = 4095 - 16 * t - i;
+              if (acc >= need) break;
+            }
+            s_misc[4] = bin;
+            s_misc[5] = need - (acc - (int)hist[bin]);  // still needed inside the crossing bin
+          }
+          __syncthreads();
+          const uint32_t bin = (uint32_t)s_misc[4];
+          need = s_misc[5];
+          prefix = pass == 0 ? bin : ((prefix << 12) | bin);
+          __syncthreads();
+        }
+        thr24 = prefix;
+      }
+      const uint32_t lo = thr24 << 8;  // unlisted after this batch: score bits < lo
+      // F3. the batch's keys and boxes (any order; the sort below orders them by queue key)
+      if (t == 0) s_misc[6] = 0;
+      __syncthreads();
+      for (int p0 = 0; p0 < n; p0 += 8 * kNmsThreads) {
+        uint32_t k[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) k[u] = gkey[min(p0 + u * kNmsThreads + t, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int p = p0 + u * kNmsThreads + t;
+          if (p < n && k[u] < hi && (k[u] >> 8) >= thr24) {
+            const int j = atomicAdd(&s_misc[6], 1);
+            if (j < pl.lp) {
+              lkey[j] = nms_key(k[u], p);
+              lbox[j] = *reinterpret_cast<const float4*>(bb + (long)gwi[p] * 4);
+            }
+          }
+        }
+      }
+      __syncthreads();
+      const int L = s_misc[6];
+      if (L > pl.lp) {
+        state = 2;
+        break;
+      }
+      rem -= L;
+      ++nbatch;
+      int ls = 1;  // sort size: the batch rounded up to a power of 2
+      while (ls < L) ls <<= 1;
+      for (int j = t; j < ls; j += kNmsThreads) {
+        lpay[j] = (uint32_t)j;
+        if (j >= L) lkey[j] = 0ull;
+      }
+      __syncthreads();
+      // bitonic sort, descending by key (keys are unique: the low word is ~position)
+      for (int k = 2; k <= ls; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+          for (int i = t; i < ls; i += kNmsThreads) {
+            const int ix = i ^ jj;
+            if (ix > i) {
+              const uint64_t a = lkey[i], b2 = lkey[ix];
+              const bool desc = (i & k) == 0;
+              if (desc ? (a < b2) : (a > b2)) {
+                lkey[i] = b2;
+                lkey[ix] = a;
+                const uint32_t pa = lpay[i];
+                lpay[i] = lpay[ix];
+                lpay[ix] = pa;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+      // F4. the lazy queue over the batch's rows + the re-queue set, wave 0 alone
+      if (wave == 0) {
+        int f = 0, st = 1;
+        int rown = 0, jn = 0;       // the row's candidates, the next one not popped yet
+        uint64_t ck = 0ull;         // lane j: the row's j-th candidate's key
+        float4 cbx = make_float4(0.f, 0.f, 0.f, 0.f);  // its box
+        NmsNBox cn = nms_norm(cbx);
+        float cs = 0.f;             // its score after the row-wide visit
+        bool dirty = false;         // a selection since that visit overlaps it
+        uint64_t rk = 0ull;         // its re-queue key once popped (0: not in the queue)
+        int rfrom = 0;              // selections at that pop
+        uint64_t qmax = 0ull;       // max of rk
+        // a new selection: lane 0 records it; the row's candidates not popped yet (lanes >= j0)
+        // that it overlaps with a decay factor other than 1 need a fresh visit
+        auto select = [&](float4 b4, float sc, int j0) {
+          const NmsNBox sn = nms_norm(b4);
+          if (lane == 0) {
+            s_sel[nsel] = b4;
+            s_sels[nsel] = sc;
+            s_seln[nsel] = make_float4(sn.y0, sn.x0, sn.y1, sn.x1);
+            s_sela[nsel] = sn.a;
+          }
+          ++nsel;
+          const bool ov = lane >= j0 && lane < rown && nms_overlap(cn, sn);
+          if (__ballot(ov)) {
+            if (ov && nms_factor(cn, sn, scale) != 1.f) dirty = true;
+          }
+        };
+        while (nsel < max_out) {
+          if (jn >= rown) {
+            // the row is used up: its re-queued candidates move to a free row of the set
+            if (qmax) {
+              const unsigned long long fr = __ballot(lane < pl.qrows && rmax == 0ull);
+              if (!fr) { st = 2; break; }
+              const int r = __ffsll(fr) - 1;
+              qkey[r * 64 + lane] = rk;
+              qbox[r * 64 + lane] = cbx;
+              qfrom[r * 64 + lane] = rfrom;
+              if (lane == r) rmax = qmax;
+              if (qmax > cmax) { cmax = qmax; crow = r; }
+              rk = 0ull;
+              qmax = 0ull;
+            }
+            rown = 0;
+            if (f < L) {
+              // the next row, visited against every selection so far, one candidate per lane
+              const int j = f + lane;
+              ck = j < L ? lkey[j] : 0ull;
+              cbx = j < L ? lbox[lpay[j]] : make_float4(0.f, 0.f, 0.f, 0.f);
+              cn = nms_norm(cbx);
+              rown = min(64, L - f);
+              f += rown;
+              jn = 0;
+              dirty = false;
+              float sc = __uint_as_float((uint32_t)(ck >> 32));
+              for (int k = nsel - 1; k >= 0; --k) {
+                const float4 s4 = s_seln[k];
+                const NmsNBox sn{s4.x, s4.y, s4.z, s4.w, s_sela[k]};
+                const bool ov = lane < rown && nms_overlap(cn, sn);
+                if (__ballot(ov)) {
+                  if (ov) sc *= nms_factor(cn, sn, scale);
+                }
+              }
+              cs = sc;
+            }
+          }
+          const uint64_t fk = jn < rown ? readlane_u64(ck, jn) : 0ull;
+          const uint64_t rtop = qmax > cmax ? qmax : cmax;
+          if (f >= L && jn >= rown && rem > 0 && (uint32_t)(rtop >> 32) < lo) { st = 0; break; }  // an unlisted one could be next
+          const uint64_t top = rtop > fk ? rtop : fk;
+          if (top == 0ull) break;
+          const float orig = __uint_as_float((uint32_t)(top >> 32));
+          if (!(orig > score_thresh)) break;
+          const int pos = (int)~(uint32_t)top;
+          ++npop;
+          if (rtop > fk) {
+            // a re-queued candidate: in this row (qmax) or in row crow of the set
+            ++nrq;
+            const bool cur = qmax > cmax;
+            uint64_t rowk = 0ull;
+            int owner, from;
+            float4 b4;
+            if (cur) {
+              owner = __ffsll(__ballot(rk == qmax)) - 1;
+              from = __builtin_amdgcn_readlane(rfrom, owner);
+              b4 = readlane_f4(cbx, owner);
+            } else {
+              rowk = qkey[crow * 64 + lane];
+              owner = __ffsll(__ballot(rowk == cmax)) - 1;
+              from = qfrom[crow * 64 + owner];
+              b4 = qbox[crow * 64 + owner];
+            }
+            const float sc = nms_visit(b4, orig, from, nsel, s_sel, scale, lane);
+            uint64_t nk = 0ull;
+            if (sc == orig) select(b4, sc, jn);
+            else if (sc > score_thresh) nk = nms_key(__float_as_uint(sc), pos);
+            if (cur) {
+              if (lane == owner) {
+                rk = nk;
+                rfrom = nsel;
+              }
+              qmax = wave_max_u64(rk);
+            } else {
+              if (lane == owner) {
+                rowk = nk;
+                qkey[crow * 64 + owner] = nk;
+                qfrom[crow * 64 + owner] = nsel;
+              }
+              const uint64_t m = wave_max_u64(rowk);
+              if (lane == crow) rmax = m;
+              cmax = wave_max_u64(rmax);
+              crow = cmax ? __ffsll(__ballot(rmax == cmax)) - 1 : 0;
+            }
+          } else {
+            // the row's next candidate: its row-wide visit holds unless a later selection overlaps it
+            const int j = jn++;
+            float sc;
+            if ((__ballot(dirty) >> j) & 1ull) sc = nms_visit(readlane_f4(cbx, j), orig, 0, nsel, s_sel, scale, lane);
+            else sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), j));
+            if (sc == orig) {
+              select(readlane_f4(cbx, j), sc, jn);
+            } else if (sc > score_thresh) {
+              const uint64_t nk = nms_key(__float_as_uint(sc), pos);
+              if (lane == j) {
+                rk = nk;
+                rfrom = nsel;
+              }
+              if (nk > qmax) qmax = nk;
+            }
+          }
+        }
+        if (lane == 0) {
+          s_misc[1] = nsel;
+          s_misc[2] = st;
+        }
+      }
+      __syncthreads();
+      state = s_misc[2];  // workgroup-uniform
+      hi = lo;
+      __syncthreads();    // the next batch rewrites the list
+    }
+    if (dbg && t == 0)
+      printf("nms image %d: %d candidates, %d batch(es), %d pops (%d re-queued), %d selected -> %s\n", b, n,
+             nbatch, npop, nrq, s_misc[1], state == 1 ? "fast path" : "general queue");
+    fast_done = state == 1;
+  }
+  if (!fast_done) {
+
   // 3. gather keys and boxes in candidate order (coalesced over positions)
   for (int p0 = 0; p0 < n; p0 += 4 * kNmsThreads) {
     int a[4];
@@ -440,42 +873,10 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
       const int c = (int)~(uint32_t)top;
       const float orig = __uint_as_float(vbits);
       const int from = c < cap ? (int)s_wb[c] : (int)vgwb[c];
+      // decay factors of the selections since the last visit, newest first; TF's decay order,
+      // exact-1 factors skipped
       const float4 cb4 = cbox[c];
-      const float cb[4] = {cb4.x, cb4.y, cb4.z, cb4.w};
-      // decay factors of the selections since the last visit, newest first: lane l holds
-      // selection nsel-1-l (and nsel-65-l)
-      const int nf = nsel - from;
-      float f0 = 1.f, f1 = 1.f;
-      if (lane < nf) {
-        const float4 s4 = s_sel[nsel - 1 - lane];
-        const float sbx[4] = {s4.x, s4.y, s4.z, s4.w};
-        const float sim = tf_iou(cb, sbx);
-        f0 = expf(scale * sim * sim);
-      }
-      if (lane + 64 < nf) {
-        const float4 s4 = s_sel[nsel - 65 - lane];
-        const float sbx[4] = {s4.x, s4.y, s4.z, s4.w};
-        const float sim = tf_iou(cb, sbx);
-        f1 = expf(scale * sim * sim);
-      }
-      // sc = orig * f(newest) * f(next) * ... in that order.  TF stops at the first product
-      // <= thresh; every factor is in (0, 1], so the full product is <= thresh too and the outcome
-      // (removed: key 0, never selected) is the same — so the chain runs without the per-factor
-      // test, 16 factors at a time, padded with exact 1.0f: independent readlanes, then a
-      // dependent multiply chain with scalar operands.
-      float sc = orig;
-      for (int k0 = 0; k0 < nf; k0 += 16) {
-        float fk[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int k = k0 + u;
-          const float v = k < 64 ? f0 : f1;  // k0 is wave-uniform: a uniform select
-          fk[u] = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)__float_as_uint(v), k & 63));
-          if (k >= nf) fk[u] = 1.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u) sc *= fk[u];
-      }
+      const float sc = nms_visit(cb4, orig, from, nsel, s_sel, scale, lane);
       uint32_t nk;
       if (sc == orig) {
         if (lane == 0) {
@@ -520,6 +921,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     }
     if (lane == 0) s_misc[1] = nsel;
   }
+  }  // general queue
   __syncthreads();
   // 6. outputs: padded to max_out, boxes clipped to [0, image_size] (postprocess.py:61-64)
   const int nsel = s_misc[1];
@@ -541,6 +943,15 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
 }
 
 size_t soft_nms_work_floats(int B, int N) { return (size_t)B * N * 7; }
+
+// PHX_NMS_STATS=1: each image's soft-NMS reports its candidate count, list size, pops and path
+static int nms_debug() {
+  static const int v = [] {
+    const char* e = std::getenv("PHX_NMS_STATS");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
+}
 
 void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* keep, int keep_mask,
                      const int* count, int B, int N, float score_thresh, float soft_sigma,
@@ -565,7 +976,7 @@ void launch_soft_nms(const float* boxes, const float* scores, const uint8_t* kee
   (void)attr;
   hipLaunchKernelGGL(k_soft_nms, dim3(B), dim3(kNmsThreads), pl.lds, s, boxes, scores, keep, keep_mask,
                      count, N, score_thresh, scale, max_out, clip_hi, out_boxes, out_scores, out_count,
-                     cbox, gkey, gwi, gwb, cand, pl);
+                     cbox, gkey, gwi, gwb, cand, pl, nms_debug());
   PHX_LAUNCH_CHECK();
 }
 
