@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <sstream>
@@ -238,6 +239,25 @@ void gemm(const float* A, const float* Bt, const float* bias, float* C, long M, 
   launch_gemm(InX{A, nullptr, nullptr, nullptr, 0}, Bt, bias, C, (int)M, N, K, acc, nullptr, 1, s, part);
 }
 
+// PHX_UN_GATHER=0: the U-Net's wide 3x3 convs write their column matrix (k_im2col) and run the plain
+// GEMM over it instead of gathering it inside the GEMM (read on every call: tests compare the two)
+bool un_gather_on() {
+  const char* e = std::getenv("PHX_UN_GATHER");
+  return !(e && e[0] == '0');
+}
+
+// a 3x3 conv of more than kConvMaxN outputs (or K > kConvMaxKp): the GEMM over the gathered column
+// matrix (k_im2col's gathers), implicit when the geometry allows it
+void conv3_gemm(const float* x, float* col, const float* Bt, const float* bias, float* out, int B, int H, int W, int C,
+                int Ho, int Wo, int N, int Kp, int mode, int st, int pt, int pl, float* part, hipStream_t s) {
+  if (un_gather_on() && gemm_gather_ok(B, H, W, C, Ho, Wo, Kp, mode, st, pt, pl)) {
+    launch_gemm_gather(x, B, H, W, C, Ho, Wo, mode, st, pt, pl, Bt, bias, out, N, Kp, s, part);
+    return;
+  }
+  un_im2col(x, col, B, H, W, C, Ho, Wo, Kp, mode, st, pt, pl, s);
+  gemm(col, Bt, bias, out, (long)B * Ho * Wo, N, Kp, false, part, s);
+}
+
 }  // namespace
 
 void phx_def::workspace(int B) {
@@ -357,8 +377,7 @@ void phx_def::unet_forward(int B, const float* W, bool train, int64_t stp, int g
     const long M = (long)B * H * H;
     DScope g(victim, "unet_conv", 2.0 * M * c.co * 9 * c.ci, 4.0 * M * (c.ci + c.co), s);
     if (un_conv3_small(x, bt + c.bt_f, W + c.b, y, B, H, H, c.ci, H, H, c.co, c.kp_f, 0, 1, 1, 1, s)) return;
-    un_im2col(x, col, B, H, H, c.ci, H, H, c.kp_f, 0, 1, 1, 1, s);
-    gemm(col, bt + c.bt_f, W + c.b, y, M, c.co, c.kp_f, false, gpart, s);
+    conv3_gemm(x, col, bt + c.bt_f, W + c.b, y, B, H, H, c.ci, H, H, c.co, c.kp_f, 0, 1, 1, 1, gpart, s);
   };
   auto bn_fwd = [&](UBn& b, const float* y, long M, float* a, int act) {
     DScope g(victim, "unet_bn", 0.0, (train ? 4.0 : 0.0) * M * b.c + (a ? 8.0 * M * b.c : 0.0), s);
@@ -395,8 +414,7 @@ void phx_def::unet_forward(int B, const float* W, bool train, int64_t stp, int g
       const long Min = (long)B * hin * hin;
       DScope g(victim, "unet_conv", 2.0 * Min * 9 * up.ci * n, 4.0 * (Min * up.ci + M * n), s);
       if (!un_conv3_small(x, bt + up.bt_f, W + up.b, d.up, B, hin, hin, up.ci, H, H, n, up.kp_f, 1, 2, 0, 0, s)) {
-        un_im2col(x, col, B, hin, hin, up.ci, H, H, up.kp_f, 1, 2, 0, 0, s);
-        gemm(col, bt + up.bt_f, W + up.b, d.up, M, n, up.kp_f, false, gpart, s);
+        conv3_gemm(x, col, bt + up.bt_f, W + up.b, d.up, B, hin, hin, up.ci, H, H, n, up.kp_f, 1, 2, 0, 0, gpart, s);
       }
     }
     const float* skip = et[3 - i].a2;
@@ -494,8 +512,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     const long M = (long)B * H * H;
     DScope g(victim, "unet_conv", 2.0 * M * c.ci * 9 * c.co, 4.0 * M * (c.co + c.ci), s);
     if (un_conv3_small(dy, bt + c.bt_d, nullptr, dx, B, H, H, c.co, H, H, c.ci, c.kp_d, 0, 1, 1, 1, s)) return;
-    un_im2col(dy, col, B, H, H, c.co, H, H, c.kp_d, 0, 1, 1, 1, s);
-    gemm(col, bt + c.bt_d, nullptr, dx, M, c.ci, c.kp_d, false, gpart, s);
+    conv3_gemm(dy, col, bt + c.bt_d, nullptr, dx, B, H, H, c.co, H, H, c.ci, c.kp_d, 0, 1, 1, 1, gpart, s);
   };
   // da2 (clobbered) -> dx of the block input (when dx != nullptr)
   auto block_bwd = [&](const Block& k, const float* xin, int H, const float* y1, const float* a1, const float* y2,
@@ -577,8 +594,7 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
     {
       DScope g(victim, "unet_conv", 2.0 * Min * 9 * up.ci * n, 4.0 * (M * n + Min * up.ci), s);
       if (!un_conv3_small(tmpX, bt + up.bt_d, nullptr, tmpY, B, H, H, n, hin, hin, up.ci, up.kp_d, 0, 2, 0, 0, s)) {
-        un_im2col(tmpX, col, B, H, H, n, hin, hin, up.kp_d, 0, 2, 0, 0, s);
-        gemm(col, bt + up.bt_d, nullptr, tmpY, Min, up.ci, up.kp_d, false, gpart, s);
+        conv3_gemm(tmpX, col, bt + up.bt_d, nullptr, tmpY, B, H, H, n, hin, hin, up.ci, up.kp_d, 0, 2, 0, 0, gpart, s);
       }
     }
     std::swap(tmpX, tmpY);  // tmpX = gradient of the next (earlier) block's output

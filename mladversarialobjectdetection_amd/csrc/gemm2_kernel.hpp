@@ -23,6 +23,10 @@
 //    registers (two passes, xor-32 shuffle), merged across the WM waves in LDS and folded across
 //    the workgroup's tiles (Chan), one partial row per workgroup.
 //  * Split-K (blockIdx.z) writes fp32 partial slabs reduced by k_gemm_splitk_reduce(_stats).
+//  * MODE 4 (implicit im2col): A[m][k] is gathered from an NHWC tensor — the column matrix of a 3x3
+//    convolution, k = (ky*3 + kx)*C + c — with the geometry packed into Gemm2Args::rpi (g2_geo):
+//    power-of-2 channel and spatial sizes, so a row's pixel and a quad's (tap, channel) are shifts
+//    and masks.  A 16-B quad never straddles a tap (C >= 4).
 //  * Grouped launch: up to kMaxSeg GEMMs with the same B operand, N and K but their own A, C, M and
 //    statistics sinks (the per-level members of a class/box-head conv, whose weights are shared
 //    across pyramid levels) run as one grid; blockIdx.z = segment * splits + split.
@@ -84,10 +88,23 @@ struct G2 {
   static constexpr int LDS_FLOATS = 2 * (BM + BN) * LD * ESZ / 4;
 };
 
+// MODE 4 gather geometry, packed into 26 bits of Gemm2Args::rpi: log2 C | log2 Wo | log2 Ho | log2 W |
+// log2 H | stride - 1 | pad top | pad left | gather mode (0 conv: x[oy*s + ky - pt][ox*s + kx - pl];
+// 1 stride-2 transposed conv: x[(oy - ky) / 2][(ox - kx) / 2] when both are even)
+struct G2Geo {
+  int lC, lWo, lHo, lW, lH, s, pt, pl, mode;
+};
+__host__ __device__ __forceinline__ G2Geo g2_geo(uint32_t q) {
+  return G2Geo{(int)(q & 15), (int)((q >> 4) & 15), (int)((q >> 8) & 15), (int)((q >> 12) & 15),
+               (int)((q >> 16) & 15), (int)((q >> 20) & 1) + 1, (int)((q >> 21) & 3), (int)((q >> 23) & 3),
+               (int)((q >> 25) & 1)};
+}
+
 template <int WM, int TM, int TN, int MODE, bool BF = false>
 struct G2Regs {
   using P = G2<WM, TM, TN, MODE, BF>;
   float4 a[P::NA];
+  bool gok[MODE == 4 ? P::NA : 1];
   float4 y[MODE == 3 ? P::NA : 1];
   float4 rs[MODE == 2 ? P::NA : 1];
   float4 b[P::NB];
@@ -114,17 +131,45 @@ __device__ __forceinline__ void g2_load(G2Regs<WM, TM, TN, MODE, BF>& r, const G
   const int kc = kok ? kk : kend - 4;  // kend >= 4, K % 4 == 0
   if (MODE == 1 || MODE == 2) r.ck = inx_chan4(a.A, kc);
   if (MODE == 3) r.gk = gx_chan4(a.G, kc);
+  if constexpr (MODE == 4) {
+    const G2Geo g = g2_geo((uint32_t)a.rpi);
+    const int tap = kc >> g.lC, c = kc & ((1 << g.lC) - 1);
+    const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;  // tap / 3 for tap < 9
 #pragma unroll
-  for (int u = 0; u < P::NA; ++u) {
-    const int row = m0 + (t + 256 * u) / P::KQ;
-    const long e = (long)min(row, a.M - 1) * a.K + kc;
-    if (MODE == 3) {
-      r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
-      r.y[u] = ald4<ST == 2>(a.G.y, e);
-    } else {
-      r.a[u] = ald4<ST == 1>(a.A.p, e);
-      if (MODE == 2)
-        r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(min(row, a.M - 1) / a.rpi) * a.K + kc);
+    for (int u = 0; u < P::NA; ++u) {
+      const int row = min(m0 + (t + 256 * u) / P::KQ, a.M - 1);
+      const int ox = row & ((1 << g.lWo) - 1), oy = (row >> g.lWo) & ((1 << g.lHo) - 1);
+      const int b = row >> (g.lWo + g.lHo);
+      int iy, ix;
+      bool ok = kok && tap < 9;
+      if (g.mode == 0) {
+        iy = oy * g.s + ky - g.pt;
+        ix = ox * g.s + kx - g.pl;
+      } else {
+        const int dy = oy - ky, dx = ox - kx;
+        ok = ok && dy >= 0 && dx >= 0 && !(dy & 1) && !(dx & 1);
+        iy = dy >> 1;
+        ix = dx >> 1;
+      }
+      ok = ok && iy >= 0 && iy < (1 << g.lH) && ix >= 0 && ix < (1 << g.lW);
+      const long e = ok ? ((((long)b << g.lH) + iy) << g.lW | ix) << g.lC | c : 0;
+      r.a[u] = *reinterpret_cast<const float4*>(a.A.p + e);
+      r.gok[u] = ok;
+    }
+  }
+  if constexpr (MODE != 4) {
+#pragma unroll
+    for (int u = 0; u < P::NA; ++u) {
+      const int row = m0 + (t + 256 * u) / P::KQ;
+      const long e = (long)min(row, a.M - 1) * a.K + kc;
+      if (MODE == 3) {
+        r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
+        r.y[u] = ald4<ST == 2>(a.G.y, e);
+      } else {
+        r.a[u] = ald4<ST == 1>(a.A.p, e);
+        if (MODE == 2)
+          r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(min(row, a.M - 1) / a.rpi) * a.K + kc);
+      }
     }
   }
 #pragma unroll
@@ -184,7 +229,9 @@ __device__ __forceinline__ void g2_store_act(const G2Regs<WM, TM, TN, MODE, BF>&
     if (t + 256 * u >= P::BM * P::KQ) continue;
     const int rl = (t + 256 * u) / P::KQ;
     float4 v = r.a[u];
-    if (kok && m0 + rl < a.M) {
+    if (MODE == 4) {
+      if (!(r.gok[u] && m0 + rl < a.M)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (kok && m0 + rl < a.M) {
       if (MODE == 1 || MODE == 2) v = inx_apply4(ax, r.ck, v);
       if (MODE == 2) {
         v.x *= r.rs[u].x; v.y *= r.rs[u].y; v.z *= r.rs[u].z; v.w *= r.rs[u].w;
@@ -535,6 +582,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
 // forward modes run ST 1 and its gradient views ST 2; an fp32 context always ST 0.
 template <int WM, int TM, int TN, int MODE, int SK, int NS>
 static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st) {
+  if constexpr (MODE == 4) {  // the implicit im2col: fp32 only
+    if (bf || st) throw std::logic_error("gemm2: the implicit im2col runs in fp32");
+    PHX_TLAUNCH((k_gemm2<WM, TM, TN, 4, 0, NS, false, 0>), g, dim3(256), 0, s, a);
+    return;
+  }
   if (!bf) {
     if (st) throw std::logic_error("gemm2: bf16 storage needs the bf16 compute type");
     PHX_TLAUNCH((k_gemm2<WM, TM, TN, MODE, SK, NS, false, 0>), g, dim3(256), 0, s, a);
@@ -574,6 +626,10 @@ void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>
         break;                                                                                                  \
       case 2:                                                                                                   \
         sk == 1 ? g2_go<WM, TM, TN, 2, 1, NS>(g, s, a, bf, st) : g2_go<WM, TM, TN, 2, 0, NS>(g, s, a, bf, st); \
+        break;                                                                                                  \
+      case 4:                                                                                                   \
+        if constexpr (NS == 1) g2_go<WM, TM, TN, 4, 0, NS>(g, s, a, bf, st);                                  \
+        else throw std::logic_error("gemm2: no grouped implicit im2col");                                      \
         break;                                                                                                  \
       default:                                                                                                  \
         sk == 2 ? g2_go<WM, TM, TN, 3, 2, NS>(g, s, a, bf, st) : g2_go<WM, TM, TN, 3, 0, NS>(g, s, a, bf, st); \

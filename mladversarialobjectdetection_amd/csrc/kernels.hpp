@@ -82,6 +82,10 @@ int gemm_splitk_finish(const float* partial, int splits, int M, int N, const flo
                        bool acc, StatSink sink, hipStream_t s, bool cbf = false);
 // dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
 // with a GradSink, the BN-backward sums of the dgrad's result (returns the partial rows)
+// 3x3 convolution GEMM over an implicitly gathered column matrix (kernels_conv.hip)
+bool gemm_gather_ok(int B, int H, int W, int C, int Ho, int Wo, int K, int mode, int s, int pt, int pl);
+int launch_gemm_gather(const float* x, int B, int H, int W, int C, int Ho, int Wo, int mode, int s, int pt, int pl,
+                       const float* Bt, const float* bias, float* out, int N, int K, hipStream_t st, float* partial);
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                       hipStream_t s, float* partial, GradSink gs = GradSink{}, bool bf16 = false);
 int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16 = false);

@@ -973,6 +973,38 @@ int launch_gemm(InX A, const float* Bt, const float* bias, float* C, int M, int 
                    GradSink{});
 }
 
+// A 3x3 convolution as one GEMM whose A operand is the column matrix gathered on the fly (k_gemm2
+// MODE 4): out[m][n] = bias[n] + sum_k col[m][k] Bt[n][k], k = (ky*3 + kx)*C + c, for the gathers of
+// k_im2col (mode 0: stride s, pads (pt, pl); mode 1: the stride-2 transposed conv's parity gather).
+// Needs power-of-2 C >= 4 and spatial sizes (shifts and masks in the kernel) and K = 9C; returns
+// false (nothing launched) otherwise.
+static int ilog2_exact(long v) {
+  int l = 0;
+  while ((1L << l) < v) ++l;
+  return (1L << l) == v ? l : -1;
+}
+
+bool gemm_gather_ok(int B, int H, int W, int C, int Ho, int Wo, int K, int mode, int s, int pt, int pl) {
+  const int lC = ilog2_exact(C), lW = ilog2_exact(W), lH = ilog2_exact(H), lWo = ilog2_exact(Wo),
+            lHo = ilog2_exact(Ho);
+  return C >= 4 && K == 9 * C && lC >= 0 && lC <= 15 && lW >= 0 && lW <= 15 &&
+         lH >= 0 && lH <= 15 && lWo >= 0 && lWo <= 15 && lHo >= 0 && lHo <= 15 && (s == 1 || s == 2) && pt >= 0 &&
+         pt <= 3 && pl >= 0 && pl <= 3 && (mode == 0 || (mode == 1 && s == 2)) &&
+         (long)B * Ho * Wo < (1L << 31) && ((long)B << (lH + lW + lC)) < (1L << 40);
+}
+
+int launch_gemm_gather(const float* x, int B, int H, int W, int C, int Ho, int Wo, int mode, int s, int pt, int pl,
+                       const float* Bt, const float* bias, float* out, int N, int K, hipStream_t st, float* partial) {
+  if (!gemm_gather_ok(B, H, W, C, Ho, Wo, K, mode, s, pt, pl))
+    throw std::runtime_error("gemm gather: unsupported geometry");
+  if (reinterpret_cast<uintptr_t>(x) & 15) throw std::runtime_error("gemm gather: input not 16-B aligned");
+  const uint32_t geo = (uint32_t)ilog2_exact(C) | (uint32_t)ilog2_exact(Wo) << 4 | (uint32_t)ilog2_exact(Ho) << 8 |
+                       (uint32_t)ilog2_exact(W) << 12 | (uint32_t)ilog2_exact(H) << 16 | (uint32_t)(s - 1) << 20 |
+                       (uint32_t)pt << 21 | (uint32_t)pl << 23 | (uint32_t)mode << 25;
+  return gemm2_run(4, InX{x, nullptr, nullptr, nullptr, 0}, GradX{}, Bt, bias, out, B * Ho * Wo, N, K, false,
+                   nullptr, (int)geo, st, partial, StatSink{}, gemm2_target_wgs(), GradSink{}, false);
+}
+
 // GradSink partial rows a dgrad GEMM of this shape writes (0: the sums cannot be fused: split-K)
 int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16) {
   if (gemm_impl_for(N, bf16) == 2) {

@@ -156,7 +156,9 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   const int sk = kstats ? 1 : gs ? 2 : 0;
   Gemm2Group<1> a{};
   a.n = 1;
-  a.a[0] = Gemm2Args{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1,
+  if (mode == 4 && (stats || gs)) throw std::runtime_error("gemm: the implicit im2col has no fused sinks");
+  // rpi: rows per image of the SE row scale (mode 2) or the packed gather geometry (mode 4, g2_geo)
+  a.a[0] = Gemm2Args{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, (mode == 2 || mode == 4) ? rows_per_img : 1,
                      p.kslice, p.splits > 1 ? partial : nullptr, sink, p.mtiles, gsk};
   dim3 g(p.gx, p.gy, p.splits);
   const int st = g2_storage(A, G, gsk);

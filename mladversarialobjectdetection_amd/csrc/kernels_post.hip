@@ -262,7 +262,8 @@ constexpr int kNmsTopWant = 960;  // a batch of ~1000 sorts at 1024 entries
 constexpr int kNmsTopMax = 4096;
 constexpr int kNmsHistBins = 4096;
 constexpr int kNmsRowBytes = 64 * (8 + 16 + 4);  // a re-queue row: keys | boxes | last-visit counts
-constexpr int kNmsSelBytes = PHX_MAX_OUT_DEV * 16 + (PHX_MAX_OUT_DEV * 4 + 15) / 16 * 16;
+constexpr int kNmsFl = 24;  // decay factors other than 1 kept per row candidate (its product's terms)
+constexpr int kNmsSelBytes = PHX_MAX_OUT_DEV * 16 + (PHX_MAX_OUT_DEV * 4 + 15) / 16 * 16 + kNmsFl * 64 * 4;
 
 static NmsPlan nms_plan(int N) {
   NmsPlan p;
@@ -285,32 +286,25 @@ static NmsPlan nms_plan(int N) {
   return p;
 }
 
-// Wave-wide max of a 64-bit key, on the queue's critical path (a dependent chain per pop): within
-// each 16-lane row by DPP moves (quad xor 1, xor 2, half-row mirror, row mirror — VALU latency), then
-// the four row maxima by readlane (scalar).  A shuffle (ds_bpermute) per step cost ~6x as much.
-template <int CTRL>
-__device__ __forceinline__ void dpp_max_step(uint32_t& hi, uint32_t& lo) {
-  const uint32_t oh = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xf, 0xf, false);
-  const uint32_t ol = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xf, 0xf, false);
-  const bool gt = oh > hi || (oh == hi && ol > lo);
-  hi = gt ? oh : hi;
-  lo = gt ? ol : lo;
+// Wave-wide max of a 64-bit key, on the queue's critical path (a dependent chain per pop): the max
+// of the high words, then of the low words among the lanes holding it — each within 16-lane rows by
+// DPP (quad xor 1, xor 2, half-row mirror, row mirror: one v_max with a DPP operand per step), the
+// four row maxima by readlane.  A shuffle (ds_bpermute) per step cost ~6x as much.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));   // quad_perm [1,0,3,2]
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));   // quad_perm [2,3,0,1]
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+  const uint32_t a = max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16));
+  const uint32_t c = max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48));
+  return max(a, c);
 }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
-  uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
-  dpp_max_step<0xB1>(hi, lo);   // quad_perm [1,0,3,2]
-  dpp_max_step<0x4E>(hi, lo);   // quad_perm [2,3,0,1]
-  dpp_max_step<0x141>(hi, lo);  // row_half_mirror
-  dpp_max_step<0x140>(hi, lo);  // row_mirror
-  uint64_t m = 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const uint64_t w = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 16 * r) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)lo, 16 * r);
-    m = w > m ? w : m;
-  }
-  return m;
+  const uint32_t hi = (uint32_t)(v >> 32), lo = (uint32_t)v;
+  const uint32_t mh = wave_max_u32(hi);
+  const uint32_t ml = wave_max_u32(hi == mh ? lo : 0u);
+  return ((uint64_t)mh << 32) | ml;
 }
 
 // sc = orig * f(newest) * f(next) * ... in that order (lane l holds the factor of selection
@@ -390,6 +384,11 @@ __device__ __forceinline__ NmsNBox nms_norm(float4 b) {
   return n;
 }
 
+__device__ __forceinline__ NmsNBox nms_sel_at(const float4* s_seln, const float* s_sela, int k) {
+  const float4 v = s_seln[k];
+  return NmsNBox{v.x, v.y, v.z, v.w, s_sela[k]};
+}
+
 // whether candidate c and selection s intersect; when not, their decay factor is exactly 1
 __device__ __forceinline__ bool nms_overlap(const NmsNBox& c, const NmsNBox& s) {
   return fminf(c.y1, s.y1) > fmaxf(c.y0, s.y0) && fminf(c.x1, s.x1) > fmaxf(c.x0, s.x0);
@@ -404,6 +403,23 @@ __device__ __forceinline__ float nms_factor(const NmsNBox& c, const NmsNBox& s, 
   return expf(scale * sim * sim);
 }
 
+// nms_visit on the normalised selections: the factors of the selections that do not intersect the
+// candidate are exactly 1 and skipped without the division and exponential
+__device__ __forceinline__ float nms_visit_n(const NmsNBox& cn, float orig, int from, int nsel, const float4* s_seln,
+                                             const float* s_sela, float scale, int lane) {
+  const int nf = nsel - from;
+  float f0 = 1.f, f1 = 1.f;
+  if (lane < nf) {
+    const NmsNBox sn = nms_sel_at(s_seln, s_sela, nsel - 1 - lane);
+    if (nms_overlap(cn, sn)) f0 = nms_factor(cn, sn, scale);
+  }
+  if (lane + 64 < nf) {
+    const NmsNBox sn = nms_sel_at(s_seln, s_sela, nsel - 65 - lane);
+    if (nms_overlap(cn, sn)) f1 = nms_factor(cn, sn, scale);
+  }
+  return decay_chain(orig, f0, f1);
+}
+
 __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     const float* __restrict__ boxes, const float* __restrict__ scores,
     const uint8_t* __restrict__ keep, int keep_mask, const int* __restrict__ count, int N,
@@ -413,7 +429,9 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     NmsCand cand, NmsPlan pl, int dbg) {
   extern __shared__ __attribute__((aligned(16))) unsigned char nms_smem[];
   const int b = blockIdx.x;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // wave: readfirstlane makes it (and everything decided in wave 0's queue loop) uniform to the
+  // compiler, so the loop's state lives in scalar registers and its branches are scalar
+  const int t = threadIdx.x, lane = t & 63, wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const float* bb = boxes + (long)b * N * 4;
   const float* sb = scores + (long)b * N;
   float4* cbox = cbox_all + (long)b * N;
@@ -432,6 +450,9 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
   uint8_t* s_wb = reinterpret_cast<uint8_t*>(s_key + pl.cap);
   const int cap = pl.cap;
 
+  // PHX_NMS_STATS: phase times (100 MHz realtime clock; stamps only when dbg)
+  auto stamp = [&]() -> uint64_t { return dbg ? __builtin_amdgcn_s_memrealtime() : 0ull; };
+  const uint64_t ts0 = stamp();
   // 1. bitmap of the candidate anchors (or count-prefix positions)
   const int nbits = N;
   const int nwords = (nbits + 63) / 64 * 2;
@@ -498,7 +519,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
       }
     }
   }
-  const int n = s_scan[kNmsThreads - 1];
+  const int n = __builtin_amdgcn_readfirstlane(s_scan[kNmsThreads - 1]);
   __syncthreads();  // gwi complete (global writes of this workgroup, visible after the barrier)
 
   // ---- fast path -------------------------------------------------------------------------
@@ -516,6 +537,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     float4* lbox = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(lpay) + pl.lp * 4);  // [lp]
     float4* s_seln = lbox + pl.lp;                                           // [PHX_MAX_OUT_DEV]
     float* s_sela = reinterpret_cast<float*>(s_seln + PHX_MAX_OUT_DEV);      // [PHX_MAX_OUT_DEV]
+    float* flist = s_sela + (PHX_MAX_OUT_DEV + 3) / 4 * 4;                     // [kNmsFl][64]
     unsigned char* qbase = reinterpret_cast<unsigned char*>(s_seln) + kNmsSelBytes;
     uint64_t* qkey = reinterpret_cast<uint64_t*>(qbase);                     // [qrows][64]
     float4* qbox = reinterpret_cast<float4*>(qkey + pl.qrows * 64);           // [qrows][64]
@@ -539,7 +561,10 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
     int nsel = 0;
     uint64_t rmax = 0ull, cmax = 0ull;
     int crow = 0;
-    int npop = 0, nrq = 0, nbatch = 0;  // PHX_NMS_STATS counts
+    int npop = 0, nrq = 0, nbatch = 0;  // PHX_NMS_STATS counts and phase times
+    int ndirty = 0;
+    uint64_t tsel = 0, tlist = 0, tsort = 0, tpop = 0, tsa = stamp();
+    const uint64_t ts1 = tsa;
     uint32_t hi = 0xffffffffu;  // candidates with score bits < hi are not listed yet
     int rem = n;                // how many
     int state = 0;              // 0 next batch, 1 done, 2 fall back
@@ -589,14 +614,16 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
             s_misc[5] = need - (acc - (int)hist[bin]);  // still needed inside the crossing bin
           }
           __syncthreads();
-          const uint32_t bin = (uint32_t)s_misc[4];
-          need = s_misc[5];
+          const uint32_t bin = (uint32_t)__builtin_amdgcn_readfirstlane(s_misc[4]);
+          need = __builtin_amdgcn_readfirstlane(s_misc[5]);
           prefix = pass == 0 ? bin : ((prefix << 12) | bin);
           __syncthreads();
         }
         thr24 = prefix;
       }
       const uint32_t lo = thr24 << 8;  // unlisted after this batch: score bits < lo
+      uint64_t tsb = stamp();
+      tsel += tsb - tsa;
       // F3. the batch's keys and boxes (any order; the sort below orders them by queue key)
       if (t == 0) s_misc[6] = 0;
       __syncthreads();
@@ -617,13 +644,15 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
         }
       }
       __syncthreads();
-      const int L = s_misc[6];
+      const int L = __builtin_amdgcn_readfirstlane(s_misc[6]);
       if (L > pl.lp) {
         state = 2;
         break;
       }
       rem -= L;
       ++nbatch;
+      tsa = stamp();
+      tlist += tsa - tsb;
       int ls = 1;  // sort size: the batch rounded up to a power of 2
       while (ls < L) ls <<= 1;
       for (int j = t; j < ls; j += kNmsThreads) {
@@ -652,19 +681,40 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
         }
       }
       // F4. the lazy queue over the batch's rows + the re-queue set, wave 0 alone
+      tsb = stamp();
+      tsort += tsb - tsa;
       if (wave == 0) {
         int f = 0, st = 1;
         int rown = 0, jn = 0;       // the row's candidates, the next one not popped yet
         uint64_t ck = 0ull;         // lane j: the row's j-th candidate's key
         float4 cbx = make_float4(0.f, 0.f, 0.f, 0.f);  // its box
         NmsNBox cn = nms_norm(cbx);
-        float cs = 0.f;             // its score after the row-wide visit
-        bool dirty = false;         // a selection since that visit overlaps it
+        float cs = 0.f;             // its score: the product over every selection so far
+        int fc = 0;                 // its decay factors other than 1 (flist[0..fc), oldest first)
+        bool dirty = false;         // more than kNmsFl of them: a full visit at its pop
         uint64_t rk = 0ull;         // its re-queue key once popped (0: not in the queue)
         int rfrom = 0;              // selections at that pop
         uint64_t qmax = 0ull;       // max of rk
-        // a new selection: lane 0 records it; the row's candidates not popped yet (lanes >= j0)
-        // that it overlaps with a decay factor other than 1 need a fresh visit
+        // TF's product of a row candidate: its score times its factors, newest first (factors of
+        // exactly 1 leave it unchanged and are not kept)
+        auto product = [&](bool on) {
+          if (on) {
+            float sc = __uint_as_float((uint32_t)(ck >> 32));
+            for (int q = min(fc, kNmsFl) - 1; q >= 0; --q) sc *= flist[q * 64 + lane];
+            cs = sc;
+          }
+        };
+        // a factor other than 1 of a new selection for the lanes `on`: appended, the product redone
+        auto add_factor = [&](bool on, float g) {
+          if (on) {
+            if (fc < kNmsFl) flist[fc * 64 + lane] = g;
+            else dirty = true;
+            ++fc;
+          }
+          product(on && !dirty);
+        };
+        // a new selection: lane 0 records it; the row's candidates not popped yet (lanes >= j0) take
+        // its decay factor into their product
         auto select = [&](float4 b4, float sc, int j0) {
           const NmsNBox sn = nms_norm(b4);
           if (lane == 0) {
@@ -676,7 +726,8 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
           ++nsel;
           const bool ov = lane >= j0 && lane < rown && nms_overlap(cn, sn);
           if (__ballot(ov)) {
-            if (ov && nms_factor(cn, sn, scale) != 1.f) dirty = true;
+            const float g = ov ? nms_factor(cn, sn, scale) : 1.f;
+            if (__ballot(g != 1.f)) add_factor(g != 1.f, g);
           }
         };
         while (nsel < max_out) {
@@ -705,16 +756,21 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
               f += rown;
               jn = 0;
               dirty = false;
-              float sc = __uint_as_float((uint32_t)(ck >> 32));
-              for (int k = nsel - 1; k >= 0; --k) {
-                const float4 s4 = s_seln[k];
-                const NmsNBox sn{s4.x, s4.y, s4.z, s4.w, s_sela[k]};
+              fc = 0;
+              // the factors other than 1, oldest selection first, then the product newest first
+              for (int k = 0; k < nsel; ++k) {
+                const NmsNBox sn = nms_sel_at(s_seln, s_sela, k);
                 const bool ov = lane < rown && nms_overlap(cn, sn);
                 if (__ballot(ov)) {
-                  if (ov) sc *= nms_factor(cn, sn, scale);
+                  const float g = ov ? nms_factor(cn, sn, scale) : 1.f;
+                  if (g != 1.f) {
+                    if (fc < kNmsFl) flist[fc * 64 + lane] = g;
+                    else dirty = true;
+                    ++fc;
+                  }
                 }
               }
-              cs = sc;
+              product(!dirty);
             }
           }
           const uint64_t fk = jn < rown ? readlane_u64(ck, jn) : 0ull;
@@ -743,7 +799,7 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
               from = qfrom[crow * 64 + owner];
               b4 = qbox[crow * 64 + owner];
             }
-            const float sc = nms_visit(b4, orig, from, nsel, s_sel, scale, lane);
+            const float sc = nms_visit_n(nms_norm(b4), orig, from, nsel, s_seln, s_sela, scale, lane);
             uint64_t nk = 0ull;
             if (sc == orig) select(b4, sc, jn);
             else if (sc > score_thresh) nk = nms_key(__float_as_uint(sc), pos);
@@ -768,8 +824,10 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
             // the row's next candidate: its row-wide visit holds unless a later selection overlaps it
             const int j = jn++;
             float sc;
-            if ((__ballot(dirty) >> j) & 1ull) sc = nms_visit(readlane_f4(cbx, j), orig, 0, nsel, s_sel, scale, lane);
-            else sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), j));
+            if ((__ballot(dirty) >> j) & 1ull) {
+              sc = nms_visit_n(nms_norm(readlane_f4(cbx, j)), orig, 0, nsel, s_seln, s_sela, scale, lane);
+              ++ndirty;
+            } else sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cs), j));
             if (sc == orig) {
               select(readlane_f4(cbx, j), sc, jn);
             } else if (sc > score_thresh) {
@@ -788,13 +846,18 @@ __global__ __launch_bounds__(kNmsThreads) void k_soft_nms(
         }
       }
       __syncthreads();
-      state = s_misc[2];  // workgroup-uniform
+      state = __builtin_amdgcn_readfirstlane(s_misc[2]);  // workgroup-uniform
       hi = lo;
+      tsa = stamp();
+      tpop += tsa - tsb;
       __syncthreads();    // the next batch rewrites the list
     }
     if (dbg && t == 0)
-      printf("nms image %d: %d candidates, %d batch(es), %d pops (%d re-queued), %d selected -> %s\n", b, n,
-             nbatch, npop, nrq, s_misc[1], state == 1 ? "fast path" : "general queue");
+      printf("nms image %d: %d candidates, %d batch(es), %d pops (%d re-queued), %d selected -> %s | us: "
+             "compaction + scores %.1f, batch select %.1f list %.1f sort %.1f, pops %.1f; %d full visits of row "
+             "candidates\n", b, n, nbatch, npop,
+             nrq, s_misc[1], state == 1 ? "fast path" : "general queue", (ts1 - ts0) * 0.01, tsel * 0.01,
+             tlist * 0.01, tsort * 0.01, tpop * 0.01, ndirty);
     fast_done = state == 1;
   }
   if (!fast_done) {

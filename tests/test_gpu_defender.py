@@ -177,6 +177,27 @@ def test_train_step_deterministic(victim):
     assert out[0][1] == out[1][1]
 
 
+def test_unet_implicit_im2col_matches_column_matrix(victim, monkeypatch):
+    """The U-Net's wide 3x3 convs (more than 32 outputs or K > 288: the 64- and 128-channel levels,
+    their data gradients, the transposed convs and theirs) gather the column matrix inside the GEMM
+    (k_gemm2 MODE 4, no column matrix in HBM); PHX_UN_GATHER=0 writes it with k_im2col and runs the
+    GEMM over it.  The products and their order are the same, so two training steps are bit-identical
+    (variables and loss)."""
+    from mladversarialobjectdetection_amd.defender import PatchAttackDefender
+    imgs = torch.as_tensor(_images(6)).cuda()
+    out = []
+    for g in ("1", "0"):
+        monkeypatch.setenv("PHX_UN_GATHER", g)
+        d = PatchAttackDefender(victim, seed=11)
+        for _ in range(2):
+            d.train_step(imgs)
+        torch.cuda.synchronize()
+        out.append((d.params.cpu().numpy().copy(), float(d.loss_buf.item())))
+    assert np.isfinite(out[0][1])
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+
+
 def test_eval_step_matches_oracle(victim):
     """PatchAttackDefender.call(training=False) / test_step (attack_detection.py:168-198, 320-326):
     the Masker's evaluation branch pastes the attacker's patch (print, brightness match, centred
