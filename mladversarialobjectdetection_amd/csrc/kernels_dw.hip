@@ -36,10 +36,6 @@ struct DwGeom {
   int otw, oth;     // tile (in the space of the tensor this launch writes)
   int nrg;          // row groups per block
   int rin, cin;     // staged window
-  int cp, ne;       // LDS pixels per staged row; ne > 0: columns de-interleaved (stride-2 forwards:
-                    // the even window columns first, the odd ones from position ne, so the lanes of a
-                    // tap — every other column — read consecutive 16-B slots instead of two lanes per
-                    // slot); ne = 0: in order (cp = cin)
   int tiles_x, ntiles, ncg;
   int per;          // work items per XCD
 };
@@ -250,23 +246,20 @@ __device__ __forceinline__ void dw_stage_t(float4* tile, const Src& src, int b, 
   for (; p < npx; p += U * pstep) {
     typename Src::Raw v[U];
     bool ok[U];
-    int at[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int pp = p + u * pstep;
       const int prow = pp / g.cin, pcol = pp - prow * g.cin;
-      const int pos = prow * g.cp + (g.ne ? ((pcol & 1) ? g.ne + (pcol >> 1) : (pcol >> 1)) : pcol);
       const int iy = r0 + prow, ix = c0 + pcol;
       ok[u] = pp < npx && iy >= 0 && iy < sh && ix >= 0 && ix < sw;
       const int iyc = min(max(iy, 0), sh - 1), ixc = min(max(ix, 0), sw - 1);
       v[u] = src.load((((long)b * sh + iyc) * sw + ixc) * C + chan);
-      at[u] = pos;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int pp = p + u * pstep;
       if (pp < npx)
-        tile[(at[u] << g.lcg) + ecg] = ok[u] ? src.template finish_t<ACT>(v[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
+        tile[(pp << g.lcg) + ecg] = ok[u] ? src.template finish_t<ACT>(v[u]) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
 }
@@ -368,7 +361,7 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
 
   Stage src;
   src.init(xv, c);
-  float4* wt = tile + g.rin * g.cp * CG;
+  float4* wt = tile + g.rin * g.cin * CG;
   Taps<K> wr;
   wr.stage(wt, w, g.C, cgi, g.lcg);
   dw_stage<Stage, SU>(tile, src, b, g.H, g.W, g.C, oy0 * S - g.pt, ox0 * S - g.pl, c, g);
@@ -384,14 +377,12 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
   if (active) {
     wr.init(wt, w, g.C, c, cg, g.lcg);
     constexpr int NR = (RPT - 1) * S + K;
-    // window column col*S + j at position col*S + j, or (de-interleaved) col + j/2 (+ ne if j odd)
-    const float4* base = tile + ((row0 * S) * g.cp + (g.ne ? col : col * S)) * CG + cg;
+    const float4* base = tile + ((row0 * S) * g.cin + col * S) * CG + cg;
 #pragma unroll
     for (int ir = 0; ir < NR; ++ir) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
-        const int jp = g.ne ? ((j & 1) ? g.ne + (j >> 1) : (j >> 1)) : j;
-        const float4 v = base[(ir * g.cp + jp) * CG];
+        const float4 v = base[(ir * g.cin + j) * CG];
 #pragma unroll
         for (int r = 0; r < RPT; ++r) {
           const int i = ir - r * S;
@@ -472,7 +463,7 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
 
   StageGradX<YBF> src;
   src.init(gv, c);
-  float4* wt = tile + g.rin * g.cp * CG;
+  float4* wt = tile + g.rin * g.cin * CG;
   Taps<K> wr;
   wr.stage(wt, w, g.C, cgi, g.lcg);
   dw_stage<StageGradX<YBF>, SU>(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
@@ -596,15 +587,6 @@ static int dw_lcg(int C, int k, int s, bool bwd) {
   return std::min(l, cap);
 }
 
-// stride-2 forwards stage their window columns de-interleaved (PHX_DW_DEINT=0: in order)
-static bool dw_deinterleave() {
-  static const bool v = [] {
-    const char* e = std::getenv("PHX_DW_DEINT");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
 // tile over an output space of (oh x ow) written by this launch
 static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k, int s, int rpt,
                       bool bwd) {
@@ -629,16 +611,6 @@ static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k
       g.cin = g.otw + k - 1;
     }
   }
-  g.cp = g.cin;
-  g.ne = 0;
-  if (!bwd && s == 2 && dw_deinterleave()) {
-    // the odd columns start at a position ne with ne * CG = 8 (mod 16): the staging stores of two
-    // neighbouring window columns (one even, one odd) then land in different halves of the banks too
-    const int CG = 1 << g.lcg;
-    g.ne = (g.cin + 1) / 2;
-    while ((g.ne * CG) % 16 != 8) ++g.ne;
-    g.cp = g.ne + g.cin / 2;
-  }
   g.tiles_x = cdiv(ow, g.otw);
   g.ntiles = g.tiles_x * cdiv(oh, g.oth);
   g.ncg = C / (4 << g.lcg);
@@ -648,7 +620,7 @@ static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k
 
 static size_t dw_lds(const DwGeom& g, int k) {
   const bool lds_taps = PHX_DW_LDS_TAPS == 2 || (PHX_DW_LDS_TAPS == 1 && k > 3);
-  return ((size_t)g.rin * g.cp + (lds_taps ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
+  return ((size_t)g.rin * g.cin + (lds_taps ? k * k : 0)) * (1 << g.lcg) * sizeof(float4);
 }
 
 static bool xv_bf(const InX& x) { return x.bf != 0; }
