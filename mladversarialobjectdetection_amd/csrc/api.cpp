@@ -957,10 +957,11 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
         segs[r] = GemmSeg{view(ctx, E, op.in[0], input), GradX{}, op.b >= 0 ? W + op.b : nullptr,
                           E.tptr(op.out, input), (int)P.tensors[op.in[0]].rows(), false, sink_of(r), GradSink{}};
       }
-      const int np = gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s, E.bf16);
+      int np[kMaxSeg];  // each member's statistics partial rows
+      gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s, E.bf16, np);
       if (sink_on)
         for (int r = 0; r < n; ++r) {
-          E.stat_P[P.ops[g[r]].out] = np;
+          E.stat_P[P.ops[g[r]].out] = np[r];
           E.stat_region[P.ops[g[r]].out] = r;
         }
       break;
@@ -1053,10 +1054,11 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                           (int)P.tensors[op.in[0]].rows(), op.acc[0], StatSink{}, gsk_of(r)};
       }
       // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
-      const int np = gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s, E.bf16);
+      int np[kMaxSeg];  // each member's BN-backward-sum partial rows
+      gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s, E.bf16, np);
       if (gs_on)
         for (int r = 0; r < n; ++r) {
-          E.gstat_P[g[r] - 1] = np;
+          E.gstat_P[g[r] - 1] = np[r];
           E.gstat_region[g[r] - 1] = r;
         }
       break;

@@ -578,6 +578,358 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
   }
 }
 
+// ---- A-resident variant (k_gemm2r) ---------------------------------------------------------
+// The workgroup's M tile of A' — its view (BN + activation, SE scale, BN backward) applied once per
+// element — stays in LDS chunk by chunk while the workgroup sweeps every N tile over it, instead of
+// each N tile re-loading A and re-applying the view (exp / rcp per element, which serialises with the
+// fp32 MFMAs and dominates the bf16 ones).  Grid (gx, 1, segments), persistent along M; B chunks
+// double-buffered behind the resident A tile (dynamic LDS: ksteps * BM * BK + 2 * BN * BK elements).
+// One pipeline over the (M tile, N tile, k chunk) steps: the loads of step s+1 (A only while the
+// first N tile of an M tile is swept) are in flight while step s multiplies.  The statistics /
+// BN-backward sums go out per (M tile, wave row): partial row tile * WM + wm of the sink (no
+// cross-wave merge; the finalize folds them in a fixed order).  No split-K; ksteps >= 2 (the next M
+// tile's chunk 0 is written while the last chunk is read).  Few M tiles: blockIdx.y splits the N
+// tiles into runs of Gemm2Args::kslice (unused without split-K) N tiles, one run per workgroup.
+template <class P>
+__device__ __forceinline__ void g2r_put(char* base, int row, int k, float4 v) {
+  char* p = base + (size_t)g2_off<P>(row, k) * P::ESZ;
+  if constexpr (P::ESZ == 2) *reinterpret_cast<uint2*>(p) = pack_bf16x4(v);
+  else *reinterpret_cast<float4*>(p) = v;
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF, int ST>
+__device__ __forceinline__ void g2r_load_a(G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, int m0, int k0) {
+  using P = G2<WM, TM, TN, MODE, BF>;
+  const int t = threadIdx.x;
+  const int kk = k0 + 4 * (t % P::KQ);
+  const int kc = kk < a.K ? kk : a.K - 4;
+  if (MODE == 1 || MODE == 2) r.ck = inx_chan4(a.A, kc);
+  if (MODE == 3) r.gk = gx_chan4(a.G, kc);
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) {
+    const int row = min(m0 + (t + 256 * u) / P::KQ, a.M - 1);
+    const long e = (long)row * a.K + kc;
+    if (MODE == 3) {
+      r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
+      r.y[u] = ald4<ST == 2>(a.G.y, e);
+    } else {
+      r.a[u] = ald4<ST == 1>(a.A.p, e);
+      if (MODE == 2) r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(row / a.rpi) * a.K + kc);
+    }
+  }
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2r_load_b(G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, int n0, int k0) {
+  using P = G2<WM, TM, TN, MODE, BF>;
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) {
+    const int idx = threadIdx.x + 256 * u;
+    const int kb = k0 + 4 * (idx % P::KQ);
+    r.b[u] = *reinterpret_cast<const float4*>(a.Bt + (long)min(n0 + idx / P::KQ, a.N - 1) * a.K +
+                                              (kb < a.K ? kb : a.K - 4));
+  }
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF, int ACT>
+__device__ __forceinline__ void g2r_store_a_act(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, char* base,
+                                                int m0, int k0) {
+  using P = G2<WM, TM, TN, MODE, BF>;
+  const int t = threadIdx.x;
+  const int c4 = t % P::KQ;
+  const bool kok = k0 + 4 * c4 < a.K;
+  InX ax = a.A;
+  ax.act = ACT;
+  GradX gx = a.G;
+  gx.act = ACT;
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) {
+    if (t + 256 * u >= P::BM * P::KQ) continue;
+    const int rl = (t + 256 * u) / P::KQ;
+    float4 v = r.a[u];
+    if (kok && m0 + rl < a.M) {
+      if (MODE == 1 || MODE == 2) v = inx_apply4(ax, r.ck, v);
+      if (MODE == 2) {
+        v.x *= r.rs[u].x; v.y *= r.rs[u].y; v.z *= r.rs[u].z; v.w *= r.rs[u].w;
+      }
+      if (MODE == 3) v = gx_apply4(gx, r.gk, v, r.y[u]);
+    } else {
+      v = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    g2r_put<P>(base, rl, 4 * c4, v);
+  }
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2r_store_a(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, char* base,
+                                            int m0, int k0) {
+  const int act = MODE == 0 ? 0 : MODE == 3 ? a.G.act : a.A.act;
+  if (act == 1) g2r_store_a_act<WM, TM, TN, MODE, BF, 1>(r, a, base, m0, k0);
+  else if (act == 2) g2r_store_a_act<WM, TM, TN, MODE, BF, 2>(r, a, base, m0, k0);
+  else g2r_store_a_act<WM, TM, TN, MODE, BF, 0>(r, a, base, m0, k0);
+}
+
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2r_store_b(const G2Regs<WM, TM, TN, MODE, BF>& r, const Gemm2Args& a, char* base,
+                                            int n0, int k0) {
+  using P = G2<WM, TM, TN, MODE, BF>;
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) {
+    const int idx = threadIdx.x + 256 * u;
+    if (idx < P::BN * P::KQ) {
+      const bool ok = n0 + idx / P::KQ < a.N && k0 + 4 * (idx % P::KQ) < a.K;
+      g2r_put<P>(base, idx / P::KQ, 4 * (idx % P::KQ), ok ? r.b[u] : make_float4(0.f, 0.f, 0.f, 0.f));
+    }
+  }
+}
+
+// dynamic LDS bytes of k_gemm2r for K
+template <int WM, int TM, int TN, bool BF>
+constexpr size_t g2r_lds_bytes(int K) {
+  using P = G2<WM, TM, TN, 1, BF>;
+  return ((size_t)((K + P::BK - 1) / P::BK) * P::BM + 2 * P::BN) * P::LD * P::ESZ;
+}
+
+template <int WM, int TM, int TN, int MODE, int SK, int NS, bool BF, int ST>
+__global__ __launch_bounds__(256, 2) void k_gemm2r(Gemm2Group<NS> grp) {
+  constexpr bool CBF = ST == 1;
+  const Gemm2Args a = pick_seg(grp.a, NS == 1 ? 0 : (int)blockIdx.z);
+  using P = G2<WM, TM, TN, MODE, BF>;
+  constexpr int BM = P::BM, BN = P::BN, BK = P::BK;
+  constexpr size_t ACH = (size_t)BM * P::LD * P::ESZ, BCH = (size_t)BN * P::LD * P::ESZ;
+  extern __shared__ __attribute__((aligned(16))) float g2r_sm[];
+  const int ksteps = (a.K + BK - 1) / BK;
+  const int nt0 = (int)blockIdx.y * a.kslice;                        // this workgroup's N tiles
+  const int nte = min((a.N + BN - 1) / BN, nt0 + a.kslice);
+  char* const Ares = reinterpret_cast<char*>(g2r_sm);
+  char* const Bb = Ares + (size_t)ksteps * ACH;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int r32 = lane & 31, h = lane >> 5;
+  int tile = blockIdx.x;
+  if (tile >= a.mtiles || nt0 >= nte) return;  // workgroup-uniform, before any barrier
+  G2Regs<WM, TM, TN, MODE, BF> rg;
+  g2r_load_a<WM, TM, TN, MODE, BF, ST>(rg, a, tile * BM, 0);
+  g2r_load_b(rg, a, nt0 * BN, 0);
+  g2r_store_a(rg, a, Ares, tile * BM, 0);
+  g2r_store_b(rg, a, Bb, nt0 * BN, 0);
+  int buf = 0, nt = nt0, kc = 0;
+  auto advance = [&](int t, int n, int k, int& t2, int& n2, int& k2) {
+    t2 = t;
+    n2 = n;
+    k2 = k + 1;
+    if (k2 == ksteps) {
+      k2 = 0;
+      if (++n2 == nte) {
+        n2 = nt0;
+        t2 = t + gridDim.x;
+      }
+    }
+  };
+  // the loads of step (tl, nl, kl) into R (A only on the first N tile of a run)
+  auto load = [&](G2Regs<WM, TM, TN, MODE, BF>& R, int tl, int nl, int kl) {
+    if (nl == nt0) g2r_load_a<WM, TM, TN, MODE, BF, ST>(R, a, tl * BM, kl * BK);
+    g2r_load_b(R, a, nl * BN, kl * BK);
+  };
+  int t1, n1, k1;
+  advance(tile, nt0, 0, t1, n1, k1);
+  bool h1 = t1 < a.mtiles;
+  auto load_bias = [&](float (&bv)[TN], int n0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bv[j] = a.bias ? a.bias[min(n0 + wn * TN * 32 + j * 32 + r32, a.N - 1)] : 0.f;
+  };
+  float bias[TN];
+  load_bias(bias, nt0 * BN);
+  __syncthreads();
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  // one pipeline step: the loads of the next step go out first (unconditionally: past the end a
+  // step re-loads its own chunk), then this step's MFMAs (and epilogue), then the next chunk's store.
+  // (A two-deep register prefetch measured no faster on C2 / C4: 28.60 vs 28.56 ms on C4.)
+  auto step = [&]() -> bool {
+    load(rg, h1 ? t1 : tile, h1 ? n1 : nt, h1 ? k1 : kc);
+    __builtin_amdgcn_sched_barrier(0);
+      // MFMAs: A chunk kc of the resident tile, B chunk of buffer buf
+      {
+        char* const Ab = Ares + (size_t)kc * ACH;
+        char* const Bc = Bb + (size_t)buf * BCH;
+        if constexpr (BF) {
+  #pragma unroll
+          for (int kk = 0; kk < BK / 16; ++kk) {
+            bf16x8_t fa[TM], fb[TN];
+  #pragma unroll
+            for (int i = 0; i < TM; ++i)
+              fa[i] = *reinterpret_cast<const bf16x8_t*>(Ab + (size_t)g2_off<P>(wm * TM * 32 + i * 32 + r32, 16 * kk + 8 * h) * 2);
+  #pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fb[j] = *reinterpret_cast<const bf16x8_t*>(Bc + (size_t)g2_off<P>(wn * TN * 32 + j * 32 + r32, 16 * kk + 8 * h) * 2);
+  #pragma unroll
+            for (int i = 0; i < TM; ++i)
+  #pragma unroll
+              for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          }
+        } else {
+          const float* As = reinterpret_cast<const float*>(Ab);
+          const float* Bs = reinterpret_cast<const float*>(Bc);
+          const int kvalid = a.K - kc * BK;
+  #pragma unroll
+          for (int s8 = 0; s8 < BK / 8; ++s8) {
+            if (s8 > 0 && 8 * s8 >= kvalid) break;  // wave-uniform
+            float4 fa[TM], fb[TN];
+  #pragma unroll
+            for (int i = 0; i < TM; ++i)
+              fa[i] = *reinterpret_cast<const float4*>(As + g2_off<P>(wm * TM * 32 + i * 32 + r32, 8 * s8 + 4 * h));
+  #pragma unroll
+            for (int j = 0; j < TN; ++j)
+              fb[j] = *reinterpret_cast<const float4*>(Bs + g2_off<P>(wn * TN * 32 + j * 32 + r32, 8 * s8 + 4 * h));
+  #pragma unroll
+            for (int i = 0; i < TM; ++i)
+  #pragma unroll
+              for (int j = 0; j < TN; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].x, fb[j].x, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].y, fb[j].y, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].z, fb[j].z, acc[i][j], 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i].w, fb[j].w, acc[i][j], 0, 0, 0);
+              }
+          }
+        }
+      }
+      if (kc == ksteps - 1) {
+        // ---- epilogue of (tile, nt): lane (r32, h) holds column r32, rows (e&3) + 8*(e>>2) + 4*h ----
+        const int mrow0 = tile * BM + wm * TM * 32;
+        const int ncol0 = nt * BN + wn * TN * 32;
+        const bool full = mrow0 + TM * 32 <= a.M && ncol0 + TN * 32 <= a.N;
+        const bool accum = a.acc != 0;
+  #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int col = ncol0 + j * 32 + r32;
+          const bool cok = col < a.N;
+          const float bv = bias[j];
+  #pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            if (full) {
+              const long cbase = (long)(mrow0 + i * 32 + 4 * h) * a.N + col;
+              float old[16];
+              if (accum) {
+  #pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                  const long ce = cbase + (long)((e & 3) + 8 * (e >> 2)) * a.N;
+                  old[e] = CBF ? ald1<true>(a.C, ce) : a.C[ce];
+                }
+              }
+  #pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                float v = acc[i][j][e] + bv;
+                acc[i][j][e] = v;
+                if (accum) v += old[e];
+                const long ce = cbase + (long)((e & 3) + 8 * (e >> 2)) * a.N;
+                if (CBF) ast1<true>(a.C, ce, v);
+                else a.C[ce] = v;
+                if (SK == 2) acc[i][j][e] = v;
+                if (CBF && SK == 1) acc[i][j][e] = round_bf16(v);  // statistics of the stored values
+              }
+            } else {
+  #pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                float v = acc[i][j][e] + bv;
+                acc[i][j][e] = v;
+                if (cok && row < a.M) {
+                  const long ce = (long)row * a.N + col;
+                  if (accum) v += CBF ? ald1<true>(a.C, ce) : a.C[ce];
+                  if (CBF) ast1<true>(a.C, ce, v);
+                  else a.C[ce] = v;
+                  if (SK == 2) acc[i][j][e] = v;
+                }
+                if (CBF && SK == 1) acc[i][j][e] = round_bf16(v);
+              }
+            }
+          }
+        }
+        const long prow = (long)tile * WM + wm;  // this wave's partial row of the sink
+        if constexpr (SK == 1) {
+          const float nw = (float)max(0, min(TM * 32, a.M - mrow0));
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            float s = 0.f;
+  #pragma unroll
+            for (int i = 0; i < TM; ++i)
+  #pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (full || mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) s += acc[i][j][e];
+            s += __shfl_xor(s, 32);
+            const float mean = nw > 0.f ? s / nw : 0.f;
+            float q = 0.f;
+  #pragma unroll
+            for (int i = 0; i < TM; ++i)
+  #pragma unroll
+              for (int e = 0; e < 16; ++e)
+                if (full || mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) {
+                  const float d = acc[i][j][e] - mean;
+                  q = fmaf(d, d, q);
+                }
+            q += __shfl_xor(q, 32);
+            const int col = ncol0 + j * 32 + r32;
+            if (h == 0 && col < a.N) sink_put(a.sink, prow, col, nw, mean, q);
+          }
+          if (nt == nt0 && blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[prow] = nw;
+        }
+        if constexpr (SK == 2) {
+  #pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int col = ncol0 + j * 32 + r32;
+            const int cc = min(col, a.N - 1);
+            const float mu = a.gsk.mu[cc], rs = a.gsk.rstd[cc], sc = a.gsk.sc[cc], be = a.gsk.be[cc];
+            float s1 = 0.f, s2 = 0.f;
+  #pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              float yv[16];
+  #pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                const int row = min(mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h, a.M - 1);
+                yv[e] = ald1<ST == 2>(a.gsk.y, (long)row * a.N + cc);
+              }
+  #pragma unroll
+              for (int e = 0; e < 16; ++e) {
+                const int row = mrow0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                if (col < a.N && row < a.M) gs_one(acc[i][j][e], yv[e], mu, rs, sc, be, a.gsk.act, s1, s2);
+              }
+            }
+            s1 += __shfl_xor(s1, 32);
+            s2 += __shfl_xor(s2, 32);
+            if (h == 0 && col < a.N) gsink_put(a.gsk, prow, col, s1, s2);
+          }
+        }
+  #pragma unroll
+        for (int i = 0; i < TM; ++i)
+  #pragma unroll
+          for (int j = 0; j < TN; ++j)
+  #pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+      }
+    if (!h1) return false;
+    if (n1 == nt0) g2r_store_a(rg, a, Ares + (size_t)k1 * ACH, t1 * BM, k1 * BK);
+    g2r_store_b(rg, a, Bb + (size_t)(buf ^ 1) * BCH, n1 * BN, k1 * BK);
+    if (k1 == 0) load_bias(bias, n1 * BN);  // the epilogue above has used this (tile, N tile)'s
+    __syncthreads();
+    buf ^= 1;
+    tile = t1;
+    nt = n1;
+    kc = k1;
+    advance(tile, nt, kc, t1, n1, k1);
+    h1 = t1 < a.mtiles;
+    return true;
+  };
+  while (step()) {
+  }
+}
+
 // st: activation storage variant (ST of k_gemm2).  A bf16 context stores bf16 activations, so its
 // forward modes run ST 1 and its gradient views ST 2; an fp32 context always ST 0.
 template <int WM, int TM, int TN, int MODE, int SK, int NS>
@@ -606,15 +958,90 @@ static void g2_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int s
     else throw std::logic_error("gemm2: raw dgrad with a bf16 y");
   }
 }
+// The A-resident kernel of a tile (k_gemm2r), storage variants as g2_go; lds = its dynamic LDS bytes
+template <int WM, int TM, int TN>
+constexpr bool g2r_cfg() {
+  return (WM == 2 && TM == 2 && TN == 2) || (WM == 4 && TM == 1 && (TN == 3 || TN == 5)) || (WM == 2 && TM == 1 && TN == 2);
+}
+
+template <auto KFN>
+static void g2r_attr() {
+  static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(KFN),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  if (!ok) throw std::runtime_error("gemm2r: cannot raise the dynamic LDS limit");
+}
+
+template <int WM, int TM, int TN, int MODE, int SK, int NS>
+static void g2r_go(dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st, size_t lds) {
+  if constexpr (MODE == 4) {
+    throw std::logic_error("gemm2r: no implicit im2col");
+  } else if (!bf) {
+    if (st) throw std::logic_error("gemm2r: bf16 storage needs the bf16 compute type");
+    g2r_attr<&k_gemm2r<WM, TM, TN, MODE, SK, NS, false, 0>>();
+    PHX_TLAUNCH((k_gemm2r<WM, TM, TN, MODE, SK, NS, false, 0>), g, dim3(256), lds, s, a);
+  } else {
+    constexpr bool fwd_only = MODE == 1 || MODE == 2 || SK == 1;
+    constexpr bool dgrad_only = MODE == 3 || SK == 2;
+    if constexpr (fwd_only) {
+      if (st != 1) throw std::logic_error("gemm2r: bf16 forward without bf16 activations");
+      g2r_attr<&k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 1>>();
+      PHX_TLAUNCH((k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), lds, s, a);
+    } else if constexpr (dgrad_only) {
+      if (st != 2) throw std::logic_error("gemm2r: bf16 gradient view without bf16 activations");
+      g2r_attr<&k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 2>>();
+      PHX_TLAUNCH((k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 2>), g, dim3(256), lds, s, a);
+    } else {
+      if (st == 1) {
+        g2r_attr<&k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 1>>();
+        PHX_TLAUNCH((k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 1>), g, dim3(256), lds, s, a);
+      } else if (st == 0) {
+        g2r_attr<&k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 0>>();
+        PHX_TLAUNCH((k_gemm2r<WM, TM, TN, MODE, SK, NS, true, 0>), g, dim3(256), lds, s, a);
+      } else {
+        throw std::logic_error("gemm2r: raw dgrad with a bf16 y");
+      }
+    }
+  }
+}
+
+template <int WM, int TM, int TN, int NS>
+static void g2r_launch(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st, size_t lds) {
+  if constexpr (!g2r_cfg<WM, TM, TN>()) {
+    throw std::logic_error("gemm2r: no A-resident kernel for this tile");
+  } else {
+    switch (mode) {
+      case 0:
+        if (sk == 1) g2r_go<WM, TM, TN, 0, 1, NS>(g, s, a, bf, st, lds);
+        else if (sk == 2) g2r_go<WM, TM, TN, 0, 2, NS>(g, s, a, bf, st, lds);
+        else g2r_go<WM, TM, TN, 0, 0, NS>(g, s, a, bf, st, lds);
+        break;
+      case 1:
+        sk == 1 ? g2r_go<WM, TM, TN, 1, 1, NS>(g, s, a, bf, st, lds) : g2r_go<WM, TM, TN, 1, 0, NS>(g, s, a, bf, st, lds);
+        break;
+      case 2:
+        sk == 1 ? g2r_go<WM, TM, TN, 2, 1, NS>(g, s, a, bf, st, lds) : g2r_go<WM, TM, TN, 2, 0, NS>(g, s, a, bf, st, lds);
+        break;
+      case 3:
+        sk == 2 ? g2r_go<WM, TM, TN, 3, 2, NS>(g, s, a, bf, st, lds) : g2r_go<WM, TM, TN, 3, 0, NS>(g, s, a, bf, st, lds);
+        break;
+      default:
+        throw std::logic_error("gemm2r: no implicit im2col");
+    }
+  }
+}
+
 // sk: 1 forward statistics (modes 0-2), 2 BN-backward sums (dgrad modes 0, 3).  Each (WM, TM, TN, NS)
 // is instantiated in its own translation unit (kernels_gemm_cfg*.hip) so the variants compile in
 // parallel.
+// res_lds > 0: the A-resident kernel (k_gemm2r) with that much dynamic LDS.
 template <int WM, int TM, int TN, int NS>
-void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st);
+void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st, size_t res_lds);
 
 #define PHX_G2_DEFINE_LAUNCH_CFG                                                                                 \
   template <int WM, int TM, int TN, int NS>                                                                     \
-  void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st) { \
+  void g2_launch_cfg(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Group<NS>& a, bool bf, int st,  \
+                     size_t res_lds) {                                                                          \
+    if (res_lds) return g2r_launch<WM, TM, TN, NS>(mode, sk, g, s, a, bf, st, res_lds);                       \
     switch (mode) {                                                                                             \
       case 0:                                                                                                   \
         if (sk == 1) g2_go<WM, TM, TN, 0, 1, NS>(g, s, a, bf, st);                                          \

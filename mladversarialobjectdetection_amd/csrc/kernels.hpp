@@ -64,8 +64,11 @@ int gemm_stat_partials(int M, int N, int K, bool bf16 = false);
 // the two GEMM implementations behind launch_gemm (gemm_impl(): PHX_GEMM env, default 2)
 struct Gemm2Plan {
   int wm, tm, tn, mtiles, gx, gy, splits, kslice;
+  int P;           // statistics / BN-backward-sum partial rows the launch writes
+  size_t res_lds;  // > 0: the A-resident kernel (k_gemm2r) with this much dynamic LDS; kslice then
+                   // counts the N tiles of one workgroup's sweep and gy the sweeps
 };
-Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false);
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false, bool allow_res = true);
 void gemm2_force_cfg(int wm, int tm, int tn, int splits);  // tools/gemm_bench sweeps only (0 = off)
 int gemm_impl();
 int gemm_impl_for(int N, bool bf16 = false);
@@ -80,18 +83,19 @@ int gemm_splitk_stats_partials(int M, int N);
 // cbf: C holds bf16 activations (the partial slabs are fp32)
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
                        bool acc, StatSink sink, hipStream_t s, bool cbf = false);
-// dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
-// with a GradSink, the BN-backward sums of the dgrad's result (returns the partial rows)
 // 3x3 convolution GEMM over an implicitly gathered column matrix (kernels_conv.hip)
 bool gemm_gather_ok(int B, int H, int W, int C, int Ho, int Wo, int K, int mode, int s, int pt, int pl);
 int launch_gemm_gather(const float* x, int B, int H, int W, int C, int Ho, int Wo, int mode, int s, int pt, int pl,
                        const float* Bt, const float* bias, float* out, int N, int K, hipStream_t st, float* partial);
+// dgrad GEMM whose A operand is a gradient view (BN backward applied on load)
+// with a GradSink, the BN-backward sums of the dgrad's result (returns the partial rows)
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                       hipStream_t s, float* partial, GradSink gs = GradSink{}, bool bf16 = false);
 int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16 = false);
 // Grouped GEMM: members share Bt [N][K] (weights shared across pyramid levels) and differ in A,
 // C, M and sinks.  mode as gemm2 (0 raw, 1 BN view, 3 gradient view).  No split-K: see
-// gemm_group_ok.  Returns the partial rows P written per member (the same for all).
+// gemm_group_ok.  Returns the most partial rows any member's sinks get; P_out[i] = member i's
+// (the same for all members, except on the A-resident sweep: one row per (M tile, wave row)).
 struct GemmSeg {
   InX A;
   GradX G;
@@ -104,7 +108,7 @@ struct GemmSeg {
 };
 bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16 = false);
 int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s,
-                   bool bf16 = false);
+                   bool bf16 = false, int* P_out = nullptr);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
 int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
                   int Wo, int k, int stride, int pt, int pl, hipStream_t s,

@@ -886,7 +886,7 @@ int gemm_stat_partials(int M, int N, int K, bool bf16) {
   if (gemm_impl_for(N, bf16) == 2) {
     Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16);
     if (q.splits > 1) return N <= 1024 ? gemm_splitk_stats_partials(M, N) : 0;
-    return q.gx;
+    return q.P;
   }
   GemmPlan p = plan_gemm(M, N, K);
   if (p.splits > 1) return N <= 1024 ? gemm_splitk_stats_partials(M, N) : 0;
@@ -1009,7 +1009,7 @@ int launch_gemm_gather(const float* x, int B, int H, int W, int C, int Ho, int W
 int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16) {
   if (gemm_impl_for(N, bf16) == 2) {
     Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16);
-    return q.splits > 1 ? 0 : q.gx;
+    return q.splits > 1 ? 0 : q.P;
   }
   GemmPlan p = plan_gemm(M, N, K);
   return p.splits > 1 ? 0 : p.gx;

@@ -68,7 +68,7 @@ void gemm2_force_cfg(int wm, int tm, int tn, int splits) {
   g_force[0] = wm; g_force[1] = tm; g_force[2] = tn; g_force[3] = splits;
 }
 
-Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16, bool allow_res) {
   Gemm2Plan p;
   G2Cfg c = g2_pick(N, K, bf16);
   if (g_force[0]) {
@@ -83,6 +83,8 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
     const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
     p.gx = (int)std::min<long>(p.mtiles, want);
     if (p.gy > 1 && p.gx > 8) p.gx = p.gx / 8 * 8;
+    p.P = p.gx;
+    p.res_lds = 0;
     return p;
   }
   // few 128x128 tiles (small M, wide N, no split-K): 64-row tiles double the workgroups so
@@ -128,6 +130,33 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16) {
     return !(e && e[0] == '0');
   }();
   if (xcd8 && p.gy > 1 && p.gx > 8) p.gx = p.gx / 8 * 8;
+  p.P = p.gx;
+  p.res_lds = 0;
+  // A-resident sweeps (k_gemm2r): a workgroup keeps its M tile of A' in LDS for a run of N tiles, so
+  // the A view is applied once per run instead of once per N tile.  Runs are as long as the grid
+  // stays >= ~512 workgroups allows; at least 2 N tiles per run, K of at least 2 chunks, no split-K.
+  static const bool res_on = [] {
+    const char* e = std::getenv("PHX_GEMM_RES");
+    return !(e && e[0] == '0');
+  }();
+  const bool res_tile = (c.wm == 2 && c.tm == 2 && c.tn == 2) || (c.wm == 4 && c.tm == 1 && (c.tn == 3 || c.tn == 5)) ||
+                        (c.wm == 2 && c.tm == 1 && c.tn == 2);
+  const int ksteps = (K + bk - 1) / bk;
+  const int esz = bf16 ? 2 : 4;
+  const size_t lds = ((size_t)ksteps * c.bm() + 2 * c.bn()) * bk * esz;
+  if (allow_res && res_on && res_tile && p.splits == 1 && p.gy >= 2 && ksteps >= 2 && lds <= 160 * 1024) {
+    const int per_cu = std::max(1, std::min(2, (int)((160 * 1024) / lds)));
+    const int runs_want = (int)std::max<long>(1, std::min<long>(p.gy, cdiv(512, p.mtiles)));
+    const int nper = cdiv(p.gy, runs_want);
+    if (nper >= 2) {
+      const int runs = cdiv(p.gy, nper);
+      p.res_lds = lds;
+      p.kslice = nper;
+      p.gy = runs;
+      p.gx = (int)std::min<long>(p.mtiles, std::max<long>(1, (long)256 * per_cu / runs));
+      p.P = p.mtiles * c.wm;
+    }
+  }
   return p;
 }
 
@@ -143,16 +172,16 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
               float* partial, StatSink sink, int target_wgs, GradSink gsk, bool bf16) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
-  const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs, bf16);
+  const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs, bf16, mode != 4);
   const bool stats = sink.part != nullptr;
   if (stats && (acc || mode == 3 || (N & 3) || (p.splits > 1 && N > 1024)))
     throw std::runtime_error("gemm: unsupported statistics epilogue");
   if (p.splits > 1 && !partial) throw std::runtime_error("gemm: split-K needs a partial buffer");
   const bool kstats = stats && p.splits == 1;
-  if (stats) sink.P = p.splits > 1 ? gemm_splitk_stats_partials(M, N) : p.gx;
+  if (stats) sink.P = p.splits > 1 ? gemm_splitk_stats_partials(M, N) : p.P;
   const bool gs = gsk.part != nullptr;
   if (gs && (p.splits > 1 || mode == 1 || mode == 2)) throw std::runtime_error("gemm: unsupported GradSink");
-  gsk.P = p.gx;
+  gsk.P = p.P;
   const int sk = kstats ? 1 : gs ? 2 : 0;
   Gemm2Group<1> a{};
   a.n = 1;
@@ -164,19 +193,19 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   const int st = g2_storage(A, G, gsk);
   const int key = p.wm * 100 + p.tm * 10 + p.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a, bf16, st); break;
-    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a, bf16, st); break;
+    case 411: g2_launch_cfg<4, 1, 1, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 412: g2_launch_cfg<4, 1, 2, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 413: g2_launch_cfg<4, 1, 3, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 415: g2_launch_cfg<4, 1, 5, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 222: g2_launch_cfg<2, 2, 2, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 212: g2_launch_cfg<2, 1, 2, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 211: g2_launch_cfg<2, 1, 1, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
+    case 111: g2_launch_cfg<1, 1, 1, 1>(mode, sk, g, s, a, bf16, st, p.res_lds); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
   if (p.splits > 1) return gemm_splitk_finish(partial, p.splits, M, N, bias, C, acc, sink, s, st == 1);
-  return p.gx;
+  return p.P;
 }
 
 bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16) {
@@ -187,7 +216,7 @@ bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16) {
 }
 
 int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s,
-                   bool bf16) {
+                   bool bf16, int* P_out) {
   std::vector<int> M(n);
   for (int i = 0; i < n; ++i) M[i] = segs[i].M;
   if (!gemm_group_ok(M.data(), n, N, K, bf16)) throw std::runtime_error("gemm group: unsupported shapes");
@@ -197,22 +226,31 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
   if (gs && (mode == 1 || mode == 2)) throw std::runtime_error("gemm group: unsupported GradSink");
   Gemm2Group<kMaxSeg> a{};
   a.n = n;
-  int gx = 1;
+  int gx = 1, P = 1;
   Gemm2Plan p0{};
   for (int i = 0; i < n; ++i) {
     const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16);
     if (i == 0) p0 = p;
     gx = std::max(gx, p.gx);
   }
+  // the A-resident sweep when the first (largest) member takes it: every member runs p0's N-tile runs
+  // and writes one partial row per (M tile, wave row)
+  const int kslice = p0.res_lds ? p0.kslice : K;
+  std::vector<int> Pm(n);  // partial rows of each member's sinks
+  for (int i = 0; i < n; ++i) {
+    Pm[i] = p0.res_lds ? cdiv(M[i], p0.wm * p0.tm * 32) * p0.wm : gx;
+    P = std::max(P, Pm[i]);
+    if (P_out) P_out[i] = Pm[i];
+  }
   for (int i = 0; i < n; ++i) {
     const GemmSeg& g = segs[i];
     if ((g.sink.part != nullptr) != stats || (g.gsk.part != nullptr) != gs)
       throw std::runtime_error("gemm group: members differ in their sinks");
     StatSink sink = g.sink;
-    sink.P = gx;
+    sink.P = Pm[i];
     GradSink gsk = g.gsk;
-    gsk.P = gx;
-    a.a[i] = Gemm2Args{g.A, g.G, Bt, g.bias, g.C, g.M, N, K, g.acc ? 1 : 0, nullptr, 1, K, nullptr, sink,
+    gsk.P = Pm[i];
+    a.a[i] = Gemm2Args{g.A, g.G, Bt, g.bias, g.C, g.M, N, K, g.acc ? 1 : 0, nullptr, 1, kslice, nullptr, sink,
                        cdiv(g.M, p0.wm * p0.tm * 32), gsk};
   }
   const int sk = stats ? 1 : gs ? 2 : 0;
@@ -220,18 +258,18 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
   dim3 grid(gx, p0.gy, n);
   const int key = p0.wm * 100 + p0.tm * 10 + p0.tn;
   switch (key) {
-    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
-    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st); break;
+    case 411: g2_launch_cfg<4, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 412: g2_launch_cfg<4, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 413: g2_launch_cfg<4, 1, 3, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 415: g2_launch_cfg<4, 1, 5, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 222: g2_launch_cfg<2, 2, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 212: g2_launch_cfg<2, 1, 2, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 211: g2_launch_cfg<2, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
+    case 111: g2_launch_cfg<1, 1, 1, kMaxSeg>(mode, sk, grid, s, a, bf16, st, p0.res_lds); break;
     default: throw std::runtime_error("gemm2: no kernel for this configuration");
   }
   PHX_LAUNCH_CHECK();
-  return gx;
+  return P;
 }
 
 }  // namespace phx

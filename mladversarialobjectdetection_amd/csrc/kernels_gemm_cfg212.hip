@@ -4,6 +4,6 @@
 
 namespace phx {
 PHX_G2_DEFINE_LAUNCH_CFG
-template void g2_launch_cfg<2, 1, 2, 1>(int, int, dim3, hipStream_t, const Gemm2Group<1>&, bool, int);
-template void g2_launch_cfg<2, 1, 2, kMaxSeg>(int, int, dim3, hipStream_t, const Gemm2Group<kMaxSeg>&, bool, int);
+template void g2_launch_cfg<2, 1, 2, 1>(int, int, dim3, hipStream_t, const Gemm2Group<1>&, bool, int, size_t);
+template void g2_launch_cfg<2, 1, 2, kMaxSeg>(int, int, dim3, hipStream_t, const Gemm2Group<kMaxSeg>&, bool, int, size_t);
 }  // namespace phx
