@@ -100,10 +100,11 @@ KIND_KERNELS = {
 }
 
 
-def pmc_traffic(kind):
-    """HBM bytes per launch of `kind` from the committed rocprofv3 PMC summary (FETCH_SIZE x2 for
-    gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def pmc_traffic(kind, fname="pmc_traffic.json"):
+    """HBM bytes per launch of `kind` from a committed rocprofv3 PMC summary of this configuration
+    (FETCH_SIZE x2 for gfx950's half-counted wide reads + WRITE_SIZE, MI355X_MICROARCH.md HBM
+    section; scripts/pmc_summary.py), or None."""
+    p = os.path.join(ROOT, "profiles", fname)
     try:
         with open(p) as f:
             d = json.load(f)
@@ -113,7 +114,7 @@ def pmc_traffic(kind):
     return None if e is None else e.get("bytes_per_launch")
 
 
-def kernel_roofline(kind, r, mfma_peak=PEAK_FP32_TFLOPS, pmc=True):
+def kernel_roofline(kind, r, mfma_peak=PEAK_FP32_TFLOPS, pmc="pmc_traffic.json"):
     """Roofline of the dominant launch group: its bound is the one whose peak-time for the group's
     algorithmic work is larger; achieved = algorithmic bytes (FLOPs) / measured time."""
     sec = r["ms"] * 1e-3
@@ -123,7 +124,7 @@ def kernel_roofline(kind, r, mfma_peak=PEAK_FP32_TFLOPS, pmc=True):
     else:
         ach, peak, unit, bound = r["flops"] / sec / 1e12, mfma_peak, "TFLOP/s", "mfma"
     out = {"bound": bound, "achieved": round(ach, 3), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-           "traffic": pmc_traffic(kind) if pmc else None, "kernel": kind, "kernels": KIND_KERNELS.get(kind, kind),
+           "traffic": pmc_traffic(kind, pmc) if pmc else None, "kernel": kind, "kernels": KIND_KERNELS.get(kind, kind),
            "launches": r["count"], "avg_us": round(1e3 * r["ms"] / r["count"], 2),
            "algorithmic_bytes_per_launch": round(r["bytes"] / r["count"]),
            "algorithmic_flops_per_launch": round(r["flops"] / r["count"]),
@@ -232,8 +233,11 @@ def main():
         victim.ctx.profile(False)
         kind, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
         mpeak = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
-        # the committed PMC traffic summary was collected on the C2 configuration only
-        roofline = kernel_roofline(kind, r, mpeak, pmc=(args.model, args.dtype, S, B) == ("efficientdet-d0", "f32", 512, 16))
+        # committed PMC traffic summaries: C2 (pmc_traffic.json) and C4 (pmc_traffic_d4bf16.json)
+        cfg = (args.model, args.dtype, S, B)
+        pmc = {("efficientdet-d0", "f32", 512, 16): "pmc_traffic.json",
+               ("efficientdet-d4", "bf16", 1024, 4): "pmc_traffic_d4bf16.json"}.get(cfg)
+        roofline = kernel_roofline(kind, r, mpeak, pmc=pmc)
         step_ach = flop_per_image(args.model, S) * images_per_s / world / 1e12
         step_roof = {"achieved_tflops_per_gpu": round(step_ach, 3),
                      "frac_mfma_peak": round(step_ach / mpeak, 4), "mfma_peak_tflops": mpeak,

@@ -5,15 +5,19 @@ FETCH_SIZE counts exactly half the bytes of wide (16 B/lane) coalesced reads; WR
 16-B stores.  Kinds match the library profiler's launch groups; `launches` counts the group's primary
 kernel.
 
-    python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_traffic.json
+    python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/pmc_traffic.json [set] [source]
+
+set: "detector" (default; the attack step's kinds) or "defender" (tools/defender_bench.py's U-Net kinds).
 """
 import csv
 import json
+import re
 import sys
 from collections import defaultdict
 
 KINDS = [  # (kind, substring, primary?) — first match wins
-    ("gemm", "k_gemm_splitk_reduce", False), ("gemm", "k_gemm2<", True), ("gemm", "k_gemm<", True),
+    ("gemm", "k_gemm_splitk_reduce", False), ("gemm", "k_gemm2<", True), ("gemm", "k_gemm2r<", True),
+    ("gemm", "k_gemm<", True),
     ("dw_fwd", "k_dw_fwd<", True), ("dw_bwd", "k_dw_bwd<", True),
     ("bn_stats", "k_bn_finalize<false", True),
     ("bn_stats", "k_colred_part<phx::StatsAcc", True), ("bn_stats", "k_colred_final<phx::StatsEpi>", False),
@@ -24,9 +28,21 @@ KINDS = [  # (kind, substring, primary?) — first match wins
 ]
 
 
-def kind_of(name):
-    for k, sub, prim in KINDS:
-        if sub in name:
+# the defender step: U-Net 3x3 convs (implicit-gather GEMMs are k_gemm2 MODE 4, the template's 4th
+# argument), weight gradients, BN reductions; regex patterns start with "re:"
+DEF_KINDS = [
+    ("unet_conv", "k_conv3_small<", True), ("unet_conv", r"re:k_gemm2<\d+, \d+, \d+, 4,", True),
+    ("unet_conv", "k_im2col", False),
+    ("unet_wgrad", "k_wgrad_mfma<", True), ("unet_wgrad", "k_wgrad_fold", False),
+    ("unet_bn", "k_colred64", True), ("unet_bn", "k_un_bn_final", False), ("unet_bn", "k_un_bnb_final", False),
+    ("unet_bn", "k_un_bnb_apply", False), ("unet_bn", "k_un_bnact", False),
+    ("soft_nms", "k_soft_nms", True),
+]
+
+
+def kind_of(name, kinds=None):
+    for k, sub, prim in (kinds or KINDS):
+        if sub.startswith("re:") and re.search(sub[3:], name) or not sub.startswith("re:") and sub in name:
             return k, prim
     return None, False
 
@@ -40,12 +56,13 @@ def load(d, counter):
     return out
 
 
-def main(fd, wd, dst):
+def main(fd, wd, dst, kset="detector", source=None):
+    kinds_tab = DEF_KINDS if kset == "defender" else KINDS
     f, w = load(fd, "FETCH_SIZE"), load(wd, "WRITE_SIZE")
     agg = defaultdict(lambda: {"launches": 0, "fetch_kib": 0.0, "write_kib": 0.0})
     per_kernel = defaultdict(lambda: {"n": 0, "fetch_kib": 0.0})
     for did, (name, v) in f.items():
-        k, prim = kind_of(name)
+        k, prim = kind_of(name, kinds_tab)
         per_kernel[name]["n"] += 1
         per_kernel[name]["fetch_kib"] += v
         if k is None:
@@ -54,7 +71,7 @@ def main(fd, wd, dst):
         agg[k]["launches"] += int(prim)
     # the two passes are separate runs of the same deterministic program: match by kernel order
     for did, (name, v) in w.items():
-        k, _ = kind_of(name)
+        k, _ = kind_of(name, kinds_tab)
         if k is not None:
             agg[k]["write_kib"] += v
         per_kernel[name].setdefault("write_kib", 0.0)
@@ -65,8 +82,8 @@ def main(fd, wd, dst):
         kinds[k] = {"launches": a["launches"], "hbm_bytes": byt,
                     "bytes_per_launch": round(byt / max(1, a["launches"])),
                     "read_bytes": 2.0 * a["fetch_kib"] * 1024.0, "write_bytes": a["write_kib"] * 1024.0}
-    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), "
-                     "python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile",
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes), " +
+                     (source or "python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile"),
            "correction": "bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB), gfx950 half-counted wide reads",
            "kinds": kinds}
     with open(dst, "w") as fh:
@@ -80,4 +97,4 @@ def main(fd, wd, dst):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:6])

@@ -105,7 +105,9 @@ def main():
         rep = victim.ctx.profile_report()
         victim.ctx.profile(False)
         kind, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
-        roofline = kernel_roofline(kind, r, pmc=False)
+        # PMC traffic of the C5 configuration (512^2, 8 images): profiles/pmc_traffic_defender.json
+        c5 = a.image_size == 512 and a.batch == 8
+        roofline = kernel_roofline(kind, r, pmc="pmc_traffic_defender.json" if c5 else None)
         roofline["kernels"] = DEF_KINDS.get(kind, kind)
         fl = sum(v["flops"] for v in rep.values())
         step_roof = {"achieved_tflops_per_gpu": round(fl / (el / a.steps) / 1e12, 3),
