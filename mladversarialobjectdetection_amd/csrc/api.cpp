@@ -1990,6 +1990,12 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
             ctx->fwd_hook_at = i;
             break;
           }
+        // bf16 activations: not before half the ops.  With the side pass's first (1024^2 bf16)
+        // layers beside the second pass's stages 6-7, about one D4 bf16 1024^2 step in five came
+        // out different (every score ~2e-2 off; never in fp32 or at 512^2; root cause not found,
+        // DESIGN.md section 12).  Forking at 35-98 % of the ops gave bit-identical back-to-back
+        // steps in every trial, and at half the ops C4 takes the same time (28.86 ms).
+        if (E.abf) ctx->fwd_hook_at = std::max(ctx->fwd_hook_at, E.prog.ops.size() / 2);
       }
     }
   } else {
@@ -2180,7 +2186,9 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
     const Op& op = E.prog.ops[i];
     if (op.name != op_name) continue;
     const int t = (op.t == OP_BN && which == 0) ? op.in[0] : op.out;
-    if (nfloats != E.prog.tensors[t].numel()) throw std::invalid_argument("tap: size mismatch");
+    if (nfloats != E.prog.tensors[t].numel())
+      throw std::invalid_argument("tap: size mismatch (the tensor has " + std::to_string(E.prog.tensors[t].numel()) +
+                                  " elements)");
     if (which == 0 && op.t == OP_FUSE && E.fuse_folded[i])
       throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
     const float* src = which == 0 ? E.tptr(t, nullptr) : E.gptr(op.out);

@@ -880,6 +880,12 @@ __global__ void k_def_filter(const float* __restrict__ nb, const float* __restri
     }
   }
   oc[b] = k;
+  // the rows past the kept boxes are zero (defined outputs: the caller's buffers are not cleared)
+  for (int i = k; i < maxo; ++i) {
+    float* o = ob + ((long)b * maxo + i) * 4;
+    o[0] = o[1] = o[2] = o[3] = 0.f;
+    if (os) os[(long)b * maxo + i] = 0.f;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
