@@ -21,8 +21,8 @@ sys.path.insert(0, ROOT)
 from bench import PEAK_FP32_TFLOPS, kernel_roofline, synth_images  # noqa: E402
 
 DEF_KINDS = {
-    "unet_conv": "k_conv3_small<NT,MODE,VEC> (+ k_im2col + k_gemm2 for the 64-128-channel levels): 3x3 convs, "
-                 "transposed convs and their data gradients",
+    "unet_conv": "k_conv3_small<NT,MODE,VEC> (+ k_gemm2 MODE 4, the implicit-im2col GEMM, for the 64-128-channel "
+                 "levels): 3x3 convs, transposed convs and their data gradients",
     "unet_wgrad": "k_wgrad_mfma<SRC,VEC> + column-sum bias gradients",
     "unet_bn": "k_colred64 statistics / BN-backward sums + BN apply",
     "unet_gemm": "k_gemm2 (attention 1x1 convs)",
