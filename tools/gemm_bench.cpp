@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../mladversarialobjectdetection_amd/csrc/kernels.hpp"
@@ -71,16 +72,28 @@ int main(int argc, char** argv) {
   hipEventCreate(&e0); hipEventCreate(&e1);
   double tot_us = 0, tot_roof = 0, tot1 = 0;
   const int wgs = argc > 1 ? atoi(argv[1]) : 1024;
+  // GEMM_MODE=1: A through a BN + swish view; 3: a BN-backward gradient view (dgrad, no stats)
+  const int mode = getenv("GEMM_MODE") ? atoi(getenv("GEMM_MODE")) : 0;
+  float *mu, *scl, *be, *ybuf, *m1, *m2;
+  hipMalloc(&mu, 4096 * 4); hipMalloc(&scl, 4096 * 4); hipMalloc(&be, 4096 * 4);
+  hipMalloc(&m1, 4096 * 4); hipMalloc(&m2, 4096 * 4);
+  hipMalloc(&ybuf, maxA * 4);
+  fill(mu, 4096, 4); fill(scl, 4096, 5); fill(be, 4096, 6); fill(m1, 4096, 7); fill(m2, 4096, 8);
+  fill(ybuf, maxA, 9);
   for (auto& s : shapes) {
-    InX ax{A, nullptr, nullptr, nullptr, 0};
+    InX ax{A, mode == 1 ? mu : nullptr, scl, be, mode == 1 ? 1 : 0};
+    GradX gx{A, ybuf, mu, scl, scl, be, m1, m2, 1};
     // GEMM_NOSTATS=1: every shape without the statistics epilogue (its cost by difference)
-    StatSink sink = (s.stats && !getenv("GEMM_NOSTATS")) ? StatSink{sp, sc, s.N, 0} : StatSink{};
+    StatSink sink = (s.stats && mode != 3 && !getenv("GEMM_NOSTATS")) ? StatSink{sp, sc, s.N, 0} : StatSink{};
     int impl = 1;
     auto run = [&]() {
       if (impl == 1)
         gemm1_run(0, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st, part, sink);
+      else if (mode == 3)
+        gemm2_run(3, InX{A, nullptr, nullptr, nullptr, 0}, gx, Bt, nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st,
+                  part, StatSink{}, wgs);
       else
-        gemm2_run(0, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st, part, sink,
+        gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st, part, sink,
                   wgs);
     };
     const int impl0 = getenv("GEMM_IMPL1") ? 1 : 2;
@@ -93,7 +106,13 @@ int main(int argc, char** argv) {
     hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost);
     hipMemcpy(hr.data(), R, hr.size() * 4, hipMemcpyDeviceToHost);
     double maxerr = 0;
-    for (size_t i = 0; i < hc.size(); ++i) maxerr = std::max(maxerr, (double)std::fabs(hc[i] - hr[i]));
+    unsigned long long hsh = 1469598103934665603ull;  // FNV-1a of C's bits: bit-identity across builds
+    for (size_t i = 0; i < hc.size(); ++i) {
+      maxerr = std::max(maxerr, (double)std::fabs(hc[i] - hr[i]));
+      unsigned u;
+      memcpy(&u, &hc[i], 4);
+      hsh = (hsh ^ u) * 1099511628211ull;
+    }
     const int it = 20;
     for (int i = 0; i < 3; ++i) run();
     hipEventRecord(e0, st);
@@ -103,6 +122,10 @@ int main(int argc, char** argv) {
     float ms;
     hipEventElapsedTime(&ms, e0, e1);
     const double us = ms * 1e3 / it;
+    // the last timed run's C must equal the first run's bit for bit
+    std::vector<float> hl(hc.size());
+    hipMemcpy(hl.data(), C, hl.size() * 4, hipMemcpyDeviceToHost);
+    const bool det = memcmp(hl.data(), hc.data(), hc.size() * 4) == 0;
     const double by = 4.0 * ((double)s.M * s.K + (double)s.M * s.N + (double)s.N * s.K);
     const double fl = 2.0 * s.M * s.N * s.K;
     const double roof = std::max(by / 8e12, fl / 157.3e12) * 1e6;
@@ -113,9 +136,9 @@ int main(int argc, char** argv) {
     GemmPlan p = plan_gemm(s.M, s.N, s.K);
     Gemm2Plan q = plan_gemm2(s.M, s.N, s.K, wgs);
     if (impl == 1) { tot1 += us; }
-    printf("impl%d M=%8d N=%5d K=%5d stats=%d  %8.1f us  %6.0f GB/s  %6.1f TF/s  roof %6.1f us (%4.0f%%)  grid=%dx%dx%d  err=%.2e\n",
+    printf("impl%d M=%8d N=%5d K=%5d stats=%d  %8.1f us  %6.0f GB/s  %6.1f TF/s  roof %6.1f us (%4.0f%%)  grid=%dx%dx%d  err=%.2e  hash=%016llx%s\n",
            impl, s.M, s.N, s.K, (int)s.stats, us, by / us * 1e-3, fl / us * 1e-6, roof, 100 * roof / us,
-           impl == 1 ? p.gx : q.gx, impl == 1 ? p.gy : q.gy, impl == 1 ? p.splits : q.splits, maxerr);
+           impl == 1 ? p.gx : q.gx, impl == 1 ? p.gy : q.gy, impl == 1 ? p.splits : q.splits, maxerr, hsh, det ? "" : "  NONDETERMINISTIC");
     }
   }
   printf("impl1 total %.1f us; impl2 total %.1f us, roofline %.1f us (%.0f%%)\n", tot1, tot_us, tot_roof,
@@ -124,14 +147,7 @@ int main(int argc, char** argv) {
   if (getenv("GEMM_SWEEP")) {
     // GEMM_MODE=1: A through a BN + swish view; 3: a BN-backward gradient view (dgrad, no stats)
     // GEMM_BF16=1: bf16 matrix cores
-    const int mode = getenv("GEMM_MODE") ? atoi(getenv("GEMM_MODE")) : 0;
     const bool bf = getenv("GEMM_BF16") != nullptr;
-    float *mu, *scl, *be, *ybuf, *m1, *m2;
-    hipMalloc(&mu, 4096 * 4); hipMalloc(&scl, 4096 * 4); hipMalloc(&be, 4096 * 4);
-    hipMalloc(&m1, 4096 * 4); hipMalloc(&m2, 4096 * 4);
-    hipMalloc(&ybuf, maxA * 4);
-    fill(mu, 4096, 4); fill(scl, 4096, 5); fill(be, 4096, 6); fill(m1, 4096, 7); fill(m2, 4096, 8);
-    fill(ybuf, maxA, 9);
     printf("sweep mode %d bf16 %d\n", mode, (int)bf);
     const int cfgs[8][3] = {{4, 1, 1}, {4, 1, 2}, {4, 1, 3}, {4, 1, 5}, {2, 2, 2}, {2, 1, 2}, {2, 1, 1}, {1, 1, 1}};
     const int splits_opt[4] = {1, 2, 4, 8};
