@@ -36,6 +36,21 @@ T* dalloc(size_t n) {
   return reinterpret_cast<T*>(p);
 }
 
+// PHX_GUARD_BYTES=n (diagnostics): every executor allocation gets n guard bytes of 0xA5 after its
+// end, and phx_step_grad checks them after the step (synchronising), reporting any overwrite on
+// stderr — an out-of-bounds write past a buffer shows up even when it corrupts nothing visible.
+size_t guard_bytes() {
+  static const size_t g = [] {
+    const char* e = std::getenv("PHX_GUARD_BYTES");
+    return e ? (size_t)std::atol(e) : (size_t)0;
+  }();
+  return g;
+}
+struct Guard {
+  const char* base;
+  size_t size;  // the buffer's own bytes (the guard follows)
+};
+
 struct DevFree {
   void operator()(void* p) const {
     if (p) (void)hipFree(p);
@@ -145,12 +160,21 @@ struct Exec {
   bool abf = false;
   size_t bytes = 0;  // device bytes owned by this executor
   uint64_t used = 0;  // phx_ctx::clock at the last use
+  std::vector<Guard> guards;  // PHX_GUARD_BYTES
   template <typename T>
   T* alloc(size_t n) {
-    T* p = dalloc<T>(n);
-    owned.emplace_back(p);
+    const size_t gb = guard_bytes();
+    if (n == 0) n = 1;
+    // [gb guard][buffer][gb guard] (gb a multiple of 256 keeps the buffer's alignment)
+    char* q = dalloc<char>(n * sizeof(T) + 2 * gb);
+    owned.emplace_back(q);
+    if (gb) {
+      PHX_HIP(hipMemset(q, 0xA5, gb));
+      PHX_HIP(hipMemset(q + gb + n * sizeof(T), 0xA5, gb));
+      guards.push_back(Guard{q + gb, n * sizeof(T)});
+    }
     bytes += n * sizeof(T);
-    return p;
+    return reinterpret_cast<T*>(q + gb);
   }
   // base pointer of tensor t (bf16 elements when tbf(t): kernels index it as such)
   float* tptr(int t, const float* input) const {
@@ -1449,6 +1473,38 @@ void run_nms(phx_ctx* ctx, Exec& E, int keep_mask, float* ob, float* os, int* oc
                   NmsCand{E.cand_list, E.cand_count, keep_mask, t});
 }
 
+// PHX_GUARD_BYTES: after a step, every executor allocation's guard band must still be 0xA5
+void check_guards(phx_ctx* ctx, hipStream_t s) {
+  PHX_HIP(hipStreamSynchronize(s));
+  if (ctx->s1) PHX_HIP(hipStreamSynchronize(ctx->s1));
+  const size_t gb = guard_bytes();
+  std::vector<unsigned char> h(gb);
+  for (auto& ep : ctx->execs) {
+    for (size_t i = 0; i < ep->guards.size(); ++i) {
+      const Guard& g = ep->guards[i];
+      for (int side = 0; side < 2; ++side) {
+        const char* band = side ? g.base + g.size : g.base - gb;
+        PHX_HIP(hipMemcpy(h.data(), band, gb, hipMemcpyDeviceToHost));
+        size_t first = gb, last = 0;
+        for (size_t k = 0; k < gb; ++k)
+          if (h[k] != 0xA5) {
+            first = std::min(first, k);
+            last = k;
+          }
+        if (first < gb) {
+          if (side)
+            fprintf(stderr, "phx guard: exec B=%d tag=%d allocation %zu (%zu bytes) overwritten at +%zu..+%zu past its end\n",
+                    ep->B, ep->tag, i, g.size, first, last);
+          else
+            fprintf(stderr, "phx guard: exec B=%d tag=%d allocation %zu (%zu bytes) overwritten at -%zu..-%zu before its start\n",
+                    ep->B, ep->tag, i, g.size, gb - last, gb - first);
+          PHX_HIP(hipMemset(const_cast<char*>(band), 0xA5, gb));
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
 
 phx::ExtTiming*& phx::ext_timing() {
@@ -2052,6 +2108,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
   if (fork || side_nms) PHX_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
   if (fork) launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), E1p->side, E.side, s);
+  if (guard_bytes()) check_guards(ctx, s);
   return PHX_OK;
   PHX_CATCH(ctx)
 }

@@ -679,6 +679,9 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
   }
 }
 
+// slabs whose loads a split-K reduce issues together (more are added one by one)
+constexpr int kSkMax = 8;
+
 // split-K reduction: C (+)= sum_s partial[s] + bias (BF: C holds bf16 activations)
 template <bool BF>
 __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(const float* __restrict__ partial,
@@ -687,8 +690,15 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce(const float* __restr
                                                             float* __restrict__ C, int acc_flag) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= MN) return;
+  // every slab's load in flight at once (clamped to the last slab past S), added in slab order
+  float p[kSkMax];
+#pragma unroll
+  for (int s = 0; s < kSkMax; ++s) p[s] = partial[(long)min(s, S - 1) * MN + i];
   float v = 0.f;
-  for (int s = 0; s < S; ++s) v += partial[(long)s * MN + i];
+#pragma unroll
+  for (int s = 0; s < kSkMax; ++s)
+    if (s < S) v += p[s];
+  for (int s = kSkMax; s < S; ++s) v += partial[(long)s * MN + i];
   if (bias) v += bias[i % N];
   if (acc_flag) v += ald1<BF>(C, i);
   ast1<BF>(C, i, v);
@@ -717,10 +727,19 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce_stats(const float* _
     const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + c4 * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
     for (int r = r0 + rs; r < r1; r += rpi) {
       const long e = (long)r * N + c4 * 4;
+      // every slab's load in flight at once (clamped to the last slab past S), added in slab order
+      float4 p[kSkMax];
+#pragma unroll
+      for (int k = 0; k < kSkMax; ++k) p[k] = *reinterpret_cast<const float4*>(partial + min(k, S - 1) * MN + e);
       float4 v = bv;
-      for (int k = 0; k < S; ++k) {
-        const float4 p = *reinterpret_cast<const float4*>(partial + k * MN + e);
-        v.x += p.x; v.y += p.y; v.z += p.z; v.w += p.w;
+#pragma unroll
+      for (int k = 0; k < kSkMax; ++k)
+        if (k < S) {
+          v.x += p[k].x; v.y += p[k].y; v.z += p[k].z; v.w += p[k].w;
+        }
+      for (int k = kSkMax; k < S; ++k) {
+        const float4 q = *reinterpret_cast<const float4*>(partial + k * MN + e);
+        v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
       }
       ast4<BF>(C, e, v);
       if constexpr (BF) v = make_float4(round_bf16(v.x), round_bf16(v.y), round_bf16(v.z), round_bf16(v.w));
