@@ -508,7 +508,22 @@ __device__ __forceinline__ void wave_fold(const double* __restrict__ part, int n
   const int lane = threadIdx.x & 63;
   s0 = 0.0;
   s1 = 0.0;
-  for (int z = lane; z < nblk; z += 64) {
+  int z = lane;
+  // four blocks' loads in flight, added in block order
+  for (; z + 192 < nblk; z += 256) {
+    double v0[4], v1[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v0[u] = part[((long)(z + 64 * u) * C + c) * 2];
+      v1[u] = part[((long)(z + 64 * u) * C + c) * 2 + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s0 += v0[u];
+      s1 += v1[u];
+    }
+  }
+  for (; z < nblk; z += 64) {
     s0 += part[((long)z * C + c) * 2];
     s1 += part[((long)z * C + c) * 2 + 1];
   }
@@ -982,8 +997,14 @@ void un_wgrad(const float* dy, int ldy, const float* x, int ldx, int src, int B,
 }
 
 // row blocks of a column reduction: about 8192 elements per block (32 per lane), at most 1024
+#ifndef PHX_UN_RED_ELEMS
+#define PHX_UN_RED_ELEMS 8192
+#endif
+#ifndef PHX_UN_RED_MAXBLK
+#define PHX_UN_RED_MAXBLK 1024
+#endif
 static int un_colred_blocks(long M, int C) {
-  return (int)std::min<long>(std::max<long>(std::min<long>(cdiv(M * C, 8192), M), 1), 1024);
+  return (int)std::min<long>(std::max<long>(std::min<long>(cdiv(M * C, PHX_UN_RED_ELEMS), M), 1), PHX_UN_RED_MAXBLK);
 }
 
 static void colred(const ColRed& r, long M, int C, int mode, double* part, int* nblk, hipStream_t st) {
