@@ -161,7 +161,20 @@ __global__ __launch_bounds__(256) void k_colred_final(E e, const double* __restr
   const int c = blockIdx.x * 16 + cl;
   double s0 = 0.0, s1 = 0.0;
   if (c < C) {
-    for (int k = g; k < chunks; k += 16) {
+    int k = g;
+    // four chunks' loads in flight, added in chunk order
+    for (; k + 48 < chunks; k += 64) {
+      double2 p[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        p[u] = *reinterpret_cast<const double2*>(part + (((long)seg * chunks + k + 16 * u) * C + c) * 2);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        s0 += p[u].x;
+        s1 += p[u].y;
+      }
+    }
+    for (; k < chunks; k += 16) {
       const double2 p = *reinterpret_cast<const double2*>(part + (((long)seg * chunks + k) * C + c) * 2);
       s0 += p.x;
       s1 += p.y;
