@@ -281,16 +281,23 @@ __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, lo
   }
 }
 
+// rows per lane whose loads are in flight together (fp32 / bf16 BN input of the GradSink)
+#ifndef PHX_EW_D
+#define PHX_EW_D 4
+#endif
+#ifndef PHX_EW_DBF
+#define PHX_EW_DBF 4
+#endif
 template <class F>
 static int ew_gstats(F f, long seg_rows, int C, int nseg, GradSink g, hipStream_t s) {
   if (C % 4) throw std::runtime_error("ew_gstats: C % 4 != 0");
   RedPlan p = red_plan(seg_rows, C, nseg);
   g.P = nseg * p.chunks;
   if (g.part && g.ybf)
-    hipLaunchKernelGGL((k_ew_gstats<F, 4, true>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+    hipLaunchKernelGGL((k_ew_gstats<F, PHX_EW_DBF, true>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
                        C, p.rpc, g);
   else
-    hipLaunchKernelGGL((k_ew_gstats<F, 4, false>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
+    hipLaunchKernelGGL((k_ew_gstats<F, PHX_EW_D, false>), dim3(p.chunks, p.cgroups, nseg), dim3(256), 0, s, f, seg_rows,
                        C, p.rpc, g);
   PHX_LAUNCH_CHECK();
   return g.P;
