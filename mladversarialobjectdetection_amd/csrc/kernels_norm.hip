@@ -458,7 +458,20 @@ __global__ __launch_bounds__(256) void k_bn_finalize(FinGroup<E, NS> grp) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) fold(v[u], n[u]);
   }
-  for (; p < P; p += 256) fold(pc[p], BWD ? 1.f : cnt[p]);
+  // the remaining (at most three) partials of this lane: loads in flight together, folded in order
+  if (P > 0) {
+    float2 v[3];
+    float n[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int pu = min(p + 256 * u, P - 1);
+      v[u] = pc[pu];
+      n[u] = BWD ? 1.f : cnt[pu];
+    }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (p + 256 * u < P) fold(v[u], n[u]);
+  }
   r1[t] = s1;
   r2[t] = s2;
   __syncthreads();
