@@ -253,6 +253,13 @@ int phx_debug_last_image_grad(phx_ctx* ctx, float* out, void* stream);
  * = 1 the loss gradient w.r.t. its output (a batch norm's after its activation); NHWC [B,h,w,C] =
  * nfloats floats (device->device).  PHX_EINVAL if the name or size is wrong, or no gradient exists. */
 int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size_t nfloats, void* stream);
+/* Stream-hazard diagnostics.  With PHX_CKSUM=1 in the environment (read per call), every
+ * phx_step_grad takes an order-independent 64-bit hash of each tensor / statistics slot an op
+ * writes, on the op's stream right after it.  This copies the last step's list ("name\thex\n" lines,
+ * launch order) of the executor with `tag` (0: the step's, 1: the concurrent first pass's) into buf
+ * (synchronising); *needed = bytes including the NUL.  Two steps on the same inputs must give the
+ * same list; the first differing line names the launch that broke. */
+int phx_debug_checksums(phx_ctx* ctx, int tag, char* buf, size_t cap, size_t* needed);
 
 /* ---- defender step (BASELINE C5) ------------------------------------------
  * attack_detection.PatchAttackDefender (attack_detection.py:31-206, training) over a frozen
@@ -278,7 +285,12 @@ int64_t phx_def_num_moving(phx_def* d);
 int phx_def_manifest(phx_def* d, char* buf, size_t cap, size_t* needed);
 /* BN moving statistics: src != NULL loads them, dst != NULL copies them out (any memory) */
 int phx_def_moving(phx_def* d, float* dst, const float* src, void* stream);
+/* Device bytes of the batch-B workspace a training step uses (built if needed). */
 int phx_def_workspace_bytes(phx_def* d, int B, size_t* bytes);
+/* Device bytes the first phx_def_eval_step at batch B adds to that workspace (the evaluation
+ * Masker's matched patches and worst-case resized-patch store, reserved on first use and freed with
+ * the workspace); a run that only trains never holds them. */
+int phx_def_eval_workspace_bytes(phx_def* d, int B, size_t* bytes);
 /* PatchAttackDefender.call(images, training=True) + tape.gradient (attack_detection.py:168-206).
  * boxes [B,100,4] + count [B] (device) place the patches; NULL = the victim's first pass.
  * grad: num_params floats followed by the metric row [loss] (SUM-all-reducible). */

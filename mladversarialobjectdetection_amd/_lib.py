@@ -93,6 +93,7 @@ _SIGS = [
     ("phx_debug_last_detections", c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_debug_last_image_grad", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_tap", c_int, [c_void_p, c_char_p, c_int, c_void_p, c_size_t, c_void_p]),
+    ("phx_debug_checksums", c_int, [c_void_p, c_int, c_char_p, c_size_t, POINTER(c_size_t)]),
     # defender step
     ("phx_def_create", c_int, [c_void_p, c_int, c_uint64, POINTER(c_void_p)]),
     ("phx_def_destroy", None, [c_void_p]),
@@ -102,6 +103,7 @@ _SIGS = [
     ("phx_def_manifest", c_int, [c_void_p, c_char_p, c_size_t, POINTER(c_size_t)]),
     ("phx_def_moving", c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
     ("phx_def_workspace_bytes", c_int, [c_void_p, c_int, POINTER(c_size_t)]),
+    ("phx_def_eval_workspace_bytes", c_int, [c_void_p, c_int, POINTER(c_size_t)]),
     ("phx_def_step_grad", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     ("phx_def_eval_step", c_int,
@@ -209,6 +211,14 @@ class Context:
         n = c_size_t(0)
         self.call("phx_workspace_bytes", int(batch), ctypes.byref(n))
         return int(n.value)
+
+    def checksums(self, tag: int = 0) -> list:
+        """PHX_CKSUM diagnostics: [(name, hash)] of the last step's writes, in launch order."""
+        need = c_size_t()
+        self.call("phx_debug_checksums", int(tag), None, 0, ctypes.byref(need))
+        buf = ctypes.create_string_buffer(need.value)
+        self.call("phx_debug_checksums", int(tag), buf, need.value, ctypes.byref(need))
+        return [tuple(ln.split("\t")) for ln in buf.value.decode().splitlines() if ln]
 
     def call(self, name: str, *args):
         rc = getattr(self.lib, name)(self.h, *args)

@@ -39,10 +39,15 @@ T* dalloc(size_t n) {
 // PHX_GUARD_BYTES=n (diagnostics): every executor allocation gets n guard bytes of 0xA5 after its
 // end, and phx_step_grad checks them after the step (synchronising), reporting any overwrite on
 // stderr — an out-of-bounds write past a buffer shows up even when it corrupts nothing visible.
+// (rounded up to a multiple of 256 so every buffer keeps the 256-B alignment its 16-B vector loads
+// and the GEMM planner assume; counted in Exec::bytes)
 size_t guard_bytes() {
   static const size_t g = [] {
     const char* e = std::getenv("PHX_GUARD_BYTES");
-    return e ? (size_t)std::atol(e) : (size_t)0;
+    const long v = e ? std::atol(e) : 0;
+    const size_t r = v > 0 ? ((size_t)v + 255) / 256 * 256 : 0;
+    if (r) fprintf(stderr, "phx: PHX_GUARD_BYTES: %zu-byte guard bands around every executor buffer\n", r);
+    return r;
   }();
   return g;
 }
@@ -161,6 +166,12 @@ struct Exec {
   size_t bytes = 0;  // device bytes owned by this executor
   uint64_t used = 0;  // phx_ctx::clock at the last use
   std::vector<Guard> guards;  // PHX_GUARD_BYTES
+  // PHX_CKSUM=1 (diagnostics): a hash of every tensor / statistics slot an op writes, taken on the
+  // op's stream right after it, in launch order (phx_debug_checksums)
+  unsigned long long* ck = nullptr;
+  size_t ck_cap = 0;
+  bool ck_on = false;
+  std::vector<std::string> ck_names;
   template <typename T>
   T* alloc(size_t n) {
     const size_t gb = guard_bytes();
@@ -173,7 +184,7 @@ struct Exec {
       PHX_HIP(hipMemset(q + gb + n * sizeof(T), 0xA5, gb));
       guards.push_back(Guard{q + gb, n * sizeof(T)});
     }
-    bytes += n * sizeof(T);
+    bytes += n * sizeof(T) + 2 * gb;
     return reinterpret_cast<T*>(q + gb);
   }
   // base pointer of tensor t (bf16 elements when tbf(t): kernels index it as such)
@@ -798,6 +809,68 @@ GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
   return GradX{E.gptr(t), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 }
 
+// ---- PHX_CKSUM diagnostics -----------------------------------------------------------------
+// Read per call, so one process can compare a one-stream step with concurrent ones op by op: the
+// first checksum that differs between two steps on the same inputs names the launch whose inputs
+// still agreed and whose output did not.
+bool cksum_env() {
+  const char* e = std::getenv("PHX_CKSUM");
+  return e && e[0] == '1';
+}
+
+void ck_begin(Exec& E, hipStream_t s) {
+  E.ck_on = cksum_env();
+  E.ck_names.clear();
+  if (!E.ck_on) return;
+  if (!E.ck) {
+    E.ck_cap = 8 * E.prog.ops.size() + 256;
+    E.ck = E.alloc<unsigned long long>(E.ck_cap);
+  }
+  PHX_HIP(hipMemsetAsync(E.ck, 0, E.ck_cap * sizeof(unsigned long long), s));
+}
+
+void ck_note(Exec& E, const std::string& name, const void* p, size_t bytes, hipStream_t s) {
+  if (!E.ck_on || !p || E.ck_names.size() >= E.ck_cap) return;
+  launch_cksum(p, bytes, E.ck + E.ck_names.size(), s);
+  E.ck_names.push_back(name);
+}
+
+// what forward op i wrote (every member, for a grouped launch)
+void ck_fwd(Exec& E, int i, int pass, hipStream_t s) {
+  if (!E.ck_on) return;
+  const Program& P = E.prog;
+  const Op& op = P.ops[i];
+  if (E.fuse_folded[i]) return;
+  const std::string nm = "p" + std::to_string(pass) + " f " + std::to_string(i) + " " + op.name;
+  const Tensor& ti = P.tensors[op.in[0]];
+  if (op.t == OP_BN) {
+    ck_note(E, nm + " mean", E.slot_a[op.slot], ti.c * 4, s);
+    ck_note(E, nm + " rstd", E.slot_b[op.slot], ti.c * 4, s);
+    ck_note(E, nm + " scale", E.slot_c[op.slot], ti.c * 4, s);
+  } else if (op.t == OP_SE) {
+    ck_note(E, nm + " excite", E.slot_c[op.slot], (size_t)E.B * ti.c * 4, s);
+  } else {
+    const Tensor& to = P.tensors[op.out];
+    ck_note(E, nm + " out", E.tptr(op.out, nullptr), to.numel() * (E.tbf(op.out) ? 2 : 4), s);
+  }
+}
+
+// what backward op i wrote: its inputs' gradients (BN: the backward means)
+void ck_bwd(Exec& E, int i, hipStream_t s) {
+  if (!E.ck_on) return;
+  const Program& P = E.prog;
+  const Op& op = P.ops[i];
+  const std::string nm = "b " + std::to_string(i) + " " + op.name;
+  if (op.t == OP_BN) {
+    const int C = P.tensors[op.in[0]].c;
+    ck_note(E, nm + " mdz", E.slot_d[op.slot], C * 4, s);
+    ck_note(E, nm + " mdzx", E.slot_e[op.slot], C * 4, s);
+    return;
+  }
+  for (int k = 0; k < op.nin; ++k)
+    if (const float* g = E.gptr(op.in[k])) ck_note(E, nm + " d" + std::to_string(k), g, P.tensors[op.in[k]].numel() * 4, s);
+}
+
 // ---- level-batched heads -----------------------------------------------------------------
 bool grouping_enabled() {
   static const bool on = [] {
@@ -982,7 +1055,8 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                           E.tptr(op.out, input), (int)P.tensors[op.in[0]].rows(), false, sink_of(r), GradSink{}};
       }
       int np[kMaxSeg];  // each member's statistics partial rows
-      gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s, E.bf16, np);
+      gemm_group_run(mode, segs, n, ctx->wt_of(o0.w), to0.c, ti0.c, s, E.bf16, np,
+                     std::min<long>((long)(E.sp_region / to0.c), (long)E.sc_region));
       if (sink_on)
         for (int r = 0; r < n; ++r) {
           E.stat_P[P.ops[g[r]].out] = np[r];
@@ -1079,7 +1153,7 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
       }
       // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
       int np[kMaxSeg];  // each member's BN-backward-sum partial rows
-      gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s, E.bf16, np);
+      gemm_group_run(mode, segs, n, W + o0.w, ti0.c, to0.c, s, E.bf16, np, (long)(E.sp_region / ti0.c));
       if (gs_on)
         for (int r = 0; r < n; ++r) {
           E.gstat_P[g[r] - 1] = np[r];
@@ -1134,7 +1208,10 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
       h();
     }
     if (E.grp_of[i] >= 0) {
-      if (E.groups[E.grp_of[i]].front() == (int)i) run_group_fwd(ctx, E, E.grp_of[i], input, s, frozen);
+      if (E.groups[E.grp_of[i]].front() == (int)i) {
+        run_group_fwd(ctx, E, E.grp_of[i], input, s, frozen);
+        for (int m : E.groups[E.grp_of[i]]) ck_fwd(E, m, pass, s);
+      }
       continue;
     }
     if (E.fuse_folded[i]) continue;  // computed by the depthwise conv that follows
@@ -1259,6 +1336,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
       E.stat_P[op.out] = np;
       E.stat_region[op.out] = 0;
     }
+    ck_fwd(E, (int)i, pass, s);
   }
 }
 
@@ -1303,7 +1381,10 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     if (!op.bwd) continue;
     if (op.t == OP_PW && is_cls_out(P, op.out)) continue;  // handled by the scatter
     if (E.grp_of[i] >= 0) {
-      if (E.groups[E.grp_of[i]].back() == i) run_group_bwd(ctx, E, E.grp_of[i], input, s);
+      if (E.groups[E.grp_of[i]].back() == i) {
+        run_group_bwd(ctx, E, E.grp_of[i], input, s);
+        for (int m : E.groups[E.grp_of[i]]) ck_bwd(E, m, s);
+      }
       continue;
     }
     const Tensor& ti = P.tensors[op.in[0]];
@@ -1439,6 +1520,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     if (gsk.part && np != E.gstat_P[i - 1])
       throw std::logic_error("BN backward sums: planned and launched partial counts differ");
     if (gsk.part) E.gstat_region[i - 1] = 0;
+    ck_bwd(E, i, s);
   }
 }
 
@@ -1980,6 +2062,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   Exec& E = ctx->exec_for(B);
   ctx->last = &E;
   PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
+  ck_begin(E, s);
   const bool inject = boxes != nullptr;
   // Injected placement: the first pass only feeds the ASR denominator (and the moving statistics),
   // so it runs on a second stream beside the second pass and the backward, on its own executor
@@ -2023,9 +2106,11 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
     E1.defer_mov = true;
     PHX_HIP(hipEventRecord(ctx->ev_fork, s));
     PHX_HIP(hipStreamWaitEvent(s1, ctx->ev_fork, 0));
+    ck_begin(E1, s1);
     run_forward(ctx, E1, images, s1, 0, step, gimg0);
     E1.defer_mov = false;
     run_pre_nms(ctx, E1, s1, 2);
+    ck_note(E1, "p0 scores", E1.scores, (size_t)B * ctx->A * 4, s1);
     run_nms(ctx, E1, 2, E1.nms1_boxes, E1.nms1_scores, E1.nms1_count, s1);
     launch_count_ge(E1.nms1_scores, E1.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s1);
     PHX_HIP(hipEventRecord(ctx->ev_join, s1));
@@ -2051,7 +2136,8 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
         // out different (every score ~2e-2 off; never in fp32 or at 512^2; root cause not found,
         // DESIGN.md section 12).  Forking at 35-98 % of the ops gave bit-identical back-to-back
         // steps in every trial, and at half the ops C4 takes the same time (28.86 ms).
-        if (E.abf) ctx->fwd_hook_at = std::max(ctx->fwd_hook_at, E.prog.ops.size() / 2);
+        const char* hf = std::getenv("PHX_BF16_HALF_FORK");
+        if (E.abf && !(hf && hf[0] == '0')) ctx->fwd_hook_at = std::max(ctx->fwd_hook_at, E.prog.ops.size() / 2);
       }
     }
   } else {
@@ -2069,6 +2155,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   eot_forward(ctx, E, images, B, inject ? E.inj_boxes : E.nms1_boxes,
               inject ? E.inj_count : E.nms1_count, params, step, gimg0, s);
   launch_eot_count(E.ed, E.place, metrics, s);
+  ck_note(E, "eot patched", E.patched, (size_t)B * ctx->mc.image_size * ctx->mc.image_size * 12, s);
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);
   if (ctx->fwd_hook) {
@@ -2078,6 +2165,8 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   }
   E.defer_mov = false;
   run_pre_nms(ctx, E, s, 1);
+  ck_note(E, "p1 scores", E.scores, (size_t)B * ctx->A * 4, s);
+  ck_note(E, "p1 keep", E.keep, (size_t)B * ctx->A, s);
   // 5. ASR metric: soft-NMS over second-pass person boxes (attacker.py:203-205).  It reads the
   // pre_nms outputs only (the backward reads them too, nothing writes them until the next step),
   // so it runs on the side stream beside the backward and joins at the end of the step
@@ -2091,6 +2180,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   }
   launch_image_max(E.scores, E.keep, B, ctx->A, E.mraw, E.argm, E.nties, E.imax_scratch, s);
   launch_loss(E.mraw, B, params, E.dm, grad + PHX_NPATCH, metrics, s);
+  ck_note(E, "image max", E.mraw, (size_t)B * 4, s);
   // 4. victim data-gradient -> d(patched images)
   run_backward(ctx, E, E.patched, s);
   if (!side_nms) {
@@ -2106,6 +2196,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   launch_eot_resize_bwd(d, E.place, E.spans, E.dstore, E.rstore, E.dmatched, s);
   launch_eot_patch_bwd(d, params, E.img, E.ymean, E.dmatched, E.dsum, grad, add_tv != 0, s);
   launch_tv(params, PHX_PATCH_SIZE, E.tvs, metrics, add_tv != 0, s);
+  ck_note(E, "grad", grad, (size_t)(PHX_NPATCH + 1) * 4, s);
   if (fork || side_nms) PHX_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
   if (fork) launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), E1p->side, E.side, s);
   if (guard_bytes()) check_guards(ctx, s);
@@ -2255,6 +2346,35 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
     return PHX_OK;
   }
   throw std::invalid_argument(std::string("tap: no op named ") + op_name);
+  PHX_CATCH(ctx)
+}
+
+int phx_debug_checksums(phx_ctx* ctx, int tag, char* buf, size_t cap, size_t* needed) {
+  if (!ctx || ctx->execs.empty()) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->last) throw std::logic_error("no step has run");
+  Exec* E = nullptr;
+  for (auto& e : ctx->execs)
+    if (e->B == ctx->last->B && e->tag == tag) E = e.get();
+  if (!E) throw std::invalid_argument("checksums: no executor with this tag");
+  std::string out;
+  if (E->ck && !E->ck_names.empty()) {
+    PHX_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(E->ck_names.size());
+    PHX_HIP(hipMemcpy(h.data(), E->ck, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    char v[32];
+    for (size_t i = 0; i < h.size(); ++i) {
+      snprintf(v, sizeof v, "%016llx", h[i]);
+      out += E->ck_names[i] + "\t" + v + "\n";
+    }
+  }
+  if (needed) *needed = out.size() + 1;
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, out.size());
+    memcpy(buf, out.data(), n);
+    buf[n] = 0;
+  }
+  return PHX_OK;
   PHX_CATCH(ctx)
 }
 

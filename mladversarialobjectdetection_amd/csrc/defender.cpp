@@ -207,9 +207,12 @@ struct phx_def {
     js << "]}";
     return js.str();
   }
-  // evaluation Masker (the attacker's 640^2 patch), part of workspace(B)
+  // evaluation Masker (the attacker's 640^2 patch): reserved by the first evaluation of a workspace
+  // (eval_reserve), freed with it
   float *ematched = nullptr, *erstore = nullptr;
   int eB = 0;
+  size_t eval_bytes(int B) const;
+  void eval_reserve(int B);
 
   void workspace(int B);
   void prep_weights(const float* W, hipStream_t s);
@@ -361,13 +364,23 @@ void phx_def::workspace(int B) {
   count = alloc<int>(B);
   info = alloc<int>((size_t)B * 3);
   eerr = alloc<int>(1);
-  // evaluation Masker (the attacker's 640^2 patch): reserved here with the rest of the batch's
-  // workspace, so phx_def_workspace_bytes is the whole footprint before the first evaluation and a
-  // rebuild for another batch size never leaves them dangling.  Placement side <= floor(longer side
-  // * scale) <= S for scale in [0, 1] (the attacker's clip); soft-NMS may return 100 overlapping
-  // image-sized boxes, so the R store keeps the worst case.
-  ematched = F((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3);
-  erstore = F((size_t)B * PHX_MAX_OUT * S_ * S_ * 3);
+  // the evaluation Masker's buffers are reserved by the first evaluation (eval_reserve): a run that
+  // only trains never holds them; this rebuild freed any earlier ones with the rest of `owned`
+  ematched = erstore = nullptr;
+  eB = 0;
+}
+
+// evaluation Masker (the attacker's 640^2 patch) buffers for the current workspace batch size.
+// Placement side <= floor(longer side * scale) <= S for scale in [0, 1] (the attacker's clip);
+// soft-NMS may return 100 overlapping image-sized boxes, so the R store keeps the worst case.
+size_t phx_def::eval_bytes(int B) const {
+  return ((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3 + (size_t)B * PHX_MAX_OUT * S * S * 3) * sizeof(float);
+}
+
+void phx_def::eval_reserve(int B) {
+  if (eB == B && ematched && erstore) return;
+  ematched = alloc<float>((size_t)B * PHX_PATCH_SIZE * PHX_PATCH_SIZE * 3);
+  erstore = alloc<float>((size_t)B * PHX_MAX_OUT * S * S * 3);
   eB = B;
 }
 
@@ -628,7 +641,7 @@ void phx_def::eval(const float* images, int B, const float* boxes_in, const int*
   e2.P = PHX_PATCH_SIZE;
   // placement side <= floor(longer side * scale) <= S for scale in [0, 1] (the attacker's clip)
   e2.rcap = (long)B * PHX_MAX_OUT * S * S * 3;
-  if (eB != B || !ematched || !erstore) throw std::logic_error("defender evaluation buffers not reserved");
+  eval_reserve(B);
   prep_weights(W, s);
   const float* bx = boxes_in;
   const int* cn = count_in;
@@ -740,6 +753,12 @@ int phx_def_workspace_bytes(phx_def* d, int B, size_t* bytes) {
   *bytes = d->ws_bytes;
   return PHX_OK;
   DEF_CATCH(d)
+}
+
+int phx_def_eval_workspace_bytes(phx_def* d, int B, size_t* bytes) {
+  if (!d || !bytes || B <= 0 || B > d->max_batch) return PHX_EINVAL;
+  *bytes = d->eval_bytes(B);
+  return PHX_OK;
 }
 
 int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,

@@ -107,8 +107,10 @@ struct GemmSeg {
   GradSink gsk;
 };
 bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16 = false);
+// max_part_rows >= 0: the partial rows one member's region holds (throws before launching if any
+// member would write more)
 int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s,
-                   bool bf16 = false, int* P_out = nullptr);
+                   bool bf16 = false, int* P_out = nullptr, long max_part_rows = -1);
 // depthwise k x k, stride s, TF SAME: x [B,H,W,C] -> y [B,Ho,Wo,C]; w [k,k,C]
 int launch_dw_fwd(InX x, const float* w, float* y, int B, int H, int W, int C, int Ho,
                   int Wo, int k, int stride, int pt, int pl, hipStream_t s,
@@ -229,6 +231,9 @@ void launch_drop_keep(const int* block, const float* p, int nd, int B, uint64_t 
                       int gimg0, int pass, float* keep, hipStream_t s);
 // dst[n] (fp32) = src[n] (bf16 storage)
 void launch_bf16_to_f32(const float* src, float* dst, long n, hipStream_t s);
+// *out += an order-independent 64-bit hash of the bytes (PHX_CKSUM diagnostics; *out zeroed by the
+// caller)
+void launch_cksum(const void* p, size_t bytes, unsigned long long* out, hipStream_t s);
 // y = drop(a) + b
 void launch_add(InX a, InX b, float* y, long n, int C, hipStream_t s, DropView dv = DropView{});
 // dst (+)= drop'(src); with a GradSink (C channels) the BN-backward sums of the result come along

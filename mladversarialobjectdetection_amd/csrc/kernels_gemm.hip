@@ -216,7 +216,7 @@ bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16) {
 }
 
 int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N, int K, hipStream_t s,
-                   bool bf16, int* P_out) {
+                   bool bf16, int* P_out, long max_part_rows) {
   std::vector<int> M(n);
   for (int i = 0; i < n; ++i) M[i] = segs[i].M;
   if (!gemm_group_ok(M.data(), n, N, K, bf16)) throw std::runtime_error("gemm group: unsupported shapes");
@@ -242,6 +242,11 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
     P = std::max(P, Pm[i]);
     if (P_out) P_out[i] = Pm[i];
   }
+  // every member's partial rows must fit its region of the caller's partial buffer (sized from each
+  // op's own plan): a member planned with another member's tile must not spill into the next region,
+  // where two workgroups of this launch would then race for the same partials
+  if ((stats || gs) && max_part_rows >= 0 && P > max_part_rows)
+    throw std::logic_error("gemm group: a member's partial rows exceed its region");
   for (int i = 0; i < n; ++i) {
     const GemmSeg& g = segs[i];
     if ((g.sink.part != nullptr) != stats || (g.gsk.part != nullptr) != gs)

@@ -1117,6 +1117,33 @@ void launch_bf16_to_f32(const float* src, float* dst, long n, hipStream_t s) {
   PHX_LAUNCH_CHECK();
 }
 
+// PHX_CKSUM diagnostics: an order-independent hash of n 16-bit words (sum over i of a mix of
+// (word, i), wrapping 64-bit integer adds), so the value does not depend on how the grid splits the
+// buffer and any single changed bit changes it
+__device__ __forceinline__ unsigned long long ck_mix(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+__global__ void k_cksum(const uint16_t* __restrict__ p, long n, unsigned long long* __restrict__ out) {
+  unsigned long long h = 0;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    h += ck_mix(((unsigned long long)i << 16) ^ p[i] ^ 0x9e3779b97f4a7c15ull);
+  for (int o = 32; o > 0; o >>= 1) h += __shfl_xor(h, o);
+  if ((threadIdx.x & 63) == 0 && h) atomicAdd(out, h);
+}
+
+void launch_cksum(const void* p, size_t bytes, unsigned long long* out, hipStream_t s) {
+  const long n = (long)(bytes / 2);
+  if (!p || n == 0) return;
+  hipLaunchKernelGGL(k_cksum, dim3((unsigned)std::min<long>(cdiv(n, 256), 2048)), dim3(256), 0, s,
+                     reinterpret_cast<const uint16_t*>(p), n, out);
+  PHX_LAUNCH_CHECK();
+}
+
 // drop connect keep flags: tf.floor(survival + tf.random.uniform([B,1,1,1])) per block and image
 __global__ void k_drop_keep(const int* __restrict__ block, const float* __restrict__ p, int nd, int B,
                             uint64_t seed, int64_t step, int gimg0, int pass,

@@ -280,11 +280,10 @@ static NmsPlan nms_plan(int N) {
   p.lp = 4;  // >= 4: the list boxes after the u32 payload stay 16-B aligned
   while (p.lp < std::min(N, kNmsTopMax)) p.lp <<= 1;
   const int fast = std::max(p.lp * 8, kNmsHistBins * 4) + p.lp * 4 + p.lp * 16 + kNmsSelBytes;
-  // PHX_NMS_FAST=0: the general queue only (A/B and diagnosis)
-  static const bool fast_on = [] {
-    const char* e = std::getenv("PHX_NMS_FAST");
-    return !(e && e[0] == '0');
-  }();
+  // PHX_NMS_FAST=0: the general queue only (A/B and diagnosis; read per call, so one process can
+  // compare both paths bit for bit)
+  const char* fe = std::getenv("PHX_NMS_FAST");
+  const bool fast_on = !(fe && fe[0] == '0');
   p.qrows = fast_on ? std::max(0, std::min(64, (kNmsLdsBytes - fixed - p.ck_bytes - fast) / kNmsRowBytes)) : 0;
   p.lds = std::max(p.lds, fixed + p.ck_bytes + fast + p.qrows * kNmsRowBytes);
   p.lds = (p.lds + 15) / 16 * 16;

@@ -64,6 +64,26 @@ def test_soft_nms_semantics():
     assert sel.tolist() == [0, 1, 2, 3]
 
 
+def test_soft_nms_exact_duplicates_are_decayed_not_hard_suppressed():
+    """postprocess.nms's gaussian branch passes iou_threshold = 1.0 to NonMaxSuppressionV5
+    (postprocess.py:184-200).  TF's kernel (non_max_suppression_op.cc, DoNonMaxSuppressionOp)
+    hard-suppresses only when soft_nms_sigma == 0 (`!is_soft_nms && similarity >
+    similarity_threshold`); with sigma 0.25 every overlap, an exact duplicate at IoU 1.0 included,
+    only scales the score by exp(-2 * iou^2) and the candidate is re-queued while above the
+    threshold.  So at the NMS threshold 0.001 (score_thresh 0) duplicates are selected again with
+    decayed scores, and at 0.5 they drop out."""
+    bx = np.array([[0, 0, 10, 10]] * 3 + [[50, 50, 60, 60]], np.float32)
+    sc = np.array([0.9, 0.8, 0.7, 0.6], np.float32)
+    sel, ss = pp.soft_nms(bx, sc, 100, 0.001, 0.25)
+    e2 = np.float32(np.exp(np.float32(-2.0)))
+    assert sel.tolist() == [0, 3, 1, 2]
+    np.testing.assert_array_equal(ss[1], sc[3])
+    np.testing.assert_array_equal(ss[2], np.float32(sc[1] * e2))
+    np.testing.assert_array_equal(ss[3], np.float32(np.float32(sc[2] * e2) * e2))
+    sel, _ = pp.soft_nms(bx, sc, 100, 0.5, 0.25)
+    assert sel.tolist() == [0, 3]
+
+
 def test_valid_mask():
     bx = np.array([[0, 0, 20, 20], [0, 0, 5, 30], [-10, 0, 600, 20], [0, 0, 10, 10]], np.float32)
     m = pp.valid_mask(bx, 512, 512, np.array([0.9, 0.9, 0.9, 0.4], np.float32), 0.5)
