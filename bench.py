@@ -153,6 +153,10 @@ def main():
                          "(C4: bf16 matrix cores, fp32 accumulation)")
     ap.add_argument("--person-bias", type=float, default=0.0,
                     help="lift the person class-logit bias so the clean pass yields real soft-NMS candidates")
+    ap.add_argument("--draw", choices=("auto", "standard", "well-conditioned"), default="auto",
+                    help="synthetic weight draw: standard = SURVEY.md 8d; well-conditioned = weights.WELL_CONDITIONED "
+                         "(the draw test_bf16_d4_1024_four_images validates C4 on); auto = well-conditioned for "
+                         "D4 bf16, standard otherwise")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary line (the reference's own placement flow, measured after the headline)")
     args = ap.parse_args()
@@ -168,8 +172,19 @@ def main():
 
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim, PatchAttacker, _pad_boxes
     B, S = args.batch, args.image_size
-    victim = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
-                                device=local, person_bias=args.person_bias, dtype=args.dtype)
+    draw = args.draw
+    if draw == "auto":
+        draw = "well-conditioned" if (args.model == "efficientdet-d4" and args.dtype == "bf16") else "standard"
+    if draw == "well-conditioned":
+        # the parity test's configuration: its weights, its EOT key (rng_seed 5), its images and boxes
+        from mladversarialobjectdetection_amd import _lib
+        from mladversarialobjectdetection_amd import weights as wmod
+        wts = wmod.well_conditioned_blob(_lib.Context(args.model, S, 1).manifest())
+        victim = EfficientDetVictim(args.model, wts, image_size=S, max_batch=B, rng_seed=5, device=local,
+                                    dtype=args.dtype)
+    else:
+        victim = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
+                                    device=local, person_bias=args.person_bias, dtype=args.dtype)
     att = PatchAttacker(victim, seed=7, device=dev)
     gidx = list(range(rank * B, (rank + 1) * B))
     images = torch.as_tensor(synth_images(gidx, S), device=dev)
@@ -301,7 +316,10 @@ def main():
             "dtype": args.dtype,
             "data": ("synthetic (U(-1,1) images, " + ("1-3 injected person boxes/image" if boxes is not None else
                      "placement from the first pass's soft-NMS boxes") + f", synthetic {args.model} weights"
-                     + (f", person_bias {args.person_bias}" if args.person_bias else "") + ")"),
+                     + (f", person_bias {args.person_bias}" if args.person_bias and draw == "standard" else "")
+                     + (", well-conditioned draw (gamma U(0.2,0.4), beta N(1,0.1), person prior 3, EOT key 5): "
+                        "the configuration test_bf16_d4_1024_four_images checks" if draw == "well-conditioned"
+                        else "") + ")"),
             "config": {"workload": (f"C{2 if world == 1 else 3}: EfficientDet-D0" if args.model == "efficientdet-d0"
                                     else ("C4: " if args.model == "efficientdet-d4" else "") + args.model)
                                    + f" patch attack {S}x{S}, "

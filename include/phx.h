@@ -260,6 +260,9 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
  * (synchronising); *needed = bytes including the NUL.  Two steps on the same inputs must give the
  * same list; the first differing line names the launch that broke. */
 int phx_debug_checksums(phx_ctx* ctx, int tag, char* buf, size_t cap, size_t* needed);
+/* The raw storage (bf16 words in a PHX_DTYPE_BF16 context) of op `op_index`'s output (which = 0) or
+ * input which - 1 in the last step's executor `tag`; nbytes must equal its size (device->device). */
+int phx_debug_tensor(phx_ctx* ctx, int tag, int op_index, int which, void* out, size_t nbytes, void* stream);
 
 /* ---- defender step (BASELINE C5) ------------------------------------------
  * attack_detection.PatchAttackDefender (attack_detection.py:31-206, training) over a frozen

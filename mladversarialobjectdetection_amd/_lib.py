@@ -94,6 +94,7 @@ _SIGS = [
     ("phx_debug_last_image_grad", c_int, [c_void_p, c_void_p, c_void_p]),
     ("phx_debug_tap", c_int, [c_void_p, c_char_p, c_int, c_void_p, c_size_t, c_void_p]),
     ("phx_debug_checksums", c_int, [c_void_p, c_int, c_char_p, c_size_t, POINTER(c_size_t)]),
+    ("phx_debug_tensor", c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_size_t, c_void_p]),
     # defender step
     ("phx_def_create", c_int, [c_void_p, c_int, c_uint64, POINTER(c_void_p)]),
     ("phx_def_destroy", None, [c_void_p]),

@@ -33,6 +33,11 @@ T* dalloc(size_t n) {
   if (n == 0) n = 1;
   void* p = nullptr;
   PHX_HIP(hipMalloc(&p, n * sizeof(T)));
+  static const bool log = [] {
+    const char* e = std::getenv("PHX_ALLOC_LOG");
+    return e && e[0] == '1';
+  }();
+  if (log) fprintf(stderr, "phx alloc %p %zu\n", p, n * sizeof(T));
   return reinterpret_cast<T*>(p);
 }
 
@@ -855,6 +860,13 @@ void ck_fwd(Exec& E, int i, int pass, hipStream_t s) {
   }
 }
 
+// the forward outputs of pass `pass` once more, as "post <name>" (after the step's join)
+void ck_post(Exec& E, int pass, hipStream_t s) {
+  const size_t n0 = E.ck_names.size();
+  for (size_t i = 0; i < E.prog.ops.size(); ++i) ck_fwd(E, (int)i, pass, s);
+  for (size_t k = n0; k < E.ck_names.size(); ++k) E.ck_names[k] = "post " + E.ck_names[k];
+}
+
 // what backward op i wrote: its inputs' gradients (BN: the backward means)
 void ck_bwd(Exec& E, int i, hipStream_t s) {
   if (!E.ck_on) return;
@@ -1201,6 +1213,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train || force_frozen;
   if (E.ndrop && train)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
+  if (E.ndrop && train) ck_note(E, "p" + std::to_string(pass) + " drop keep", E.drop_keep, (size_t)E.ndrop * E.B * 4, s);
   for (size_t i = 0; i < P.ops.size(); ++i) {
     if (ctx->fwd_hook && i == ctx->fwd_hook_at) {
       auto h = std::move(ctx->fwd_hook);
@@ -1311,10 +1324,24 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
                       W + op.b2, op.act, E.slot_a[op.slot], E.slot_b[op.slot], E.slot_c[op.slot], s,
                       E.red);
         break;
-      case OP_ADD:
+      case OP_ADD: {
+        static const bool no_drop = [] {  // PHX_NO_DROP=1: diagnostics only (not the reference's step)
+          const char* e = std::getenv("PHX_NO_DROP");
+          return e && e[0] == '1';
+        }();
+        const DropView dv = (train && !no_drop) ? drop_view(E, (int)i) : DropView{};
+        if (E.ck_on) {  // what the add is about to read (PHX_CKSUM)
+          const std::string nm = "p" + std::to_string(pass) + " f " + std::to_string(i) + " add in ";
+          for (int k = 0; k < 2; ++k) {
+            const Tensor& tk = P.tensors[op.in[k]];
+            ck_note(E, nm + std::to_string(k), E.tptr(op.in[k], input), tk.numel() * (E.tbf(op.in[k]) ? 2 : 4), s);
+          }
+          if (dv.keep) ck_note(E, nm + "keep", dv.keep, (size_t)E.B * 4, s);
+        }
         launch_add(view(ctx, E, op.in[0], input), view(ctx, E, op.in[1], input), y,
-                   (long)to.numel(), to.c, s, train ? drop_view(E, (int)i) : DropView{});
+                   (long)to.numel(), to.c, s, dv);
         break;
+      }
       case OP_MAXPOOL:
         launch_maxpool_fwd(view(ctx, E, op.in[0], input), y, E.pool_amax[i], ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k, op.stride, op.pad_t,
                            op.pad_l, s);
@@ -2131,13 +2158,6 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
             ctx->fwd_hook_at = i;
             break;
           }
-        // bf16 activations: not before half the ops.  With the side pass's first (1024^2 bf16)
-        // layers beside the second pass's stages 6-7, about one D4 bf16 1024^2 step in five came
-        // out different (every score ~2e-2 off; never in fp32 or at 512^2; root cause not found,
-        // DESIGN.md section 12).  Forking at 35-98 % of the ops gave bit-identical back-to-back
-        // steps in every trial, and at half the ops C4 takes the same time (28.86 ms).
-        const char* hf = std::getenv("PHX_BF16_HALF_FORK");
-        if (E.abf && !(hf && hf[0] == '0')) ctx->fwd_hook_at = std::max(ctx->fwd_hook_at, E.prog.ops.size() / 2);
       }
     }
   } else {
@@ -2199,6 +2219,12 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   ck_note(E, "grad", grad, (size_t)(PHX_NPATCH + 1) * 4, s);
   if (fork || side_nms) PHX_HIP(hipStreamWaitEvent(s, ctx->ev_join, 0));
   if (fork) launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), E1p->side, E.side, s);
+  if (E.ck_on) {
+    // every forward tensor once more after the join: a tensor whose hash changed after its producer
+    // was overwritten later in the step (PHX_CKSUM)
+    ck_post(E, 1, s);
+    if (fork) ck_post(*E1p, 0, s);
+  }
   if (guard_bytes()) check_guards(ctx, s);
   return PHX_OK;
   PHX_CATCH(ctx)
@@ -2346,6 +2372,26 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
     return PHX_OK;
   }
   throw std::invalid_argument(std::string("tap: no op named ") + op_name);
+  PHX_CATCH(ctx)
+}
+
+int phx_debug_tensor(phx_ctx* ctx, int tag, int op_index, int which, void* out, size_t nbytes, void* stream) {
+  if (!ctx || !out || ctx->execs.empty()) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (!ctx->last) throw std::logic_error("no step has run");
+  Exec* E = nullptr;
+  for (auto& e : ctx->execs)
+    if (e->B == ctx->last->B && e->tag == tag) E = e.get();
+  if (!E) throw std::invalid_argument("tensor: no executor with this tag");
+  if (op_index < 0 || op_index >= (int)E->prog.ops.size() || which < 0 || which > 2)
+    throw std::invalid_argument("tensor: bad op index / which");
+  const Op& op = E->prog.ops[op_index];
+  const int t = which == 0 ? op.out : op.in[which - 1];
+  if (t < 0 || t == E->prog.input) throw std::invalid_argument("tensor: no such arena tensor");
+  const size_t nb = E->prog.tensors[t].numel() * (E->tbf(t) ? 2 : 4);
+  if (nb != nbytes) throw std::invalid_argument("tensor: size mismatch (" + std::to_string(nb) + " bytes)");
+  PHX_HIP(hipMemcpyAsync(out, E->tptr(t, nullptr), nb, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return PHX_OK;
   PHX_CATCH(ctx)
 }
 

@@ -72,6 +72,30 @@ __device__ __forceinline__ float round_bf16(float f) {
 }
 
 // ------------------------------------------------------------------------------------------
+// n / d for a drop-connect survival probability d in (2^-20, 1], correctly rounded as IEEE division
+// (TF's `inputs / survival_prob`, utils.py:336-344), without v_div_scale / v_div_fmas.  hipcc lowers
+// `/` to that sequence, whose v_div_fmas reads VCC; in the residual adds of a bf16 D4 step running
+// beside the side stream's first pass it produced results scaled by 2^-64 for whole 16-lane groups
+// (scripts/diag_add.py).  This is the same Newton sequence without the scaling and
+// fix-up steps, which only act when |n| < 2^-103 or |n / d| nears the exponent limits: those (and
+// 0, inf, nan) keep the plain division, so every result equals n / d bit for bit.
+// PHX_DROP_HWDIV=1 (build flag) restores the plain division everywhere (A/B diagnostics).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float div_surv(float n, float d) {
+#if defined(PHX_DROP_HWDIV) && PHX_DROP_HWDIV
+  return n / d;
+#else
+  const float a = fabsf(n);
+  if (!(a >= 0x1p-100f && a <= 0x1p100f)) return n == 0.f ? n : n / d;
+  float r = __builtin_amdgcn_rcpf(d);
+  r = fmaf(fmaf(-d, r, 1.f), r, r);
+  float q = n * r;
+  q = fmaf(fmaf(-d, q, n), r, q);
+  return fmaf(fmaf(-d, q, n), r, q);
+#endif
+}
+
+// ------------------------------------------------------------------------------------------
 // Activation storage.  A PHX_DTYPE_BF16 context stores every activation (the arena tensors: conv /
 // depthwise / fuse / resample / add outputs, i.e. the BN inputs) as bf16 — SURVEY.md 8a R4 "C4:
 // bf16 act, fp32 acc" — while gradients, statistics, EOT and the images stay fp32.  Kernels take the

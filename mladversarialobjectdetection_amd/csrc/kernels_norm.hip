@@ -1081,11 +1081,13 @@ int launch_se_bwd(const float* dy, InX x, float* dx, int B, int HW, int C, int C
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ float4 drop_fwd4(const DropView& dv, long row, float4 u) {
   const float k = dv.keep[row / dv.rows];
-  return make_float4((u.x / dv.p) * k, (u.y / dv.p) * k, (u.z / dv.p) * k, (u.w / dv.p) * k);
+  return make_float4(div_surv(u.x, dv.p) * k, div_surv(u.y, dv.p) * k, div_surv(u.z, dv.p) * k,
+                     div_surv(u.w, dv.p) * k);
 }
 __device__ __forceinline__ float4 drop_bwd4(const DropView& dv, long row, float4 g) {
   const float k = dv.keep[row / dv.rows];
-  return make_float4((g.x * k) / dv.p, (g.y * k) / dv.p, (g.z * k) / dv.p, (g.w * k) / dv.p);
+  return make_float4(div_surv(g.x * k, dv.p), div_surv(g.y * k, dv.p), div_surv(g.z * k, dv.p),
+                     div_surv(g.w * k, dv.p));
 }
 
 template <bool BF>

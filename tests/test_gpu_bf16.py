@@ -138,8 +138,7 @@ def _well_conditioned_d4(S):
     0.999998): there the C4 tolerance constrains the result."""
     from mladversarialobjectdetection_amd import _lib
     from mladversarialobjectdetection_amd import weights as W
-    return W.synthetic_blob(_lib.Context("efficientdet-d4", S, 1).manifest(), seed=0, person_bias=3.0,
-                            gamma=(0.2, 0.4), beta=(1.0, 0.1))
+    return W.well_conditioned_blob(_lib.Context("efficientdet-d4", S, 1).manifest())
 
 
 @pytest.mark.timeout(900)
