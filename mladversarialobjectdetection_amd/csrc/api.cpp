@@ -83,6 +83,11 @@ struct Exec {
   std::vector<int> se_of_tensor;               // tensor id -> SE op index producing it (-1)
   // BiFPN node fuse folded into the depthwise conv after it (computed on load, never written)
   std::vector<char> fuse_folded;               // op id of the fuse -> 1
+  // expand -> BN -> act -> depthwise fused (kernels_dw.hip): op id of the expand
+  // conv -> 1; the expand output is never stored in a training pass (ops i, i+1, i+2)
+  std::vector<char> xdw;
+  double* xdw_part = nullptr;                  // BN0 statistics partials
+  float* xdw_ref = nullptr;                    // BN0 statistics shift (y0 of row 0)
   std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
   std::vector<int> bn_consumer;                // tensor id -> BN op index reading it (-1)
   std::vector<float*> slot_d, slot_e;          // BN backward: mean(dz), mean(dz*xhat)
@@ -662,6 +667,44 @@ Exec& phx_ctx::exec_for(int B, int tag) {
       E.fuse_folded[i] = 1;
     }
   }
+  // expand -> depthwise fusion: fp32, batch statistics of the rank (bn=local), ungrouped, the expand
+  // output and BN0's output read only by the next op, BN1's statistics from the depthwise conv, and
+  // BN0's backward sums from its data gradient (PHX_XDW=1: on, default off — slower on C2, DESIGN
+  // §5; read per executor)
+  E.xdw.assign(P.ops.size(), 0);
+  {
+    const char* xe = std::getenv("PHX_XDW");
+    const bool on = xe && xe[0] == '1' && !E.abf && bn_mode == PHX_BN_LOCAL;
+    std::vector<int> nuse(P.tensors.size(), 0);
+    for (const Op& op : P.ops)
+      for (int j = 0; j < op.nin; ++j) ++nuse[op.in[j]];
+    size_t part_need = 1, ref_need = 1;
+    for (size_t i = 0; on && i + 3 < P.ops.size(); ++i) {
+      const Op& e = P.ops[i];
+      const Op& bn = P.ops[i + 1];
+      const Op& d = P.ops[i + 2];
+      if (e.t != OP_PW || bn.t != OP_BN || d.t != OP_DW || e.b >= 0 || e.nin != 1) continue;
+      if (bn.in[0] != e.out || d.in[0] != bn.out || nuse[e.out] != 1 || nuse[bn.out] != 1) continue;
+      if (E.grp_of[i] >= 0 || E.grp_of[i + 1] >= 0 || E.grp_of[i + 2] >= 0 || e.in[0] == P.input) continue;
+      const Tensor& tx = P.tensors[e.in[0]];
+      const Tensor& t0 = P.tensors[e.out];
+      if (!xdw_supported(tx.c, t0.c, d.k, d.stride, bn.act) || (d.k == 5 && d.stride == 1)) continue;
+      if (!E.fused_bn[i + 1] || !E.fused_bn[i + 3] || P.ops[i + 3].in[0] != d.out) continue;
+      if (d.bwd && (!bn.bwd || !E.gfused_bn[i + 1])) continue;
+      E.xdw[i] = 1;
+      part_need = std::max(part_need, xdw_stats_scratch_doubles((long)t0.rows(), t0.c));
+      ref_need = std::max(ref_need, (size_t)t0.c);
+      // x's BN takes its backward sums from the fused data gradient (one partial row per 8x8 tile)
+      if (e.bwd && i > 0 && E.gfused_bn[i - 1] && P.ops[i - 1].out == e.in[0]) {
+        E.gstat_P[i - 1] = xdw_dx_partials(tx.n, tx.h, tx.w);
+        sp_need = std::max(sp_need, (size_t)E.gstat_P[i - 1] * tx.c);
+      }
+    }
+    if (part_need > 1) {
+      E.xdw_part = E.alloc<double>(part_need);
+      E.xdw_ref = E.alloc<float>(ref_need);
+    }
+  }
   const size_t nreg = E.groups.empty() ? 1 : kMaxSeg;
   E.sp_region = sp_need;
   E.sc_region = sc_need;
@@ -812,6 +855,62 @@ GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
                  E.slot_c[op.slot], ctx->w() + op.beta, E.slot_d[op.slot], E.slot_e[op.slot], op.act, E.tbf(t)};
   }
   return GradX{E.gptr(t), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
+}
+
+// PHX_SKIP_TIMING=f,b,s (timing experiments only: wrong results): skip the forward BN finalizes (f),
+// the backward ones (b), the SE MLP launches (s) — what removing them would be worth at most
+bool skip_timing(char k) {
+  static const std::string v = [] {
+    const char* e = std::getenv("PHX_SKIP_TIMING");
+    return std::string(e ? e : "");
+  }();
+  return v.find(k) != std::string::npos;
+}
+
+// PHX_SKIP_KINDS=f:gemm,b:dw_bwd,...|name1,name2 (timing experiments only: wrong results): skip the
+// ungrouped launches of those kinds (f: forward, b: backward), or of ops whose name contains one of
+// the names after '|'
+bool skip_kind(const std::string& kind, const std::string& name) {
+  static const std::pair<std::vector<std::string>, std::vector<std::string>> v = [] {
+    std::pair<std::vector<std::string>, std::vector<std::string>> r;
+    const char* e = std::getenv("PHX_SKIP_KINDS");
+    std::string t = e ? e : "";
+    const size_t bar = t.find('|');
+    auto split = [](const std::string& x, std::vector<std::string>& out) {
+      size_t a = 0;
+      while (a < x.size()) {
+        size_t b = x.find(',', a);
+        if (b == std::string::npos) b = x.size();
+        if (b > a) out.push_back(x.substr(a, b - a));
+        a = b + 1;
+      }
+    };
+    split(t.substr(0, bar), r.first);
+    if (bar != std::string::npos) split(t.substr(bar + 1), r.second);
+    return r;
+  }();
+  if (v.first.empty() && v.second.empty()) return false;
+  for (const auto& k : v.first)
+    if (k == kind) return true;
+  for (const auto& n : v.second)
+    if (name.find(n) != std::string::npos) return true;
+  return false;
+}
+
+// the fused expand -> depthwise ops starting at expand op i (E.xdw[i])
+XdwArgs xdw_args(phx_ctx* ctx, const Exec& E, int i, const float* input) {
+  const Program& P = E.prog;
+  const Op& e = P.ops[i];
+  const Op& bn = P.ops[i + 1];
+  XdwArgs a{};
+  a.x = view(ctx, E, e.in[0], input);
+  a.we = ctx->w() + e.w;
+  a.bn0 = InX{nullptr, E.slot_a[bn.slot], E.slot_c[bn.slot], ctx->w() + bn.beta, bn.act, 0};
+  a.rs0 = E.slot_b[bn.slot];
+  a.mdz0 = E.slot_d[bn.slot];
+  a.mdzx0 = E.slot_e[bn.slot];
+  a.ce = P.tensors[e.out].c;
+  return a;
 }
 
 // ---- PHX_CKSUM diagnostics -----------------------------------------------------------------
@@ -1095,7 +1194,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            nullptr, nullptr, E.side_for(op.slot)};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, false, s);
-      else launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
+      else if (!skip_timing('f')) launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
       break;
     }
     default:
@@ -1184,7 +1283,7 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, true, s);
-      else launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
+      else if (!skip_timing('b')) launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
       break;
     }
     default:
@@ -1228,6 +1327,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
       continue;
     }
     if (E.fuse_folded[i]) continue;  // computed by the depthwise conv that follows
+    if (E.xdw[i] && !frozen) continue;  // the expand: recomputed by the fused statistics and depthwise
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
@@ -1247,6 +1347,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     const bool sink_on = !frozen && i + 1 < P.ops.size() && E.fused_bn[i + 1];
     const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0} : StatSink{};
     if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
+    if (skip_kind(std::string("f:") + kind, op.name)) continue;
     Scope scope(ctx, kind, fl, by, s, (prof_detail() || debug_sync()) ? op_tag(P, op, false) : std::string());
     int np = 0;
     switch (op.t) {
@@ -1270,6 +1371,12 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         break;
       }
       case OP_DW:
+        if (i >= 2 && E.xdw[i - 2] && !frozen) {
+          const XdwArgs xa = xdw_args(ctx, E, (int)i - 2, input);
+          np = launch_dw_fwd_x(xa, P.tensors[P.ops[i - 2].in[0]].c, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w,
+                               op.k, op.stride, op.pad_t, op.pad_l, sink, s);
+          break;
+        }
         if (i > 0 && E.fuse_folded[i - 1]) {
           const Op& f = P.ops[i - 1];
           FuseView fv{};
@@ -1294,12 +1401,18 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         if (frozen)
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
                                  E.slot_c[op.slot], ti.c, kBnEps, s);
-        else if (E.fused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
+        else if (i >= 1 && E.xdw[i - 1]) {
+          const XdwArgs xa = xdw_args(ctx, E, (int)i - 1, input);
+          launch_xdw_stats(xa, P.tensors[P.ops[i - 1].in[0]].c, (long)ti.rows(), E.xdw_part, E.xdw_ref, mean, rstd,
+                           W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s,
+                           E.side_for(op.slot));
+        } else if (E.fused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
           const BnFinSeg sg{E.spart + E.stat_region[op.in[0]] * E.sp_region,
                             E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]], (long)ti.rows(),
                             mean, rstd, W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, nullptr, nullptr,
                             E.side_for(op.slot)};
           sync_finalize(ctx, E, &sg, 1, ti.c, false, s);
+        } else if (E.fused_bn[i] && skip_timing('f')) {
         } else if (E.fused_bn[i])
           launch_bn_finalize(E.spart + E.stat_region[op.in[0]] * E.sp_region,
                              E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]],
@@ -1320,6 +1433,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         break;
       }
       case OP_SE:
+        if (skip_timing('s')) break;
         launch_se_fwd(view(ctx, E, op.in[0], input), nullptr, ti.n, ti.h * ti.w, ti.c, op.cse, W + op.w1, W + op.b1, W + op.w2,
                       W + op.b2, op.act, E.slot_a[op.slot], E.slot_b[op.slot], E.slot_c[op.slot], s,
                       E.red);
@@ -1445,6 +1559,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
       gsk_in = op.in[0] == bn.out ? 0 : 1;
     }
     if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
+    if (skip_kind(std::string("b:") + kind, op.name)) continue;
     Scope scope(ctx, kind, fl, by, s, (prof_detail() || debug_sync()) ? op_tag(P, op, true) : std::string());
     int np = -1;
     switch (op.t) {
@@ -1464,11 +1579,24 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       }
       case OP_PW:
+        if (E.xdw[i]) {  // the expand's data gradient from the depthwise output's, nothing stored between
+          const Op& d = P.ops[i + 2];
+          const Tensor& td = P.tensors[d.out];
+          np = launch_xdw_dx(xdw_args(ctx, E, i, input), ti.c, gview(ctx, E, d.out, input), W + d.w, dx, op.acc[0],
+                             ti.n, ti.h, ti.w, td.h, td.w, d.k, d.stride, d.pad_t, d.pad_l, gsk, s);
+          break;
+        }
         // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
         np = launch_gemm_dgrad(gview(ctx, E, op.out, input), W + op.w, dx, (int)ti.rows(), ti.c, to.c,
                                op.acc[0], s, E.gpart, gsk, E.bf16);
         break;
       case OP_DW:
+        if (i >= 2 && E.xdw[i - 2]) {  // BN0's backward sums only, y0 recomputed
+          np = launch_dw_bwd_x(xdw_args(ctx, E, i - 2, input), P.tensors[P.ops[i - 2].in[0]].c,
+                               gview(ctx, E, op.out, input), W + op.w, ti.n, ti.h, ti.w, to.h, to.w, op.k,
+                               op.stride, op.pad_t, op.pad_l, gsk, s);
+          break;
+        }
         np = launch_dw_bwd(gview(ctx, E, op.out, input), W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k,
                            op.stride, op.pad_t, op.pad_l, op.acc[0], s, gsk);
         break;
@@ -1479,6 +1607,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
           const BnFinSeg sg{E.spart + E.gstat_region[i] * E.sp_region, nullptr, E.gstat_P[i], (long)ti.rows(),
                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
           sync_finalize(ctx, E, &sg, 1, ti.c, true, s);
+        } else if (!frozen && E.gfused_bn[i] && skip_timing('b')) {
         } else if (!frozen && E.gfused_bn[i])
           launch_bn_bwd_finalize(E.spart + E.gstat_region[i] * E.sp_region, E.gstat_P[i], (long)ti.rows(),
                                  ti.c, E.slot_d[op.slot],
@@ -2365,6 +2494,10 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
                                   " elements)");
     if (which == 0 && op.t == OP_FUSE && E.fuse_folded[i])
       throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
+    for (size_t j = 0; j < E.prog.ops.size(); ++j)
+      if (E.xdw[j] && (E.prog.ops[j].out == t || (which == 1 && E.prog.ops[j + 1].out == op.out)))
+        throw std::invalid_argument("tap: this tensor is recomputed by the fused expand / depthwise kernels, "
+                                    "never stored (PHX_XDW=0 at victim creation keeps it)");
     const float* src = which == 0 ? E.tptr(t, nullptr) : E.gptr(op.out);
     if (!src) throw std::invalid_argument("tap: no gradient for this tensor");
     if (which == 0 && E.tbf(t)) launch_bf16_to_f32(src, out, (long)nfloats, (hipStream_t)stream);

@@ -405,6 +405,14 @@ void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, f
   else colred(StatsAcc<false>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
 }
 
+void launch_bn_stats_final(const double* part, int chunks, long M, int C, const float* ref, float* mean, float* rstd,
+                           const float* gamma, float* sc, float* mmean, float* mvar, float eps, double* side,
+                           hipStream_t s) {
+  StatsEpi e{ref, M, mean, rstd, gamma, sc, mmean, mvar, eps, 0, side};
+  hipLaunchKernelGGL((k_colred_final<StatsEpi>), dim3(cdiv(C, 16), 1), dim3(256), 0, s, e, part, chunks, C);
+  PHX_LAUNCH_CHECK();
+}
+
 // ---- BN statistics from producer partials (StatSink / GradSink) ---------------------------
 // One workgroup per channel: its P partials are contiguous (channel-major), each lane folds a
 // strided subset into fp64, the 256 lane pairs meet in an LDS tree and the epilogue finishes the
