@@ -112,6 +112,18 @@ struct Exec {
   size_t sp_region = 0, sc_region = 0;
   std::vector<int> stat_region;                // tensor id -> region of its producer's partials
   std::vector<int> gstat_region;               // BN op id -> region of its backward partials
+  // In-launch BN finalize (common.hpp FinDesc): fin_fwd / fin_bwd[i]: BN op i's batch statistics /
+  // backward sums are finalized by the last workgroup of their producer launch, no k_bn_finalize.
+  // Ticket r serves partial region r (a group's member r); descriptors [3 * op]: forward, forward
+  // with deferred moving statistics, backward — built for the weights buffer fin_w.
+  std::vector<char> fin_fwd, fin_bwd;
+  std::vector<int> fin_reg;
+  unsigned* fin_tick = nullptr;
+  FinDesc* fin_desc = nullptr;
+  const float* fin_w = nullptr;
+  const FinDesc* fin_of(int bn, bool bwd) const {
+    return fin_desc + 3 * (size_t)bn + (bwd ? 2 : defer_mov ? 1 : 0);
+  }
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -705,6 +717,63 @@ Exec& phx_ctx::exec_for(int B, int tag) {
       E.xdw_ref = E.alloc<float>(ref_need);
     }
   }
+  // in-launch BN finalize where the producer runs a folding kernel (gemm2 / gemm2r without split-K,
+  // depthwise, elementwise gradient sums) and the partials are few enough for one workgroup to fold
+  // (C * P <= PHX_FIN_MAX, default 8192; 0 = every BN finalizes in its own launch); a group's BNs all
+  // or none (one grouped finalize launch)
+  E.fin_fwd.assign(P.ops.size(), 0);
+  E.fin_bwd.assign(P.ops.size(), 0);
+  E.fin_reg.assign(P.ops.size(), 0);
+  if (bn_mode == PHX_BN_LOCAL) {
+    const long fin_max = [] {  // (read per executor)
+      const char* e = std::getenv("PHX_FIN_MAX");
+      return e ? atol(e) : 8192L;
+    }();
+    for (size_t i = 1; fin_max > 0 && i < P.ops.size(); ++i) {
+      const Op& bn = P.ops[i];
+      if (bn.t != OP_BN) continue;
+      const Op& pr = P.ops[i - 1];
+      const Tensor& tz = P.tensors[bn.in[0]];
+      const long C = tz.c;
+      if (E.grp_of[i] >= 0) {
+        const std::vector<int>& g = E.groups[E.grp_of[i]];
+        E.fin_reg[i] = (int)(std::find(g.begin(), g.end(), (int)i) - g.begin());
+      }
+      if (E.fused_bn[i] && pr.out == bn.in[0]) {
+        const Tensor& ti = P.tensors[pr.in[0]];
+        long np = -1;
+        if (pr.t == OP_PW && gemm_fold_ok((int)ti.rows(), tz.c, ti.c, bf16))
+          np = gemm_stat_partials((int)ti.rows(), tz.c, ti.c, bf16);
+        else if (pr.t == OP_DW && !(i >= 3 && E.xdw[i - 3]))
+          np = dw_stat_partials(ti.n, ti.h, ti.w, ti.c, tz.h, tz.w, pr.k, pr.stride, pr.pad_t, pr.pad_l);
+        if (np > 0 && C * np <= fin_max) E.fin_fwd[i] = 1;
+      }
+      if (E.gfused_bn[i] && i + 1 < P.ops.size()) {
+        const Op& L = P.ops[i + 1];
+        const Tensor& li = P.tensors[L.in[0]];
+        const Tensor& lo = P.tensors[L.out];
+        bool ok = L.t == OP_SE || L.t == OP_ADD || (L.t == OP_DW && !(i >= 1 && E.xdw[i - 1]));
+        if (L.t == OP_PW) ok = !E.xdw[i + 1] && gemm_fold_ok((int)li.rows(), li.c, lo.c, bf16);
+        if (ok && C * (long)E.gstat_P[i] <= fin_max) E.fin_bwd[i] = 1;
+      }
+    }
+    // a group's BNs: all or none
+    for (const std::vector<int>& g : E.groups) {
+      if (P.ops[g[0]].t != OP_BN) continue;
+      bool f = true, b = true;
+      for (int m : g) {
+        f = f && E.fin_fwd[m];
+        b = b && E.fin_bwd[m];
+      }
+      for (int m : g) {
+        E.fin_fwd[m] = f;
+        E.fin_bwd[m] = b;
+      }
+    }
+  }
+  E.fin_tick = E.alloc<unsigned>(kMaxSeg);
+  PHX_HIP(hipMemset(E.fin_tick, 0, kMaxSeg * sizeof(unsigned)));
+  E.fin_desc = E.alloc<FinDesc>(3 * P.ops.size());
   const size_t nreg = E.groups.empty() ? 1 : kMaxSeg;
   E.sp_region = sp_need;
   E.sc_region = sc_need;
@@ -1099,6 +1168,29 @@ void plan_groups(Exec& E, bool local_bn) {
   }
 }
 
+// the in-launch finalize descriptors of the executor's folded BNs (rebuilt when the weights buffer moves)
+void fin_prepare(phx_ctx* ctx, Exec& E) {
+  const float* W = ctx->w();
+  if (E.fin_w == W) return;
+  const Program& P = E.prog;
+  std::vector<FinDesc> h(3 * P.ops.size());
+  for (size_t i = 0; i < P.ops.size(); ++i) {
+    const Op& op = P.ops[i];
+    if (op.t != OP_BN || !(E.fin_fwd[i] || E.fin_bwd[i])) continue;
+    const long M = (long)P.tensors[op.in[0]].rows();
+    StatsEpi fe{nullptr, M, E.slot_a[op.slot], E.slot_b[op.slot], W + op.gamma, E.slot_c[op.slot],
+                const_cast<float*>(W) + op.mmean, const_cast<float*>(W) + op.mvar, kBnEps, 0, nullptr};
+    const BwdEpi2 be{M, E.slot_d[op.slot], E.slot_e[op.slot]};
+    unsigned* tk = E.fin_tick + E.fin_reg[i];
+    h[3 * i] = FinDesc{tk, fe, be};
+    h[3 * i + 2] = FinDesc{tk, fe, be};
+    fe.side = E.side + 2 * (size_t)E.side_off[op.slot];
+    h[3 * i + 1] = FinDesc{tk, fe, be};
+  }
+  PHX_HIP(hipMemcpy(E.fin_desc, h.data(), h.size() * sizeof(FinDesc), hipMemcpyHostToDevice));
+  E.fin_w = W;
+}
+
 // bn=sync: the BN sums of `segs` (fold -> the caller's all-reduce -> statistics from the global sums)
 // bn=sync: all-reduce the sums of `n` members already in E.sync_sums, then their statistics
 void sync_reduce_apply(phx_ctx* ctx, Exec& E, const BnFinSeg* segs, int n, int C, bool bwd, hipStream_t s) {
@@ -1124,7 +1216,9 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
   float* W = ctx->w();
   const bool sink_on = !frozen && g[0] + 1 < (int)P.ops.size() && E.fused_bn[g[0] + 1];
   auto sink_of = [&](int r) {
-    return sink_on ? StatSink{E.spart + (size_t)r * E.sp_region, E.scnt + (size_t)r * E.sc_region, to0.c, 0}
+    const int bn = g[r] + 1;
+    return sink_on ? StatSink{E.spart + (size_t)r * E.sp_region, E.scnt + (size_t)r * E.sc_region, to0.c, 0,
+                              E.fin_fwd[bn] ? E.fin_of(bn, false) : nullptr}
                    : StatSink{};
   };
   double fl = 0, by = 0;
@@ -1194,7 +1288,8 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            nullptr, nullptr, E.side_for(op.slot)};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, false, s);
-      else if (!skip_timing('f')) launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
+      else if (E.fin_fwd[g[0]]) {  // finalized by the producer group's launch
+      } else if (!skip_timing('f')) launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
       break;
     }
     default:
@@ -1215,7 +1310,8 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
     if (!gs_on) return GradSink{};
     const Op& bn = P.ops[g[r] - 1];
     return GradSink{E.spart + (size_t)r * E.sp_region, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input),
-                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
+                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0]),
+                    E.fin_bwd[g[r] - 1] ? E.fin_of(g[r] - 1, true) : nullptr};
   };
   double fl = 0, by = 0;
   for (int i : g) {
@@ -1283,7 +1379,8 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, true, s);
-      else if (!skip_timing('b')) launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
+      else if (E.fin_bwd[g[0]]) {  // finalized by the dgrad group's launch
+      } else if (!skip_timing('b')) launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
       break;
     }
     default:
@@ -1310,6 +1407,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
   const Program& P = E.prog;
   float* W = ctx->w();
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train || force_frozen;
+  fin_prepare(ctx, E);
   if (E.ndrop && train)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   if (E.ndrop && train) ck_note(E, "p" + std::to_string(pass) + " drop keep", E.drop_keep, (size_t)E.ndrop * E.B * 4, s);
@@ -1345,7 +1443,8 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     }
     // the BN right after this op takes its statistics from this launch (StatSink)
     const bool sink_on = !frozen && i + 1 < P.ops.size() && E.fused_bn[i + 1];
-    const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0} : StatSink{};
+    const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0, E.fin_fwd[i + 1] ? E.fin_of((int)i + 1, false) : nullptr}
+                                  : StatSink{};
     if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
     if (skip_kind(std::string("f:") + kind, op.name)) continue;
     Scope scope(ctx, kind, fl, by, s, (prof_detail() || debug_sync()) ? op_tag(P, op, false) : std::string());
@@ -1412,7 +1511,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
                             mean, rstd, W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, nullptr, nullptr,
                             E.side_for(op.slot)};
           sync_finalize(ctx, E, &sg, 1, ti.c, false, s);
-        } else if (E.fused_bn[i] && skip_timing('f')) {
+        } else if (E.fused_bn[i] && (E.fin_fwd[i] || skip_timing('f'))) {  // (finalized by the producer)
         } else if (E.fused_bn[i])
           launch_bn_finalize(E.spart + E.stat_region[op.in[0]] * E.sp_region,
                              E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]],
@@ -1491,6 +1590,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
   float* W = ctx->w();
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN;
   const int na = ctx->mc.num_anchors();
+  fin_prepare(ctx, E);
   // 1. sparse class-head gradient into the inputs of the class-predict pointwise convs
   int K = 0;
   long wpred = -1;
@@ -1555,7 +1655,8 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     if (i > 0 && E.gfused_bn[i - 1]) {
       const Op& bn = P.ops[i - 1];
       gsk = GradSink{E.spart, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input), E.slot_a[bn.slot],
-                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
+                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0]),
+                     E.fin_bwd[i - 1] ? E.fin_of(i - 1, true) : nullptr};
       gsk_in = op.in[0] == bn.out ? 0 : 1;
     }
     if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
@@ -1607,7 +1708,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
           const BnFinSeg sg{E.spart + E.gstat_region[i] * E.sp_region, nullptr, E.gstat_P[i], (long)ti.rows(),
                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
           sync_finalize(ctx, E, &sg, 1, ti.c, true, s);
-        } else if (!frozen && E.gfused_bn[i] && skip_timing('b')) {
+        } else if (!frozen && E.gfused_bn[i] && (E.fin_bwd[i] || skip_timing('b'))) {  // (finalized by the dgrad)
         } else if (!frozen && E.gfused_bn[i])
           launch_bn_bwd_finalize(E.spart + E.gstat_region[i] * E.sp_region, E.gstat_P[i], (long)ti.rows(),
                                  ti.c, E.slot_d[op.slot],

@@ -573,8 +573,12 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
         }
       }
       if constexpr (STATS)
-        if (blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[blockIdx.x] = ntot;
+        if (blockIdx.y == 0 && wn == 0 && lane == 0) sink_cnt(a.sink, blockIdx.x, ntot);
     }
+    // in-launch finalize (FinDesc): this workgroup stored partial row blockIdx.x of its columns
+    const unsigned ent = (unsigned)max(0, min(BN, a.N - n0));
+    if constexpr (STATS) sink_finish(a.sink, ent, sm);
+    else gsink_finish(a.gsk, ent, sm);
   }
 }
 
@@ -878,7 +882,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2r(Gemm2Group<NS> grp) {
             const int col = ncol0 + j * 32 + r32;
             if (h == 0 && col < a.N) sink_put(a.sink, prow, col, nw, mean, q);
           }
-          if (nt == nt0 && blockIdx.y == 0 && wn == 0 && lane == 0) a.sink.cnt[prow] = nw;
+          if (nt == nt0 && blockIdx.y == 0 && wn == 0 && lane == 0) sink_cnt(a.sink, prow, nw);
         }
         if constexpr (SK == 2) {
   #pragma unroll
@@ -928,6 +932,14 @@ __global__ __launch_bounds__(256, 2) void k_gemm2r(Gemm2Group<NS> grp) {
   };
   while (step()) {
   }
+  if constexpr (SK != 0) {
+    // in-launch finalize (FinDesc): WM partial rows per M tile of this workgroup, its N-tile run's columns
+    const int nmt = (a.mtiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const unsigned ent = (unsigned)(nmt * WM * (min(a.N, nte * BN) - nt0 * BN));
+    __syncthreads();  // (the last step's LDS reads are done before the scratch is reused)
+    if constexpr (SK == 1) sink_finish(a.sink, ent, g2r_sm);
+    else gsink_finish(a.gsk, ent, g2r_sm);
+  }
 }
 
 // st: activation storage variant (ST of k_gemm2).  A bf16 context stores bf16 activations, so its
@@ -966,8 +978,12 @@ constexpr bool g2r_cfg() {
 
 template <auto KFN>
 static void g2r_attr() {
-  static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(KFN),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  static const bool ok = [] {
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KFN)) != hipSuccess) return false;
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(KFN), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)(160 * 1024 - fa.sharedSizeBytes)) == hipSuccess;
+  }();
   if (!ok) throw std::runtime_error("gemm2r: cannot raise the dynamic LDS limit");
 }
 

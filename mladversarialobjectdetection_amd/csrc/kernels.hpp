@@ -92,6 +92,8 @@ int launch_gemm_gather(const float* x, int B, int H, int W, int C, int Ho, int W
 int launch_gemm_dgrad(GradX A, const float* Bt, float* C, int M, int N, int K, bool acc,
                       hipStream_t s, float* partial, GradSink gs = GradSink{}, bool bf16 = false);
 int gemm_dgrad_gsink_partials(int M, int N, int K, bool bf16 = false);
+// the launch of this shape runs a kernel with the in-launch BN finalize (k_gemm2 / k_gemm2r, no split-K)
+bool gemm_fold_ok(int M, int N, int K, bool bf16);
 // Grouped GEMM: members share Bt [N][K] (weights shared across pyramid levels) and differ in A,
 // C, M and sinks.  mode as gemm2 (0 raw, 1 BN view, 3 gradient view).  No split-K: see
 // gemm_group_ok.  Returns the most partial rows any member's sinks get; P_out[i] = member i's

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
       float tn = 0.f, tm = 0.f, t2 = 0.f;
       for (int k = 0; k < G; ++k) chan_merge(tn, tm, t2, gn[k], gm[k][t], g2[k][t]);
       sink_put(sink, blockIdx.x, t, tn, tm, t2);
-      if (t == 0) sink.cnt[blockIdx.x] = tn;
+      if (t == 0) sink_cnt(sink, blockIdx.x, tn);
     }
   }
 }
@@ -360,6 +360,7 @@ void launch_stem_bwd_gx(GradX g, const float* w, const int16_t* owner, float* dx
 int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                     int Co, int pt, int pl, hipStream_t s, StatSink sink, bool ybf) {
   if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
+  if (sink.fd) throw std::logic_error("stem: no in-launch finalize");
   stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, sink, ybf, s);
   PHX_LAUNCH_CHECK();
   return cdiv((long)B * Ho * Wo, 256);
@@ -493,7 +494,7 @@ __device__ __forceinline__ void gemm_stats(const floatx4 (&acc)[2][NT], const fl
       float tn = 0.f;
 #pragma unroll
       for (int w = 0; w < WM; ++w) tn += wcnt[w];
-      sink.cnt[blockIdx.x] = tn;
+      sink_cnt(sink, blockIdx.x, tn);
     }
   }
 }
@@ -768,7 +769,7 @@ __global__ __launch_bounds__(256) void k_gemm_splitk_reduce_stats(const float* _
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) sink_put(sink, blockIdx.x, c4 * 4 + j, tn[j], tm[j], t2[j]);
-    if (c4 == 0) sink.cnt[blockIdx.x] = tn[0];
+    if (c4 == 0) sink_cnt(sink, blockIdx.x, tn[0]);
   }
 }
 
@@ -916,6 +917,7 @@ int gemm_stat_partials(int M, int N, int K, bool bf16) {
 // statistics of the result come out of the same pass.  Returns the StatSink partial rows.
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
                        bool acc, StatSink sink, hipStream_t s, bool cbf) {
+  if (sink.fd) throw std::logic_error("gemm: no in-launch finalize after a split-K reduce");
   if (sink.part) {
     const int rb = splitk_stats_rb(M, N);
     sink.P = cdiv(M, rb);
@@ -943,6 +945,7 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s, float* partial,
               StatSink sink, GradSink gsk) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
+  if (sink.fd || gsk.fd) throw std::logic_error("gemm: the in-launch finalize runs in the gemm2 kernels only");
   GemmPlan p = plan_gemm(M, N, K);
   float* part = p.splits > 1 ? partial : nullptr;
   if (p.splits > 1 && !partial) throw std::runtime_error("gemm: split-K needs a partial buffer");
@@ -1022,6 +1025,10 @@ int launch_gemm_gather(const float* x, int B, int H, int W, int C, int Ho, int W
                        (uint32_t)pt << 21 | (uint32_t)pl << 23 | (uint32_t)mode << 25;
   return gemm2_run(4, InX{x, nullptr, nullptr, nullptr, 0}, GradX{}, Bt, bias, out, B * Ho * Wo, N, K, false,
                    nullptr, (int)geo, st, partial, StatSink{}, gemm2_target_wgs(), GradSink{}, false);
+}
+
+bool gemm_fold_ok(int M, int N, int K, bool bf16) {
+  return gemm_impl_for(N, bf16) == 2 && plan_gemm2(M, N, K, gemm2_target_wgs(), bf16).splits == 1;
 }
 
 // GradSink partial rows a dgrad GEMM of this shape writes (0: the sums cannot be fused: split-K)

@@ -333,7 +333,7 @@ __device__ __forceinline__ void dw_stats(const float4 (&acc)[RPT], unsigned vmas
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) sink_put(sink, p, c + j, tn[j], tm[j], t2[j]);
-    if (threadIdx.x == 0) sink.cnt[p] = tn[0];
+    if (threadIdx.x == 0) sink_cnt(sink, p, tn[0]);
   }
 }
 
@@ -403,7 +403,10 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
     if constexpr (BF && STATS)
       acc[r] = make_float4(round_bf16(acc[r].x), round_bf16(acc[r].y), round_bf16(acc[r].z), round_bf16(acc[r].w));
   }
-  if constexpr (STATS) dw_stats<RPT>(acc, vmask, g.lcg, c, (long)b * g.ntiles + tl, sink);
+  if constexpr (STATS) {
+    dw_stats<RPT>(acc, vmask, g.lcg, c, (long)b * g.ntiles + tl, sink);
+    sink_finish(sink, 4u << g.lcg, tile);
+  }
 }
 
 // ---- data gradient: dx[iy][ix] = sum over (i,j) with (iy+pt-i) and (ix+pl-j) divisible by S of
@@ -542,7 +545,10 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
     *o = a;
     if constexpr (GS) gs_acc4(gsk, kk, a, yv[r], s1, s2);
   }
-  if constexpr (GS) dw_gsums(s1, s2, g.lcg, c, (long)b * g.ntiles + tl, gsk);
+  if constexpr (GS) {
+    dw_gsums(s1, s2, g.lcg, c, (long)b * g.ntiles + tl, gsk);
+    gsink_finish(gsk, 4u << g.lcg, tile);
+  }
 }
 
 // ---- expand -> BN -> activation -> depthwise, fused ------------------------------------------
@@ -1372,7 +1378,7 @@ static void xdw_fwd_cin(int cin, const XdwArgs& a, const float* w, float* y, con
 
 int launch_dw_fwd_x(const XdwArgs& a, int cin, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                     int k, int stride, int pt, int pl, StatSink sink, hipStream_t s) {
-  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || !sink.part)
+  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || !sink.part || sink.fd)
     throw std::invalid_argument("xdw fwd: unsupported shape");
   const int rpt = dw_rpt_fwd(stride);
   if (rpt != 2 && stride == 2) throw std::invalid_argument("xdw fwd: stride 2 runs 2 rows per lane");
@@ -1404,7 +1410,7 @@ static void xdw_bwd_cin(int cin, const XdwArgs& a, GradX gv, const float* w, con
 
 int launch_dw_bwd_x(const XdwArgs& a, int cin, GradX gv, const float* w, int B, int H, int W, int Ho, int Wo,
                     int k, int stride, int pt, int pl, GradSink gs0, hipStream_t s) {
-  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || !gs0.part || (gv.y && gv.ybf))
+  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || !gs0.part || gs0.fd || (gv.y && gv.ybf))
     throw std::invalid_argument("xdw bwd: unsupported shape");
   const DwGeom g = dw_plan(H, W, a.ce, Ho, Wo, pt, pl, k, stride, 4, true);
   gs0.P = B * g.ntiles;
@@ -1447,7 +1453,7 @@ static void xdw_dx_cin(int cin, const XdwArgs& a, GradX gv, const float* w, floa
 
 int launch_xdw_dx(const XdwArgs& a, int cin, GradX gv, const float* w, float* dx, bool acc, int B, int H, int W,
                   int Ho, int Wo, int k, int stride, int pt, int pl, GradSink gsx, hipStream_t s) {
-  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || (gv.y && gv.ybf) || (gsx.part && gsx.ybf))
+  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || (gv.y && gv.ybf) || (gsx.part && gsx.ybf) || gsx.fd)
     throw std::invalid_argument("xdw dx: unsupported shape");
   XdwDxGeom g{H, W, Ho, Wo, pt, pl, cdiv(W, 8), 0, 0};
   g.wr = stride == 1 ? 8 + k - 1 : (8 - 1 + k - 1) / 2 + 2;

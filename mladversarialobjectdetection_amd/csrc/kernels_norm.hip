@@ -279,6 +279,7 @@ __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, lo
     gsink_put(g, p, c4 * 4 + 2, s1.z, s2.z);
     gsink_put(g, p, c4 * 4 + 3, s1.w, s2.w);
   }
+  gsink_finish(g, 4u * (unsigned)tpr, sh1);
 }
 
 // rows per lane whose loads are in flight together (fp32 / bf16 BN input of the GradSink)
@@ -323,58 +324,6 @@ struct StatsAcc {
     for (int j = 0; j < 4; ++j) {
       a0[j] += d[j];
       a1[j] += d[j] * d[j];
-    }
-  }
-};
-
-// one moving-average step, m - (m - batch) * (1 - momentum) in fp64 rounded to float
-__device__ __forceinline__ float moving_update(float m, double batch) { return (float)(m - (m - batch) * 0.01); }
-
-struct StatsEpi {
-  const float* y;  // for the shift (row 0)
-  long M;
-  float* mean;
-  float* rstd;
-  const float* gamma;
-  float* sc;
-  float* mmean;
-  float* mvar;
-  float eps;
-  int ybf = 0;  // y in bf16 storage
-  double* side = nullptr;  // deferred moving statistics: (mean, uvar) pairs, moving stats untouched
-  // the per-channel inputs of the epilogue, loaded before the fold (k_bn_finalize issues them with
-  // the partials, so the epilogue costs no second memory round trip)
-  struct Pre {
-    float ref, g, mm, mv;
-  };
-  __device__ Pre pre(int c) const {
-    Pre r;
-    r.ref = !y ? 0.f : ybf ? ald1<true>(y, c) : y[c];
-    r.g = gamma[c];
-    r.mm = (!side && mmean) ? mmean[c] : 0.f;
-    r.mv = (!side && mmean) ? mvar[c] : 0.f;
-    return r;
-  }
-  __device__ void operator()(int, int c, double s0, double s1) const { fin(pre(c), c, s0, s1); }
-  __device__ void fin(const Pre& pr, int c, double s0, double s1) const {
-    const double ref = (double)pr.ref;
-    const double dm = s0 / (double)M;            // mean - ref
-    double var = s1 / (double)M - dm * dm;
-    if (var < 0.0) var = 0.0;
-    const double mu = ref + dm;
-    mean[c] = (float)mu;
-    const double rs = 1.0 / sqrt(var + (double)eps);
-    rstd[c] = (float)rs;
-    sc[c] = (float)(rs * (double)pr.g);
-    // Keras: moving -= (moving - batch) * (1 - momentum); the fused op reports the
-    // Bessel-corrected variance for the moving average [TF-recall].
-    const double uvar = M > 1 ? var * (double)M / (double)(M - 1) : var;
-    if (side) {
-      side[2 * c] = mu;
-      side[2 * c + 1] = uvar;
-    } else if (mmean) {
-      mmean[c] = moving_update(pr.mm, mu);
-      mvar[c] = moving_update(pr.mv, uvar);
     }
   }
 };
@@ -493,26 +442,33 @@ __global__ __launch_bounds__(256) void k_bn_finalize(FinGroup<E, NS> grp) {
   if (t == 0) e.fin(pr, c, r1[0], r2[0]);
 }
 
+// (a one-wave-per-channel form for P <= 64 — lanes strided over the partials, an xor-shuffle tree
+// instead of the LDS tree — measured 0.04 ms/step slower on C2: the launch is latency-bound)
+template <bool BWD, class E, int NS>
+static void fin_launch(const FinGroup<E, NS>& g, int n, int C, int, hipStream_t s) {
+  hipLaunchKernelGGL((k_bn_finalize<BWD, E, NS>), dim3(C, n), dim3(256), 0, s, g);
+  PHX_LAUNCH_CHECK();
+}
 void launch_bn_finalize(const float2* part, const float* cnt, int P, long M, int C, float* mean,
                         float* rstd, const float* gamma, float* sc, float* mmean, float* mvar,
                         float eps, hipStream_t s, double* side) {
   // StatsEpi's shift is 0 here: S1, S2 are plain sums of x and x^2 in fp64
   FinGroup<StatsEpi, 1> g{};
-  g.s[0] = FinSeg<StatsEpi>{part, cnt, P, StatsEpi{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps, 0, side}};
-  hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi, 1>), dim3(C), dim3(256), 0, s, g);
-  PHX_LAUNCH_CHECK();
+  g.s[0] = FinSeg<StatsEpi>{part, cnt, P, StatsEpi{nullptr, M, mean, rstd, gamma, sc, mmean, mvar, eps, 0, side, C}};
+  fin_launch<false>(g, 1, C, P, s);
 }
 
 void launch_bn_finalize_group(const BnFinSeg* segs, int n, int C, float eps, hipStream_t s) {
   if (n < 1 || n > kMaxSeg) throw std::runtime_error("bn finalize group: bad member count");
   FinGroup<StatsEpi, kMaxSeg> g{};
+  int Pmax = 0;
   for (int i = 0; i < n; ++i) {
     const BnFinSeg& d = segs[i];
     g.s[i] = FinSeg<StatsEpi>{d.part, d.cnt, d.P,
-                              StatsEpi{nullptr, d.M, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps, 0, d.side}};
+                              StatsEpi{nullptr, d.M, d.mean, d.rstd, d.gamma, d.sc, d.mmean, d.mvar, eps, 0, d.side, C}};
+    Pmax = std::max(Pmax, d.P);
   }
-  hipLaunchKernelGGL((k_bn_finalize<false, StatsEpi, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
-  PHX_LAUNCH_CHECK();
+  fin_launch<false>(g, n, C, Pmax, s);
 }
 
 __global__ void k_bn_frozen_stats(const float* __restrict__ mm, const float* __restrict__ mv,
@@ -651,34 +607,22 @@ __global__ __launch_bounds__(256) void k_bn_bwd_apply(const float* __restrict__ 
   *op = make_float4(o[0], o[1], o[2], o[3]);
 }
 
-struct BwdEpi2 {
-  long M;
-  float* mdz;
-  float* mdzx;
-  struct Pre {};
-  __device__ Pre pre(int) const { return Pre{}; }
-  __device__ void fin(const Pre&, int c, double s0, double s1) const { (*this)(0, c, s0, s1); }
-  __device__ void operator()(int, int c, double s0, double s1) const {
-    mdz[c] = (float)(s0 / (double)M);
-    mdzx[c] = (float)(s1 / (double)M);
-  }
-};
-
 void launch_bn_bwd_finalize(const float2* part, int P, long M, int C, float* mdz, float* mdzx,
                             hipStream_t s) {
   FinGroup<BwdEpi2, 1> g{};
-  g.s[0] = FinSeg<BwdEpi2>{part, nullptr, P, BwdEpi2{M, mdz, mdzx}};
-  hipLaunchKernelGGL((k_bn_finalize<true, BwdEpi2, 1>), dim3(C), dim3(256), 0, s, g);
-  PHX_LAUNCH_CHECK();
+  g.s[0] = FinSeg<BwdEpi2>{part, nullptr, P, BwdEpi2{M, mdz, mdzx, C}};
+  fin_launch<true>(g, 1, C, P, s);
 }
 
 void launch_bn_bwd_finalize_group(const BnFinSeg* segs, int n, int C, hipStream_t s) {
   if (n < 1 || n > kMaxSeg) throw std::runtime_error("bn finalize group: bad member count");
   FinGroup<BwdEpi2, kMaxSeg> g{};
-  for (int i = 0; i < n; ++i)
-    g.s[i] = FinSeg<BwdEpi2>{segs[i].part, nullptr, segs[i].P, BwdEpi2{segs[i].M, segs[i].mdz, segs[i].mdzx}};
-  hipLaunchKernelGGL((k_bn_finalize<true, BwdEpi2, kMaxSeg>), dim3(C, n), dim3(256), 0, s, g);
-  PHX_LAUNCH_CHECK();
+  int Pmax = 0;
+  for (int i = 0; i < n; ++i) {
+    g.s[i] = FinSeg<BwdEpi2>{segs[i].part, nullptr, segs[i].P, BwdEpi2{segs[i].M, segs[i].mdz, segs[i].mdzx, C}};
+    Pmax = std::max(Pmax, segs[i].P);
+  }
+  fin_launch<true>(g, n, C, Pmax, s);
 }
 
 // bn=sync: the finalize's fold with an epilogue that keeps the fp64 sums (and the rows they cover)
