@@ -727,7 +727,7 @@ Exec& phx_ctx::exec_for(int B, int tag) {
   if (bn_mode == PHX_BN_LOCAL) {
     const long fin_max = [] {  // (read per executor)
       const char* e = std::getenv("PHX_FIN_MAX");
-      return e ? atol(e) : 8192L;
+      return e ? atol(e) : 0L;
     }();
     for (size_t i = 1; fin_max > 0 && i < P.ops.size(); ++i) {
       const Op& bn = P.ops[i];

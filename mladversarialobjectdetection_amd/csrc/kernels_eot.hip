@@ -53,6 +53,13 @@ struct EotLists {
 // output rows per separable-resize work item (k_eot_resize, k_eot_resize_bwd_rows)
 constexpr int kResizeRT = 4;
 
+// PHX_EOT_V1=1: the round-4 composite and resize-adjoint kernels (A/B and the bit-identity test;
+// read per call)
+static bool eot_v1() {
+  const char* e = std::getenv("PHX_EOT_V1");
+  return e && e[0] == '1';
+}
+
 __global__ __launch_bounds__(256) void k_eot_place(EotDims d, const float* __restrict__ boxes,
                                                    const int* __restrict__ count,
                                                    const float* __restrict__ params,
@@ -518,6 +525,9 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
   }
 }
 
+// (A v2 that walked the union of a tile's row spans once per column — one load of each source row
+// for all kResizeRT output rows, weights tabulated in LDS — measured 2.42 ms against v1's 1.73 ms on
+// the first-pass flow, and was dropped.)
 void launch_eot_resize(const EotDims& d, const float* matched, const BoxPlace* place,
                        const SpanEntry* spans, uint64_t seed, int64_t step, int gimg0,
                        float* rstore, hipStream_t s, float noise_amp) {
@@ -626,13 +636,118 @@ __global__ __launch_bounds__(256) void k_eot_composite(EotDims d, const float* _
   }
 }
 
+// v2: the workgroup first keeps only its image's boxes whose square meets the workgroup's pixel
+// rectangle (wave 0, ballot compaction: the boxes stay in paste order), so a pixel walks the few
+// boxes that can cover it instead of all of them (the first-pass flow pastes ~90 per image);
+// a box that covers none of the workgroup's pixels changes none of them: bit-identical to v1
+__global__ __launch_bounds__(256) void k_eot_composite2(EotDims d, const float* __restrict__ img_in,
+                                                        const BoxPlace* __restrict__ place,
+                                                        const float* __restrict__ rstore,
+                                                        float* __restrict__ img_out,
+                                                        int16_t* __restrict__ owner,
+                                                        float* __restrict__ mask) {
+  const long npx = (long)d.H * d.W;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const ListView L = lists_of(d, place);
+  const long first = (long)blockIdx.x * blockDim.x;
+  const long last = min(first + (long)blockDim.x, (long)d.B * npx) - 1;
+  const bool staged = first / npx == last / npx;
+  __shared__ int s_sl[PHX_MAX_OUT], s_y0[PHX_MAX_OUT], s_x0[PHX_MAX_OUT], s_dg[PHX_MAX_OUT];
+  __shared__ int s_n;
+  if (staged && threadIdx.x < 64) {
+    const int b0 = (int)(first / npx);
+    const int n0 = L.img_n[b0], f0 = L.img_first[b0];  // <= d.maxb <= PHX_MAX_OUT (launcher)
+    const int p0 = (int)(first % npx), p1 = (int)(last % npx);
+    const int ry0 = p0 / d.W, ry1 = p1 / d.W;
+    const int cx0 = ry0 == ry1 ? p0 % d.W : 0, cx1 = ry0 == ry1 ? p1 % d.W : d.W - 1;
+    const int lane = threadIdx.x;
+    int cnt = 0;
+    for (int q0 = 0; q0 < n0; q0 += 64) {
+      const int q = q0 + lane;
+      int sl = 0, y0 = 0, x0 = 0, dg = 0;
+      bool hit = false;
+      if (q < n0) {
+        sl = L.vlist[f0 + q];
+        y0 = place[sl].ymin;
+        x0 = place[sl].xmin;
+        dg = place[sl].diag;
+        hit = y0 <= ry1 && y0 + dg > ry0 && x0 <= cx1 && x0 + dg > cx0;
+      }
+      const unsigned long long bal = __ballot(hit);
+      const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+      if (hit) {
+        s_sl[pos] = sl;
+        s_y0[pos] = y0;
+        s_x0[pos] = x0;
+        s_dg[pos] = dg;
+      }
+      cnt += __popcll(bal);
+    }
+    if (lane == 0) s_n = cnt;
+  }
+  __syncthreads();
+  if (idx >= (long)d.B * npx) return;
+  const int b = (int)(idx / npx);
+  const int n = staged ? s_n : L.img_n[b], f = L.img_first[b];
+  const int p = (int)(idx % npx);
+  const int y = p / d.W, x = p % d.W;
+  const float* ip = img_in + idx * 3;
+  float v[3] = {ip[0], ip[1], ip[2]};
+  int16_t own[3] = {-1, -1, -1};
+  bool covered = false;
+  for (int q = 0; q < n; ++q) {
+    int sl, y0, x0, dg;
+    if (staged) {
+      sl = s_sl[q]; y0 = s_y0[q]; x0 = s_x0[q]; dg = s_dg[q];
+    } else {
+      sl = L.vlist[f + q]; y0 = place[sl].ymin; x0 = place[sl].xmin; dg = place[sl].diag;
+    }
+    const int qy = y - y0, qx = x - x0;
+    if (qy < 0 || qy >= dg || qx < 0 || qx >= dg) continue;
+    const BoxPlace& P = place[sl];
+    covered = true;
+    const float ox = (float)qx, oy = (float)qy;
+    const float proj = 0.0f * ox + 0.0f * oy + 1.0f;
+    const float inx = (P.fwd[0] * ox + P.fwd[1] * oy + P.fwd[2]) / proj;
+    const float iny = (P.fwd[3] * ox + P.fwd[4] * oy + P.fwd[5]) / proj;
+    const float* R = rstore + P.roff;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float r = tf_bilinear(inx, iny, [&](int yy, int xx) { return rread(R, P, yy, xx, c); });
+      if (r < -1.0f) {
+        v[c] = fminf(fmaxf(v[c], -1.0f), 1.0f);
+      } else {
+        v[c] = fminf(fmaxf(r, -1.0f), 1.0f);
+        own[c] = (int16_t)(sl % d.maxb);
+      }
+    }
+  }
+  float* op = img_out + idx * 3;
+  if (mask) {
+    float* mp = mask + idx * 3;
+    mp[0] = covered ? ip[0] - v[0] : 0.f;
+    mp[1] = covered ? ip[1] - v[1] : 0.f;
+    mp[2] = covered ? ip[2] - v[2] : 0.f;
+  }
+  op[0] = v[0]; op[1] = v[1]; op[2] = v[2];
+  if (owner) {
+    owner[idx * 3 + 0] = own[0];
+    owner[idx * 3 + 1] = own[1];
+    owner[idx * 3 + 2] = own[2];
+  }
+}
+
 void launch_eot_composite(const EotDims& d, const float* img_in, const BoxPlace* place,
                           const float* rstore, float* img_out, int16_t* owner, hipStream_t s,
                           float* mask) {
   long n = (long)d.B * d.H * d.W;
   if (d.maxb > PHX_MAX_OUT) throw std::runtime_error("eot composite: more box slots than PHX_MAX_OUT");
-  hipLaunchKernelGGL(k_eot_composite, dim3(cdiv(n, 256)), dim3(256), 0, s, d, img_in, place, rstore,
-                     img_out, owner, mask);
+  if (eot_v1())
+    hipLaunchKernelGGL(k_eot_composite, dim3(cdiv(n, 256)), dim3(256), 0, s, d, img_in, place, rstore,
+                       img_out, owner, mask);
+  else
+    hipLaunchKernelGGL(k_eot_composite2, dim3(cdiv(n, 256)), dim3(256), 0, s, d, img_in, place, rstore,
+                       img_out, owner, mask);
   PHX_LAUNCH_CHECK();
 }
 
@@ -804,9 +919,158 @@ __global__ __launch_bounds__(256) void k_eot_resize_bwd_cols(EotDims d, const Bo
   }
 }
 
+// v2 rows: the work item's kResizeRT rows of dR and the box's spans staged in LDS first (v1 read
+// every dR value from memory once per output column whose span holds it); same sums, same order
+__global__ __launch_bounds__(256) void k_eot_resize_bwd_rows2(EotDims d, const BoxPlace* __restrict__ place,
+                                                              const SpanEntry* __restrict__ spans,
+                                                              const float* __restrict__ dstore,
+                                                              float* __restrict__ tstore) {
+  extern __shared__ float sh_rows[];  // [kResizeRT][ps][3] dR rows, then [ps] spans
+  const ListView L = lists_of(d, place);
+  const int nv = *L.nvalid, total = L.tprefix[nv];
+  for (int item = blockIdx.x; item < total; item += gridDim.x) {
+    const int v = find_box(L.tprefix, nv, item);
+    const int sl = L.vlist[v];
+    const BoxPlace P = place[sl];
+    const int i0 = (item - L.tprefix[v]) * kResizeRT;
+    const int ni = min(kResizeRT, P.ps - i0);
+    const SpanEntry* sp = spans + (long)sl * d.span_stride;
+    const float scale = (float)P.ps / (float)d.P;
+    const float inv_scale = (float)(1.0 / (double)scale);
+    const float ks = fmaxf(inv_scale, 1.0f);
+    const float one_over_k = 1.0f / ks;
+    const float* D = dstore + P.roff + (long)i0 * P.ps * 3;
+    float* Dl = sh_rows;
+    SpanEntry* Sl = reinterpret_cast<SpanEntry*>(sh_rows + (long)kResizeRT * d.span_stride * 3);
+    for (int e = threadIdx.x; e < ni * P.ps * 3; e += blockDim.x) Dl[e] = D[e];
+    for (int j = threadIdx.x; j < P.ps; j += blockDim.x) Sl[j] = sp[j];
+    __syncthreads();
+    float* U = tstore + (long)L.tprefix[v] * kResizeRT * d.P * 3;
+    for (int e = threadIdx.x; e < ni * d.P; e += blockDim.x) {
+      const int ii = e / d.P, x = e - ii * d.P;
+      const int i = i0 + ii;
+      int jlo, jhi;
+      adj_range(x, inv_scale, ks, P.ps, &jlo, &jhi);
+      float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+      for (int j = jlo; j <= jhi; ++j) {
+        const SpanEntry sj = Sl[j];
+        if (x < sj.start || x >= sj.end) continue;
+        const float w = span_weight(sj, x, one_over_k);
+        const float* g = Dl + ((long)ii * P.ps + j) * 3;
+        a0 += w * g[0];
+        a1 += w * g[1];
+        a2 += w * g[2];
+      }
+      float* o = U + ((long)i * d.P + x) * 3;
+      o[0] = a0; o[1] = a1; o[2] = a2;
+    }
+    __syncthreads();
+  }
+}
+
+// v2 cols: a lane owns one source column and RB consecutive source rows; per box it walks the
+// output rows whose spans meet its rows once, loading U[i][x] once and adding it to every row of
+// the block inside span(i) — each dmatched value gets the same terms in the same order (boxes
+// ascending, then i ascending) as v1 with about 2 * scale / (RB / scale + 2) times fewer U loads
+template <int RB>
+__global__ __launch_bounds__(256) void k_eot_resize_bwd_cols2(EotDims d, const BoxPlace* __restrict__ place,
+                                                              const SpanEntry* __restrict__ spans,
+                                                              const float* __restrict__ tstore,
+                                                              float* __restrict__ dmatched) {
+  const int b = blockIdx.z;
+  const long npx = (long)d.P * d.P;
+  const ListView L = lists_of(d, place);
+  const int n = L.img_n[b], f = L.img_first[b];  // <= d.maxb <= PHX_MAX_OUT (launcher)
+  __shared__ int s_ps[PHX_MAX_OUT];
+  __shared__ long s_span[PHX_MAX_OUT], s_u[PHX_MAX_OUT];
+  __shared__ float s_inv[PHX_MAX_OUT], s_ks[PHX_MAX_OUT], s_ok[PHX_MAX_OUT];
+  for (int q = threadIdx.x; q < n; q += blockDim.x) {
+    const int v = f + q;
+    const int sl = L.vlist[v];
+    const int ps = place[sl].ps;
+    const float scale = (float)ps / (float)d.P;
+    const float inv_scale = (float)(1.0 / (double)scale);
+    const float ks = fmaxf(inv_scale, 1.0f);
+    s_ps[q] = ps;
+    s_span[q] = (long)sl * d.span_stride;
+    s_u[q] = (long)L.tprefix[v] * kResizeRT * d.P * 3;
+    s_inv[q] = inv_scale;
+    s_ks[q] = ks;
+    s_ok[q] = 1.0f / ks;
+  }
+  __syncthreads();
+  const int x = (int)blockIdx.x * 64 + (int)(threadIdx.x & 63);
+  const int y0 = ((int)blockIdx.y * 4 + (int)(threadIdx.x >> 6)) * RB;
+  if (x >= d.P || y0 >= d.P) return;
+  const int nr = min(RB, d.P - y0);
+  float a[RB][3];
+#pragma unroll
+  for (int r = 0; r < RB; ++r) a[r][0] = a[r][1] = a[r][2] = 0.f;
+  for (int q = 0; q < n; ++q) {
+    const SpanEntry* sp = spans + s_span[q];
+    const float one_over_k = s_ok[q];
+    int ilo, ihi, t0, t1;
+    adj_range(y0, s_inv[q], s_ks[q], s_ps[q], &ilo, &t0);
+    adj_range(y0 + nr - 1, s_inv[q], s_ks[q], s_ps[q], &t1, &ihi);
+    const float* U = tstore + s_u[q] + (long)x * 3;
+    for (int i = ilo; i <= ihi; i += 4) {
+      // four output rows' loads in flight (clamped to ihi: valid rows of the box), added in order
+      SpanEntry si[4];
+      float g[4][3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int iu = min(i + u, ihi);
+        si[u] = sp[iu];
+        const float* gp = U + (long)iu * d.P * 3;
+        g[u][0] = gp[0];
+        g[u][1] = gp[1];
+        g[u][2] = gp[2];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (i + u > ihi) break;
+        if (si[u].end <= y0 || si[u].start >= y0 + nr) continue;
+#pragma unroll
+        for (int r = 0; r < RB; ++r) {
+          const int y = y0 + r;
+          if (y < si[u].start || y >= si[u].end) continue;
+          const float wy = span_weight(si[u], y, one_over_k);
+          a[r][0] += wy * g[u][0];
+          a[r][1] += wy * g[u][1];
+          a[r][2] += wy * g[u][2];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RB; ++r) {
+    if (r >= nr) continue;
+    float* o = dmatched + ((long)b * npx + (long)(y0 + r) * d.P + x) * 3;
+    o[0] = a[r][0]; o[1] = a[r][1]; o[2] = a[r][2];
+  }
+}
+
 void launch_eot_resize_bwd(const EotDims& d, const BoxPlace* place, const SpanEntry* spans,
                            const float* dstore, float* tstore, float* dmatched, hipStream_t s) {
   if (d.maxb > PHX_MAX_OUT) throw std::runtime_error("eot resize backward: more box slots than PHX_MAX_OUT");
+  if (!eot_v1()) {
+    const size_t shm = (size_t)kResizeRT * d.span_stride * 3 * sizeof(float) + (size_t)d.span_stride * sizeof(SpanEntry);
+    static const size_t cap = [] {  // the dynamic LDS limit raised to what 160 KB leaves (once)
+      hipFuncAttributes fa{};
+      if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&k_eot_resize_bwd_rows2)) != hipSuccess) return (size_t)0;
+      const size_t c = 160 * 1024 - fa.sharedSizeBytes;
+      return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_eot_resize_bwd_rows2),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)c) == hipSuccess ? c : (size_t)0;
+    }();
+    if (shm > cap) throw std::runtime_error("eot resize backward: span rows exceed the LDS");
+    hipLaunchKernelGGL(k_eot_resize_bwd_rows2, dim3(kBoxGrid), dim3(256), shm, s, d, place, spans, dstore, tstore);
+    PHX_LAUNCH_CHECK();
+    constexpr int RB = 16;
+    hipLaunchKernelGGL(k_eot_resize_bwd_cols2<RB>, dim3(cdiv(d.P, 64), cdiv(d.P, 4 * RB), d.B), dim3(256), 0, s, d,
+                       place, spans, tstore, dmatched);
+    PHX_LAUNCH_CHECK();
+    return;
+  }
   hipLaunchKernelGGL(k_eot_resize_bwd_rows, dim3(kBoxGrid), dim3(256), 0, s, d, place, spans, dstore,
                      tstore);
   PHX_LAUNCH_CHECK();

@@ -28,15 +28,18 @@ def _step(monkeypatch, fin_max, model, S, B, repeat=1):
     imgs = torch.as_tensor(synth_images(list(range(B)), S)).cuda()
     boxes = synth_boxes(list(range(B)), S)
     grads = []
+    w_first = None
     for _ in range(repeat):
         att.cur_step = 3
         att.call(imgs, boxes=boxes)
         torch.cuda.synchronize()
         grads.append(att.grad.clone())
+        if w_first is None:
+            w_first = v.read_weights().copy()  # moving statistics after one step
     m = torch.empty(B, device="cuda")
     v.ctx.call("phx_debug_last_maxscores", m.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     out = (att.grad.cpu().numpy().astype(np.float64), att.metrics_buf.cpu().numpy().copy(), m.cpu().numpy(),
-           v.read_weights().copy(), grads)
+           w_first, grads)
     del att, v
     torch.cuda.empty_cache()
     return out
