@@ -185,6 +185,7 @@ struct Exec {
   // activations (the arena tensors) stored as bf16: PHX_DTYPE_BF16, SURVEY.md 8a R4 "C4: bf16 act";
   // the program input (the images) and every gradient stay fp32
   bool abf = false;
+  uint64_t frozen_ver = 0;  // ctx->w_ver whose inference-BN statistics the BN slots hold (0: none)
   size_t bytes = 0;  // device bytes owned by this executor
   uint64_t used = 0;  // phx_ctx::clock at the last use
   std::vector<Guard> guards;  // PHX_GUARD_BYTES
@@ -270,6 +271,10 @@ struct phx_ctx {
   size_t wfloats = 0;
   std::string manifest_json;
   DPtr d_w, d_wt;
+  // version of the weights and moving statistics: bumped by every load and every training-mode
+  // forward (it may update the moving statistics); an executor's inference-BN statistics computed
+  // at this version are reused (Exec::frozen_ver)
+  uint64_t w_ver = 1;
   std::vector<long> wt_map;  // weight offset -> offset in d_wt (dense map over kernel entries)
   std::vector<std::pair<long, long>> wt_pairs;
   bool weights_loaded = false;
@@ -1168,6 +1173,12 @@ void plan_groups(Exec& E, bool local_bn) {
   }
 }
 
+// PHX_FROZEN_REUSE=0: every inference pass recomputes its BN statistics (A/B; read per call)
+bool frozen_reuse_off() {
+  const char* e = std::getenv("PHX_FROZEN_REUSE");
+  return e && e[0] == '0';
+}
+
 // the in-launch finalize descriptors of the executor's folded BNs (rebuilt when the weights buffer moves)
 void fin_prepare(phx_ctx* ctx, Exec& E) {
   const float* W = ctx->w();
@@ -1271,6 +1282,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
     }
     case OP_BN: {
       if (frozen) {  // inference BN (test_step): statistics from the moving averages
+        if (E.frozen_ver == ctx->w_ver && !frozen_reuse_off()) break;  // (kept from the last inference pass)
         for (int r = 0; r < n; ++r) {
           const Op& op = P.ops[g[r]];
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, E.slot_a[op.slot], E.slot_b[op.slot],
@@ -1408,6 +1420,15 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
   float* W = ctx->w();
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train || force_frozen;
   fin_prepare(ctx, E);
+  // inference BN: the statistics from the moving averages are a function of the weights, so the
+  // slots keep them from the last inference pass at the same weights version (the frozen protege of
+  // the defender: 108 launches per step saved); a training pass overwrites the slots and may move
+  // the moving statistics
+  const bool frozen_reuse = frozen && E.frozen_ver == ctx->w_ver && !frozen_reuse_off();
+  if (!frozen) {
+    E.frozen_ver = 0;
+    ++ctx->w_ver;
+  }
   if (E.ndrop && train)
     launch_drop_keep(E.drop_block, E.drop_p, E.ndrop, E.B, ctx->seed, step, gimg0, pass, E.drop_keep, s);
   if (E.ndrop && train) ck_note(E, "p" + std::to_string(pass) + " drop keep", E.drop_keep, (size_t)E.ndrop * E.B * 4, s);
@@ -1497,7 +1518,8 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         float* mean = E.slot_a[op.slot];
         float* rstd = E.slot_b[op.slot];
         // statistics only: the normalised output is applied by every consumer on load (InX)
-        if (frozen)
+        if (frozen && frozen_reuse) {
+        } else if (frozen)
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
                                  E.slot_c[op.slot], ti.c, kBnEps, s);
         else if (i >= 1 && E.xdw[i - 1]) {
@@ -1578,6 +1600,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     }
     ck_fwd(E, (int)i, pass, s);
   }
+  if (frozen) E.frozen_ver = ctx->w_ver;
 }
 
 bool is_cls_out(const Program& P, int t) {
@@ -2040,6 +2063,7 @@ int phx_load_weights(phx_ctx* ctx, const float* blob, size_t nfloats) {
   PHX_HIP(hipSetDevice(ctx->device));
   if (!ctx->d_w) ctx->d_w.reset(dalloc<float>(ctx->wfloats));
   PHX_HIP(hipMemcpy(ctx->d_w.get(), blob, nfloats * sizeof(float), hipMemcpyHostToDevice));
+  ++ctx->w_ver;
   // transposed copies of every 1x1 kernel: [Cout][Cin] for the forward GEMM
   std::vector<float> wt;
   ctx->wt_pairs.clear();
