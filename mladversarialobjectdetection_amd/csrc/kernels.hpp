@@ -67,9 +67,13 @@ struct Gemm2Plan {
   int P;           // statistics / BN-backward-sum partial rows the launch writes
   size_t res_lds;  // > 0: the A-resident kernel (k_gemm2r) with this much dynamic LDS; kslice then
                    // counts the N tiles of one workgroup's sweep and gy the sweeps
+  int wsk = 0;     // > 0: the wave-split-K kernel (k_gemm2k, kernels_gemm_wsk.hip) with tile tm x tn
 };
 Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false, bool allow_res = true);
 void gemm2_force_cfg(int wm, int tm, int tn, int splits);  // tools/gemm_bench sweeps only (0 = off)
+void gemm2_force_wsk(int tm, int tn);                       // tools/gemm_bench sweeps only (0 = off, -1 = never)
+struct Gemm2Args;
+void g2k_launch(int tm, int tn, int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a);
 int gemm_impl();
 int gemm_impl_for(int N, bool bf16 = false);
 int gemm2_target_wgs();

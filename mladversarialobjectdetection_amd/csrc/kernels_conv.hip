@@ -858,9 +858,13 @@ GemmPlan plan_gemm(int M, int N, int K) {
 size_t gemm_partial_floats(int M, int N, int K, bool bf16) {
   GemmPlan p = plan_gemm(M, N, K);
   Gemm2Plan q = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16);
+  // the implicit-im2col launches plan without the A-resident and wave-split-K kernels: they may
+  // split K across workgroups where a 1x1 conv of the same shape does not
+  Gemm2Plan g = plan_gemm2(M, N, K, gemm2_target_wgs(), bf16, false);
   const size_t a = p.splits > 1 ? (size_t)p.splits * M * N : 0;
   const size_t b = q.splits > 1 ? (size_t)q.splits * M * N : 0;
-  return std::max(a, b);
+  const size_t c = g.splits > 1 ? (size_t)g.splits * M * N : 0;
+  return std::max(a, std::max(b, c));
 }
 
 // which GEMM implementation launch_gemm / launch_gemm_dgrad use: PHX_GEMM=1 (16x16x4 register

@@ -67,6 +67,29 @@ static int g_force[4] = {0, 0, 0, 0};
 void gemm2_force_cfg(int wm, int tm, int tn, int splits) {
   g_force[0] = wm; g_force[1] = tm; g_force[2] = tn; g_force[3] = splits;
 }
+static int g_force_wsk[2] = {0, 0};
+void gemm2_force_wsk(int tm, int tn) {
+  g_force_wsk[0] = tm; g_force_wsk[1] = tn;
+}
+
+// Wave-split-K tile (k_gemm2k) for a shape k_gemm2 would split across workgroups: the largest
+// per-workgroup MFMA work that still spreads over the chip.  Cost model in units of one 32x32 MFMA
+// tile's chunk work per wave: a CU runs its cdiv(wgs, 256) workgroups' TM*TN tiles plus a fixed
+// per-chunk overhead of about two tiles (load wait, view, LDS store, barrier) each.
+static int wsk_pick(int M, int N) {
+  static const int cand[5][2] = {{2, 2}, {1, 3}, {2, 1}, {1, 2}, {1, 1}};
+  int best = 0;
+  long bc = 0;
+  for (auto& c : cand) {
+    const long wgs = (long)cdiv(M, 32 * c[0]) * cdiv(N, 32 * c[1]);
+    const long cost = (long)cdiv(wgs, 256) * (c[0] * c[1] + 2);
+    if (!best || cost < bc) {
+      best = c[0] * 10 + c[1];
+      bc = cost;
+    }
+  }
+  return best;
+}
 
 Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16, bool allow_res) {
   Gemm2Plan p;
@@ -120,6 +143,27 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16, bool allow_
   const int bk = bf16 ? PHX_GEMM_BK_BF16 : PHX_GEMM_BK_F32;  // K chunk of the kernel variant
   p.kslice = ((K + p.splits - 1) / p.splits + bk - 1) / bk * bk;
   p.splits = (K + p.kslice - 1) / p.kslice;
+  // deep K over few tiles: split K across the waves of a workgroup instead (k_gemm2k, fp32 only;
+  // PHX_GEMM_WSK=0 keeps the cross-workgroup split)
+  static const bool wsk_on = [] {
+    const char* e = std::getenv("PHX_GEMM_WSK");
+    return !(e && e[0] == '0');
+  }();
+  const bool wsk_forced = g_force_wsk[0] > 0;
+  if (allow_res && !bf16 && g_force_wsk[0] >= 0 && (wsk_forced || (wsk_on && p.splits > 1))) {
+    p.wsk = wsk_forced ? g_force_wsk[0] * 10 + g_force_wsk[1] : wsk_pick(M, N);
+    p.tm = p.wsk / 10;
+    p.tn = p.wsk % 10;
+    p.wm = 0;
+    p.mtiles = cdiv(M, 32 * p.tm);
+    p.gx = p.mtiles;
+    p.gy = cdiv(N, 32 * p.tn);
+    p.splits = 1;
+    p.kslice = K;
+    p.P = p.mtiles * p.tm;
+    p.res_lds = 0;
+    return p;
+  }
   const long want = std::max<long>(1, target_wgs / ((long)p.gy * p.splits));
   p.gx = (int)std::min<long>(p.mtiles, want);
   // with several N tiles, a multiple of 8 workgroups along M puts the gy workgroups that stream
@@ -172,6 +216,13 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
               float* partial, StatSink sink, int target_wgs, GradSink gsk, bool bf16) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
+  // the operands each mode's loads dereference (checked here: a null view pointer faults the device)
+  if (mode == 3 ? !(G.da && G.y && G.mu && G.rstd && G.sc && G.be && G.mdz && G.mdzx) : !A.p)
+    throw std::invalid_argument("gemm: missing A operand");
+  if ((mode == 1 || mode == 2) && !(A.mu && A.sc && A.be)) throw std::invalid_argument("gemm: BN view without parameters");
+  if (mode == 2 && !rowscale) throw std::invalid_argument("gemm: SE mode without a row scale");
+  if (!Bt || !C) throw std::invalid_argument("gemm: missing B or C");
+  if (gsk.part && !(gsk.y && gsk.mu && gsk.rstd && gsk.sc && gsk.be)) throw std::invalid_argument("gemm: GradSink without its BN");
   const Gemm2Plan p = plan_gemm2(M, N, K, target_wgs, bf16, mode != 4);
   const bool stats = sink.part != nullptr;
   if (stats && (acc || mode == 3 || (N & 3) || (p.splits > 1 && N > 1024)))
@@ -183,6 +234,14 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   if (gs && (p.splits > 1 || mode == 1 || mode == 2)) throw std::runtime_error("gemm: unsupported GradSink");
   gsk.P = p.P;
   const int sk = kstats ? 1 : gs ? 2 : 0;
+  if (p.wsk) {
+    if (g2_storage(A, G, gsk) != 0 || A.bf) throw std::logic_error("gemm2k: fp32 storage only");
+    const Gemm2Args w{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1, K,
+                      nullptr, sink, p.mtiles, gsk};
+    g2k_launch(p.tm, p.tn, mode, sk, dim3(p.gx, p.gy, 1), s, w);
+    PHX_LAUNCH_CHECK();
+    return p.P;
+  }
   Gemm2Group<1> a{};
   a.n = 1;
   if (mode == 4 && (stats || gs)) throw std::runtime_error("gemm: the implicit im2col has no fused sinks");
@@ -210,8 +269,10 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
 
 bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16) {
   if (n < 1 || n > kMaxSeg || gemm_impl_for(N, bf16) != 2) return false;
-  for (int i = 0; i < n; ++i)
-    if (plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16).splits != 1) return false;
+  for (int i = 0; i < n; ++i) {
+    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16);
+    if (p.splits != 1 || p.wsk) return false;
+  }
   return true;
 }
 

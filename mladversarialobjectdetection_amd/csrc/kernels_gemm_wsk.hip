@@ -1,0 +1,324 @@
+// kernels_gemm_wsk.hip — the deep-K 1x1-convolution GEMM: K split across the four waves of a
+// workgroup instead of across workgroups (fp32 matrix cores, v_mfma_f32_32x32x2_f32).
+//
+//   C[M,N] (+)= A'[M,K] * Bt[N,K]^T (+ bias)      A' as in k_gemm2 (raw, BN view, x SE rowscale,
+//                                                 gradient view)
+//
+// Why: the stage 5-7 convs (M = 4096-16384 rows, K = 320-1152) have fewer than 256 output tiles of
+// the k_gemm2 sizes, so k_gemm2 split K across workgroups: fp32 partial slabs in HBM, a second
+// launch to reduce them (with the BN statistics), and 16-deep K chunks per barrier whose fixed cost
+// (load wait, view, LDS store, barrier, two LDS read latencies) dwarfed the 8-24 MFMAs a wave ran per
+// chunk.  Here a workgroup owns one BM x BN output tile (TM x TN MFMA tiles of 32x32) and every wave
+// computes the whole tile over its own 16-deep slice of each 64-deep K chunk:
+//  * each barrier now covers TM*TN*8 MFMAs per wave on a 4x larger chunk, and the grid is one
+//    workgroup per output tile (no partial slabs, no reduce launch);
+//  * the four per-wave accumulators are summed through LDS in wave order 0, 1, 2, 3 (fixed order:
+//    bit-reproducible run to run), each wave finishing TM*TN/4 of the tiles;
+//  * epilogue as k_gemm2 (bias, accumulate, C store), and the consumer BN's batch statistics
+//    (StatSink) or the BN-backward sums of a dgrad (GradSink) per 32-row tile: partial row
+//    blockIdx.x * TM + i, so these shapes fuse their sinks like the unsplit ones (the split-K reduce
+//    and the separate BN-backward reduction launches go away).
+// LDS: two 64-deep chunks of A (BM rows) and B (BN rows), rows of 16 XOR-swizzled 16-B units
+// (g2_off: a 16-lane ds_read_b128 group covers 16 distinct units, conflict-free); the cross-wave
+// sum reuses the same array.  fp32 compute and fp32 storage only (the bf16 context keeps k_gemm2).
+#include "gemm2_kernel.hpp"
+
+namespace phx {
+
+template <int TM, int TN>
+struct G2K {
+  static constexpr int BM = 32 * TM, BN = 32 * TN, BK = 64, LD = 64, KQ = 16;
+  static constexpr int NA = BM / 16, NB = BN / 16;  // float4 per thread per chunk (16 rows per pass)
+  static constexpr int ESZ = 4;
+  static constexpr int IMG = 2 * (BM + BN) * LD;    // double-buffered chunk image (floats)
+  static constexpr int RED = 4 * TM * TN * 1024;    // per-wave accumulators (floats)
+  static constexpr int LDS_FLOATS = IMG > RED ? IMG : RED;
+};
+
+template <class P, int MODE>
+struct G2KRegs {
+  float4 a[P::NA];
+  float4 y[MODE == 3 ? P::NA : 1];
+  float4 rs[MODE == 2 ? P::NA : 1];
+  float4 b[P::NB];
+  Chan4 ck;
+  GChan4 gk;
+};
+
+// the chunk at k0: thread t loads quad t % 16 of rows t / 16 + 16u (clamped addresses; g2k_store
+// zeroes what lies outside the matrices)
+template <class P, int MODE>
+__device__ __forceinline__ void g2k_load(G2KRegs<P, MODE>& r, const Gemm2Args& a, int m0, int n0, int k0) {
+  const int t = threadIdx.x;
+  const int kk = k0 + 4 * (t & 15);
+  const int kc = kk < a.K ? kk : a.K - 4;
+  if (MODE == 1 || MODE == 2) r.ck = inx_chan4(a.A, kc);
+  if (MODE == 3) r.gk = gx_chan4(a.G, kc);
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) {
+    const int row = min(m0 + (t >> 4) + 16 * u, a.M - 1);
+    const long e = (long)row * a.K + kc;
+    if (MODE == 3) {
+      r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
+      r.y[u] = *reinterpret_cast<const float4*>(a.G.y + e);
+    } else {
+      r.a[u] = *reinterpret_cast<const float4*>(a.A.p + e);
+      if (MODE == 2) r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(row / a.rpi) * a.K + kc);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) {
+    const int col = min(n0 + (t >> 4) + 16 * u, a.N - 1);
+    r.b[u] = *reinterpret_cast<const float4*>(a.Bt + (long)col * a.K + kc);
+  }
+}
+
+template <class P, int MODE, int ACT>
+__device__ __forceinline__ void g2k_store_act(const G2KRegs<P, MODE>& r, const Gemm2Args& a, float* img, int m0,
+                                              int n0, int k0) {
+  const int t = threadIdx.x;
+  const int q = t & 15;
+  const bool kok = k0 + 4 * q < a.K;
+  InX ax = a.A;
+  ax.act = ACT;
+  GradX gx = a.G;
+  gx.act = ACT;
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) {
+    const int rl = (t >> 4) + 16 * u;
+    float4 v = r.a[u];
+    if (kok && m0 + rl < a.M) {
+      if (MODE == 1 || MODE == 2) v = inx_apply4(ax, r.ck, v);
+      if (MODE == 2) {
+        v.x *= r.rs[u].x; v.y *= r.rs[u].y; v.z *= r.rs[u].z; v.w *= r.rs[u].w;
+      }
+      if (MODE == 3) v = gx_apply4(gx, r.gk, v, r.y[u]);
+    } else {
+      v = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    *reinterpret_cast<float4*>(img + g2_off<P>(rl, 4 * q)) = v;
+  }
+  float* bimg = img + P::BM * P::LD;
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) {
+    const int cl = (t >> 4) + 16 * u;
+    const bool ok = kok && n0 + cl < a.N;
+    *reinterpret_cast<float4*>(bimg + g2_off<P>(cl, 4 * q)) = ok ? r.b[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <class P, int MODE>
+__device__ __forceinline__ void g2k_store(const G2KRegs<P, MODE>& r, const Gemm2Args& a, float* img, int m0, int n0,
+                                          int k0) {
+  const int act = MODE == 0 ? 0 : MODE == 3 ? a.G.act : a.A.act;
+  if (act == 1) g2k_store_act<P, MODE, 1>(r, a, img, m0, n0, k0);
+  else if (act == 2) g2k_store_act<P, MODE, 2>(r, a, img, m0, n0, k0);
+  else g2k_store_act<P, MODE, 0>(r, a, img, m0, n0, k0);
+}
+
+// SK: 0 plain, 1 StatSink, 2 GradSink (as k_gemm2).  Grid (cdiv(M, BM), cdiv(N, BN)).
+template <int TM, int TN, int MODE, int SK>
+__global__ __launch_bounds__(256, 2) void k_gemm2k(Gemm2Args a) {
+  using P = G2K<TM, TN>;
+  constexpr int BM = P::BM, BN = P::BN, NT = TM * TN;
+  __shared__ __attribute__((aligned(16))) float sm[P::LDS_FLOATS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int nch = (a.K + P::BK - 1) / P::BK;
+  G2KRegs<P, MODE> rg;
+  g2k_load<P, MODE>(rg, a, m0, n0, 0);
+  g2k_store<P, MODE>(rg, a, sm, m0, n0, 0);
+  __syncthreads();
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  for (int c = 0; c < nch; ++c) {
+    float* const img = sm + (c & 1) * (P::IMG / 2);
+    // the next chunk's loads first (past the end: the last chunk again, unused), unconditionally so
+    // the MFMAs below do not wait for them
+    g2k_load<P, MODE>(rg, a, m0, n0, min(c + 1, nch - 1) * P::BK);
+    __builtin_amdgcn_sched_barrier(0);
+    const int kvalid = a.K - (c * P::BK + 16 * w);  // this wave's k of the chunk that exist
+    if (kvalid > 0) {                                 // wave-uniform
+      const float* As = img;
+      const float* Bs = img + BM * P::LD;
+      float4 fa[2][TM], fb[2][TN];
+#pragma unroll
+      for (int s8 = 0; s8 < 2; ++s8) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[s8][i] = *reinterpret_cast<const float4*>(As + g2_off<P>(i * 32 + r32, 16 * w + 8 * s8 + 4 * h));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[s8][j] = *reinterpret_cast<const float4*>(Bs + g2_off<P>(j * 32 + r32, 16 * w + 8 * s8 + 4 * h));
+      }
+#pragma unroll
+      for (int s8 = 0; s8 < 2; ++s8) {
+        if (s8 > 0 && kvalid <= 8) break;  // wave-uniform
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s8][i].x, fb[s8][j].x, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s8][i].y, fb[s8][j].y, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s8][i].z, fb[s8][j].z, acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[s8][i].w, fb[s8][j].w, acc[i][j], 0, 0, 0);
+          }
+      }
+    }
+    if (c + 1 < nch) g2k_store<P, MODE>(rg, a, sm + ((c + 1) & 1) * (P::IMG / 2), m0, n0, (c + 1) * P::BK);
+    __syncthreads();
+  }
+  // ---- cross-wave sum: wave w stores its tiles as [w][tile][e/4][lane] float4 (1 KB per
+  // instruction, contiguous), then wave v sums tiles v, v + 4, ... over the waves in order ----
+  float4* red = reinterpret_cast<float4*>(sm);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e4 = 0; e4 < 4; ++e4)
+        red[((w * NT + i * TN + j) * 4 + e4) * 64 + lane] =
+            make_float4(acc[i][j][4 * e4], acc[i][j][4 * e4 + 1], acc[i][j][4 * e4 + 2], acc[i][j][4 * e4 + 3]);
+  __syncthreads();
+  for (int qt = w; qt < NT; qt += 4) {  // wave-uniform
+    const int i = qt / TN, j = qt % TN;
+    float v[16];
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {
+      float4 s = red[(qt * 4 + e4) * 64 + lane];
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) {
+        const float4 o = red[((ww * NT + qt) * 4 + e4) * 64 + lane];
+        s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+      }
+      v[4 * e4] = s.x; v[4 * e4 + 1] = s.y; v[4 * e4 + 2] = s.z; v[4 * e4 + 3] = s.w;
+    }
+    // ---- epilogue of tile (i, j): lane (r32, h) holds column r32, rows (e&3) + 8*(e>>2) + 4*h ----
+    const int row0 = m0 + i * 32;
+    const int col = n0 + j * 32 + r32;
+    const bool cok = col < a.N;
+    const bool full = row0 + 32 <= a.M && n0 + j * 32 + 32 <= a.N;
+    const float bv = a.bias ? a.bias[min(col, a.N - 1)] : 0.f;
+    if (full) {
+      const long cbase = (long)(row0 + 4 * h) * a.N + col;
+      float old[16];
+      if (a.acc) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) old[e] = a.C[cbase + (long)((e & 3) + 8 * (e >> 2)) * a.N];
+      }
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        float x = v[e] + bv;
+        v[e] = x;
+        if (a.acc) x += old[e];
+        a.C[cbase + (long)((e & 3) + 8 * (e >> 2)) * a.N] = x;
+        if (SK == 2) v[e] = x;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        float x = v[e] + bv;
+        v[e] = x;
+        if (cok && row < a.M) {
+          const long ce = (long)row * a.N + col;
+          if (a.acc) x += a.C[ce];
+          a.C[ce] = x;
+          if (SK == 2) v[e] = x;
+        }
+      }
+    }
+    const long prow = (long)blockIdx.x * TM + i;  // this tile's partial row of the sink
+    if constexpr (SK == 1) {
+      const float nw = (float)max(0, min(32, a.M - row0));
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (full || row0 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) s += v[e];
+      s += __shfl_xor(s, 32);
+      const float mean = nw > 0.f ? s / nw : 0.f;
+      float q = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        if (full || row0 + (e & 3) + 8 * (e >> 2) + 4 * h < a.M) {
+          const float d = v[e] - mean;
+          q = fmaf(d, d, q);
+        }
+      q += __shfl_xor(q, 32);
+      if (h == 0 && cok) sink_put(a.sink, prow, col, nw, mean, q);
+      if (j == 0 && blockIdx.y == 0 && lane == 0) sink_cnt(a.sink, prow, nw);
+    }
+    if constexpr (SK == 2) {
+      const int cc = min(col, a.N - 1);
+      const float mu = a.gsk.mu[cc], rs = a.gsk.rstd[cc], sc = a.gsk.sc[cc], be = a.gsk.be[cc];
+      float yv[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = min(row0 + (e & 3) + 8 * (e >> 2) + 4 * h, a.M - 1);
+        yv[e] = a.gsk.y[(long)row * a.N + cc];
+      }
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = row0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (cok && row < a.M) gs_one(v[e], yv[e], mu, rs, sc, be, a.gsk.act, s1, s2);
+      }
+      s1 += __shfl_xor(s1, 32);
+      s2 += __shfl_xor(s2, 32);
+      if (h == 0 && cok) gsink_put(a.gsk, prow, col, s1, s2);
+    }
+  }
+  if constexpr (SK != 0) {
+    // in-launch finalize (FinDesc): TM partial rows of this workgroup's columns
+    const unsigned ent = (unsigned)(TM * max(0, min(BN, a.N - n0)));
+    __syncthreads();  // (every wave's LDS reads are done before the scratch word is reused)
+    if constexpr (SK == 1) sink_finish(a.sink, ent, sm);
+    else gsink_finish(a.gsk, ent, sm);
+  }
+}
+
+template <int TM, int TN>
+static void g2k_go(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a) {
+  switch (mode) {
+    case 0:
+      if (sk == 1) PHX_TLAUNCH((k_gemm2k<TM, TN, 0, 1>), g, dim3(256), 0, s, a);
+      else if (sk == 2) PHX_TLAUNCH((k_gemm2k<TM, TN, 0, 2>), g, dim3(256), 0, s, a);
+      else PHX_TLAUNCH((k_gemm2k<TM, TN, 0, 0>), g, dim3(256), 0, s, a);
+      break;
+    case 1:
+      if (sk == 1) PHX_TLAUNCH((k_gemm2k<TM, TN, 1, 1>), g, dim3(256), 0, s, a);
+      else PHX_TLAUNCH((k_gemm2k<TM, TN, 1, 0>), g, dim3(256), 0, s, a);
+      break;
+    case 2:
+      if (sk == 1) PHX_TLAUNCH((k_gemm2k<TM, TN, 2, 1>), g, dim3(256), 0, s, a);
+      else PHX_TLAUNCH((k_gemm2k<TM, TN, 2, 0>), g, dim3(256), 0, s, a);
+      break;
+    case 3:
+      if (sk == 2) PHX_TLAUNCH((k_gemm2k<TM, TN, 3, 2>), g, dim3(256), 0, s, a);
+      else PHX_TLAUNCH((k_gemm2k<TM, TN, 3, 0>), g, dim3(256), 0, s, a);
+      break;
+    default:
+      throw std::logic_error("gemm2k: no implicit im2col");
+  }
+}
+
+void g2k_launch(int tm, int tn, int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a) {
+  if ((mode == 1 || mode == 2) && sk == 2) throw std::logic_error("gemm2k: GradSink on a forward view");
+  if (mode == 3 && sk == 1) throw std::logic_error("gemm2k: StatSink on a gradient view");
+  switch (tm * 10 + tn) {
+    case 11: g2k_go<1, 1>(mode, sk, g, s, a); break;
+    case 12: g2k_go<1, 2>(mode, sk, g, s, a); break;
+    case 13: g2k_go<1, 3>(mode, sk, g, s, a); break;
+    case 21: g2k_go<2, 1>(mode, sk, g, s, a); break;
+    case 22: g2k_go<2, 2>(mode, sk, g, s, a); break;
+    default: throw std::logic_error("gemm2k: no kernel for this tile");
+  }
+}
+
+}  // namespace phx

@@ -81,7 +81,7 @@ int main(int argc, char** argv) {
   fill(mu, 4096, 4); fill(scl, 4096, 5); fill(be, 4096, 6); fill(m1, 4096, 7); fill(m2, 4096, 8);
   fill(ybuf, maxA, 9);
   for (auto& s : shapes) {
-    InX ax{A, mode == 1 ? mu : nullptr, scl, be, mode == 1 ? 1 : 0};
+    InX ax{A, mode == 1 || mode == 2 ? mu : nullptr, scl, be, mode == 1 || mode == 2 ? 1 : 0};
     GradX gx{A, ybuf, mu, scl, scl, be, m1, m2, 1};
     // GEMM_NOSTATS=1: every shape without the statistics epilogue (its cost by difference)
     StatSink sink = (s.stats && mode != 3 && !getenv("GEMM_NOSTATS")) ? StatSink{sp, sc, s.N, 0} : StatSink{};
@@ -93,8 +93,8 @@ int main(int argc, char** argv) {
         gemm2_run(3, InX{A, nullptr, nullptr, nullptr, 0}, gx, Bt, nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st,
                   part, StatSink{}, wgs);
       else
-        gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st, part, sink,
-                  wgs);
+        gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, mode == 2 ? m1 : nullptr,
+                  mode == 2 ? s.M : 1, st, part, sink, wgs);
     };
     const int impl0 = getenv("GEMM_IMPL1") ? 1 : 2;
     for (impl = impl0; impl <= 2; ++impl) {
@@ -143,6 +143,60 @@ int main(int argc, char** argv) {
   }
   printf("impl1 total %.1f us; impl2 total %.1f us, roofline %.1f us (%.0f%%)\n", tot1, tot_us, tot_roof,
          100 * tot_roof / tot_us);
+  // GEMM_WSK=1: per shape, the cross-workgroup split (wave-split-K off) against every forced
+  // wave-split-K tile (k_gemm2k); max |C - C_split| and the time of each
+  if (getenv("GEMM_WSK")) {
+    printf("wsk sweep mode %d\n", mode);
+    const int tiles[5][2] = {{1, 1}, {1, 2}, {1, 3}, {2, 1}, {2, 2}};
+    for (auto& s : shapes) {
+      InX ax{A, mode == 1 || mode == 2 ? mu : nullptr, scl, be, mode == 1 || mode == 2 ? 1 : 0};
+      GradX gx{A, ybuf, mu, scl, scl, be, m1, m2, 1};
+      StatSink sink = (s.stats && mode != 3) ? StatSink{sp, sc, s.N, 0} : StatSink{};
+      auto go = [&]() {
+        if (mode == 3)
+          gemm2_run(3, InX{A, nullptr, nullptr, nullptr, 0}, gx, Bt, nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st,
+                    part, StatSink{}, wgs);
+        else
+          gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, mode == 2 ? m1 : nullptr,
+                    mode == 2 ? s.M : 1, st, part, sink, wgs);
+      };
+      auto timeit = [&]() {
+        for (int i = 0; i < 3; ++i) go();
+        hipEventRecord(e0, st);
+        for (int i = 0; i < 20; ++i) go();
+        hipEventRecord(e1, st);
+        hipEventSynchronize(e1);
+        float ms;
+        hipEventElapsedTime(&ms, e0, e1);
+        return ms * 1e3 / 20;
+      };
+      gemm2_force_wsk(-1, 0);
+      go();
+      hipStreamSynchronize(st);
+      std::vector<float> base((size_t)s.M * s.N), hc(base.size());
+      hipMemcpy(base.data(), C, base.size() * 4, hipMemcpyDeviceToHost);
+      const double tb = timeit();
+      Gemm2Plan q = plan_gemm2(s.M, s.N, s.K, wgs);
+      printf("wsk M=%8d N=%5d K=%5d split  grid=%dx%dx%d  %8.1f us\n", s.M, s.N, s.K, q.gx, q.gy, q.splits, tb);
+      for (auto& t : tiles) {
+        gemm2_force_wsk(t[0], t[1]);
+        go();
+        hipStreamSynchronize(st);
+        hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost);
+        double md = 0, mr = 0;
+        for (size_t i = 0; i < hc.size(); ++i) {
+          md = std::max(md, (double)std::fabs(hc[i] - base[i]));
+          mr = std::max(mr, (double)std::fabs(base[i]));
+        }
+        const double tw = timeit();
+        printf("wsk M=%8d N=%5d K=%5d tile=%d%d %8.1f us  x%.2f  maxdiff %.2e (max |C| %.2e)\n", s.M, s.N, s.K, t[0],
+               t[1], tw, tb / tw, md, mr);
+      }
+      gemm2_force_wsk(0, 0);
+      Gemm2Plan d = plan_gemm2(s.M, s.N, s.K, wgs);
+      printf("wsk M=%8d N=%5d K=%5d default wsk=%d\n", s.M, s.N, s.K, d.wsk);
+    }
+  }
   // GEMM_SWEEP=1: every tile configuration x split count per shape (stats epilogue as listed)
   if (getenv("GEMM_SWEEP")) {
     // GEMM_MODE=1: A through a BN + swish view; 3: a BN-backward gradient view (dgrad, no stats)
@@ -152,7 +206,7 @@ int main(int argc, char** argv) {
     const int cfgs[8][3] = {{4, 1, 1}, {4, 1, 2}, {4, 1, 3}, {4, 1, 5}, {2, 2, 2}, {2, 1, 2}, {2, 1, 1}, {1, 1, 1}};
     const int splits_opt[4] = {1, 2, 4, 8};
     for (auto& s : shapes) {
-      InX ax{A, mode == 1 ? mu : nullptr, scl, be, mode == 1 ? 1 : 0};
+      InX ax{A, mode == 1 || mode == 2 ? mu : nullptr, scl, be, mode == 1 || mode == 2 ? 1 : 0};
       GradX gx{A, ybuf, mu, scl, scl, be, m1, m2, 1};
       StatSink sink = (s.stats && mode != 3) ? StatSink{sp, sc, s.N, 0} : StatSink{};
       double best = 1e30;
@@ -168,8 +222,8 @@ int main(int argc, char** argv) {
               gemm2_run(3, InX{A, nullptr, nullptr, nullptr, 0}, gx, Bt, nullptr, C, s.M, s.N, s.K, false, nullptr,
                         1, st, part, StatSink{}, wgs, GradSink{}, bf);
             else
-              gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st,
-                        part, sink, wgs, GradSink{}, bf);
+              gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false,
+                        mode == 2 ? m1 : nullptr, mode == 2 ? s.M : 1, st, part, sink, wgs, GradSink{}, bf);
           };
           for (int i = 0; i < 3; ++i) go();
           hipEventRecord(e0, st);
