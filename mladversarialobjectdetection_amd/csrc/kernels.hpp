@@ -73,7 +73,7 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false, boo
 void gemm2_force_cfg(int wm, int tm, int tn, int splits);  // tools/gemm_bench sweeps only (0 = off)
 void gemm2_force_wsk(int tm, int tn);                       // tools/gemm_bench sweeps only (0 = off, -1 = never)
 struct Gemm2Args;
-void g2k_launch(int tm, int tn, int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a);
+void g2k_launch(int tm, int tn, int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a, bool bf16, int st);
 int gemm_impl();
 int gemm_impl_for(int N, bool bf16 = false);
 int gemm2_target_wgs();

@@ -143,14 +143,26 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16, bool allow_
   const int bk = bf16 ? PHX_GEMM_BK_BF16 : PHX_GEMM_BK_F32;  // K chunk of the kernel variant
   p.kslice = ((K + p.splits - 1) / p.splits + bk - 1) / bk * bk;
   p.splits = (K + p.kslice - 1) / p.kslice;
-  // deep K over few tiles: split K across the waves of a workgroup instead (k_gemm2k, fp32 only;
-  // PHX_GEMM_WSK=0 keeps the cross-workgroup split)
+  // deep K over few tiles: split K across the waves of a workgroup instead (k_gemm2k; PHX_GEMM_WSK=0
+  // keeps the cross-workgroup split)
   static const bool wsk_on = [] {
     const char* e = std::getenv("PHX_GEMM_WSK");
     return !(e && e[0] == '0');
   }();
+  // PHX_GEMM_WSK_BF16=1: the bf16 compute type takes k_gemm2k too (default off: C4 28.25 -> 28.07 ms,
+  // gradient unchanged against the oracle, but the D4 256^2 step's loss lands 4.9e-3 from fp64
+  // against 5e-5 with the split kernels, outside test_gpu_bf16's emulation bound)
+  static const bool wsk_bf16 = [] {
+    const char* e = std::getenv("PHX_GEMM_WSK_BF16");
+    return e && e[0] == '1';
+  }();
+  // bf16: the A view (fp32 VALU, once per N tile) outweighs the cheap bf16 MFMAs, so a split tile that
+  // spans all of N exactly (one view pass: N = 160 on 128x160) stays faster than the narrower
+  // wave-split tiles (tools/gemm_bench GEMM_WSK sweeps, D4 shapes)
+  const bool bf16_keep = bf16 && p.gy == 1 && N % c.bn() == 0;
   const bool wsk_forced = g_force_wsk[0] > 0;
-  if (allow_res && !bf16 && g_force_wsk[0] >= 0 && (wsk_forced || (wsk_on && p.splits > 1))) {
+  if (allow_res && g_force_wsk[0] >= 0 &&
+      (wsk_forced || (wsk_on && p.splits > 1 && (!bf16 || (wsk_bf16 && !bf16_keep))))) {
     p.wsk = wsk_forced ? g_force_wsk[0] * 10 + g_force_wsk[1] : wsk_pick(M, N);
     p.tm = p.wsk / 10;
     p.tn = p.wsk % 10;
@@ -235,10 +247,9 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
   gsk.P = p.P;
   const int sk = kstats ? 1 : gs ? 2 : 0;
   if (p.wsk) {
-    if (g2_storage(A, G, gsk) != 0 || A.bf) throw std::logic_error("gemm2k: fp32 storage only");
     const Gemm2Args w{A, G, Bt, bias, C, M, N, K, acc ? 1 : 0, rowscale, mode == 2 ? rows_per_img : 1, K,
                       nullptr, sink, p.mtiles, gsk};
-    g2k_launch(p.tm, p.tn, mode, sk, dim3(p.gx, p.gy, 1), s, w);
+    g2k_launch(p.tm, p.tn, mode, sk, dim3(p.gx, p.gy, 1), s, w, bf16, g2_storage(A, G, gsk));
     PHX_LAUNCH_CHECK();
     return p.P;
   }

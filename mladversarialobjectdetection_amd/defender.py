@@ -20,6 +20,78 @@ import torch
 from . import _lib
 from . import distributed as ddp
 from .attacker import EfficientDetVictim, _pad_boxes, _stream
+from .h5 import read_keras_weights, write_keras_weights
+
+KERAS_MODEL = "patch_neutralizer"  # generator.py:80: PatchNeutralizer's name; its output conv is
+                                   # Conv2D(name='patch_neutralizer/output') (generator.py:81)
+
+
+def _keras_layer(name: str) -> str:
+    """The top-level Keras layer of a manifest variable: PatchNeutralizer's tracked layers are the
+    encoder blocks conv0..conv4, the decoder blocks deconv0..deconv3 (generator.py:30-41) and the
+    output conv (generator.py:81)."""
+    top = name.split("/")[0]
+    return f"{KERAS_MODEL}/output" if top == "output" else top
+
+
+def _keras_name(name: str) -> str:
+    return (f"{KERAS_MODEL}/{name}" if name.split("/")[0] == "output" else name) + ":0"
+
+
+def keras_weight_layers(manifest: dict, params: np.ndarray, moving: np.ndarray):
+    """The U-Net's variables as Keras's HDF5 `save_weights` lays them out: one entry per top-level
+    layer in PatchNeutralizer's order, each layer's weights as Keras's Layer.weights lists them —
+    the trainable ones in build order (kernel, bias / gamma, beta), then the non-trainable BN moving
+    mean / variance in build order."""
+    order, by = [], {}
+    for p in manifest["params"]:
+        lay = _keras_layer(p["name"])
+        if lay not in by:
+            by[lay] = ([], [])
+            order.append(lay)
+        n = int(np.prod(p["shape"]))
+        by[lay][0].append((_keras_name(p["name"]), params[p["offset"]:p["offset"] + n].reshape(p["shape"])))
+    for b in manifest["bn"]:
+        lay, c = _keras_layer(b["name"]), b["channels"]
+        by[lay][1].append((_keras_name(b["name"] + "/moving_mean"), moving[b["moving_mean"]:b["moving_mean"] + c]))
+        by[lay][1].append((_keras_name(b["name"] + "/moving_variance"),
+                           moving[b["moving_variance"]:b["moving_variance"] + c]))
+    return [(lay, by[lay][0] + by[lay][1]) for lay in order]
+
+
+def from_keras_weight_layers(manifest: dict, layers):
+    """(flat trainable variables, flat moving statistics) from read_keras_weights' layers.  A file
+    weight (':0' dropped) matches the manifest variable whose name it equals or ends with after a
+    '/' (Keras may prefix nested variable names with their outer layers' scopes); every manifest
+    variable must be matched exactly once, with its shape."""
+    want = {p["name"]: ("p", p["offset"], tuple(p["shape"])) for p in manifest["params"]}
+    for b in manifest["bn"]:
+        want[b["name"] + "/moving_mean"] = ("m", b["moving_mean"], (b["channels"],))
+        want[b["name"] + "/moving_variance"] = ("m", b["moving_variance"], (b["channels"],))
+    out = np.zeros(manifest["n_params"], np.float32)
+    mv = np.zeros(manifest["n_moving"], np.float32)
+    seen = set()
+    for _, weights in layers:
+        for wname, arr in weights:
+            w = wname[:-2] if wname.endswith(":0") else wname
+            if w.startswith(KERAS_MODEL + "/"):
+                w = w[len(KERAS_MODEL) + 1:]
+            hits = [m for m in want if w == m or w.endswith("/" + m)]
+            if not hits:
+                raise ValueError(f"antipatch: weight {wname!r} matches no U-Net variable")
+            m = max(hits, key=len)
+            if m in seen:
+                raise ValueError(f"antipatch: {m} appears twice")
+            kind, off, shape = want[m]
+            a = np.asarray(arr, np.float32)
+            if a.shape != shape:
+                raise ValueError(f"antipatch: {wname} has shape {a.shape}, the U-Net needs {shape}")
+            (out if kind == "p" else mv)[off:off + a.size] = a.reshape(-1)
+            seen.add(m)
+    missing = sorted(set(want) - seen)
+    if missing:
+        raise ValueError(f"antipatch: missing {missing[:4]}{' ...' if len(missing) > 4 else ''}")
+    return out, mv
 
 
 def _fans(shape, transpose=False):
@@ -208,14 +280,17 @@ class PatchAttackDefender:
         return out
 
     def save_weights(self, dirpath, **kwargs):
-        """attack_detection.py:300-308 saves antipatch.h5; h5py is not available here, so the same
-        variables go to antipatch.npz under their Keras names (plus the BN moving statistics, as
-        their mean over ranks).  Under data parallelism every rank calls it (the moving statistics
-        are all-reduced) and rank 0 writes the file."""
+        """attack_detection.py:300-308: `self._antipatch.save_weights(dirpath/antipatch.h5)` — the U-Net
+        variables and BN moving statistics in Keras's HDF5 weights layout (h5.py; the moving
+        statistics as their mean over ranks), plus the same variables in antipatch.npz under their
+        Keras names.  Under data parallelism every rank calls it (the moving statistics are
+        all-reduced) and rank 0 writes the files."""
         mv = self.moving_statistics(replica_mean=True)
         if ddp.rank() != 0:
             return
         os.makedirs(dirpath)
+        params = self.params.detach().cpu().numpy()
+        write_keras_weights(os.path.join(dirpath, "antipatch.h5"), keras_weight_layers(self.manifest, params, mv))
         arrs = {k: v.detach().cpu().numpy() for k, v in self._trainable_variables.items()}
         for b in self.manifest["bn"]:
             arrs[b["name"] + "/moving_mean"] = mv[b["moving_mean"]:b["moving_mean"] + b["channels"]]
@@ -223,7 +298,17 @@ class PatchAttackDefender:
         np.savez(os.path.join(dirpath, "antipatch.npz"), **arrs)
 
     def _read_npz(self, path):
-        p = os.path.join(path, "antipatch.npz") if os.path.isdir(path) else path
+        """initial_weights (attack_detection.py:54-55 `load_weights`): an .h5 Keras weights file, an
+        .npz of this class's save_weights, or a directory holding antipatch.h5 (preferred) or
+        antipatch.npz.  Sets the BN moving statistics; returns the flat trainable variables."""
+        p = path
+        if os.path.isdir(path):
+            h5 = os.path.join(path, "antipatch.h5")
+            p = h5 if os.path.exists(h5) else os.path.join(path, "antipatch.npz")
+        if str(p).endswith((".h5", ".hdf5", ".keras")):
+            out, mv = from_keras_weight_layers(self.manifest, read_keras_weights(p))
+            self.handle.call("phx_def_moving", None, mv.ctypes.data, None)
+            return out
         z = np.load(p)
         out = np.zeros(self.handle.num_params, np.float32)
         for q in self.manifest["params"]:

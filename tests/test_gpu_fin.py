@@ -1,6 +1,6 @@
 """In-launch BN finalize (GPU): a producer's last-arriving workgroup folds the BN partials itself
 (common.hpp fin_arrive: write-through partial stores, an agent-scope ticket, one acquire) instead
-of a k_bn_finalize launch.  The executor folds the BNs whose C * P <= PHX_FIN_MAX (default 8192;
+of a k_bn_finalize launch.  The executor folds the BNs whose C * P <= PHX_FIN_MAX (default 0, off;
 read per executor).  The fold adds the same fp64 partial sums in another order than the separate
 launch, so the comparison is to rounding: loss, per-image max scores, the gradient and the moving
 statistics of a D0 / D1 step with every eligible BN folded (PHX_FIN_MAX huge, so the multi-chunk

@@ -41,7 +41,10 @@ int main(int argc, char** argv) {
       {16384, 112, 480, false, true},  {4096, 64, 320, true, true},     {65536, 40, 240, false, true},
       {65536, 144, 24, false, true},
       // large, square-ish: the kernel's MFMA ceiling without shape effects
-      {65536, 512, 512, false, false}, {65536, 512, 512, false, true},  {16384, 1024, 1024, false, false}};
+      {65536, 512, 512, false, false}, {65536, 512, 512, false, true},  {16384, 1024, 1024, false, false},
+      // D4 1024^2 x 4 deep-K shapes (indices 24-27)
+      {4096, 272, 1632, false, true},  {16384, 160, 960, false, true},  {4096, 1632, 272, false, true},
+      {16384, 224, 224, false, true}};
   // GEMM_ONLY=i,j,...: run only those shape indices
   if (const char* e = getenv("GEMM_ONLY")) {
     std::vector<S> keep;
@@ -146,19 +149,52 @@ int main(int argc, char** argv) {
   // GEMM_WSK=1: per shape, the cross-workgroup split (wave-split-K off) against every forced
   // wave-split-K tile (k_gemm2k); max |C - C_split| and the time of each
   if (getenv("GEMM_WSK")) {
-    printf("wsk sweep mode %d\n", mode);
+    // GEMM_BF16=1: bf16 matrix cores on bf16 activations (forward modes: A and C bf16; gradient view:
+    // y bf16), as a bf16 context runs them
+    const bool wbf = getenv("GEMM_BF16") != nullptr;
+    uint16_t *Ab = nullptr, *yb = nullptr;
+    if (wbf) {
+      std::vector<uint16_t> h(maxA);
+      srand(11);
+      for (auto& v : h) {
+        const float f = (float)rand() / RAND_MAX * 2.f - 1.f;
+        uint32_t u;
+        memcpy(&u, &f, 4);
+        v = (uint16_t)(u >> 16);
+      }
+      hipMalloc(&Ab, maxA * 2);
+      hipMalloc(&yb, maxA * 2);
+      hipMemcpy(Ab, h.data(), maxA * 2, hipMemcpyHostToDevice);
+      hipMemcpy(yb, h.data(), maxA * 2, hipMemcpyHostToDevice);
+    }
+    printf("wsk sweep mode %d bf16 %d\n", mode, (int)wbf);
     const int tiles[5][2] = {{1, 1}, {1, 2}, {1, 3}, {2, 1}, {2, 2}};
     for (auto& s : shapes) {
-      InX ax{A, mode == 1 || mode == 2 ? mu : nullptr, scl, be, mode == 1 || mode == 2 ? 1 : 0};
-      GradX gx{A, ybuf, mu, scl, scl, be, m1, m2, 1};
+      InX ax{wbf ? reinterpret_cast<const float*>(Ab) : A, mode == 1 || mode == 2 ? mu : nullptr, scl, be,
+             mode == 1 || mode == 2 ? 1 : 0, wbf ? 1 : 0};
+      GradX gx{A, wbf ? reinterpret_cast<const float*>(yb) : ybuf, mu, scl, scl, be, m1, m2, 1, wbf ? 1 : 0};
       StatSink sink = (s.stats && mode != 3) ? StatSink{sp, sc, s.N, 0} : StatSink{};
       auto go = [&]() {
         if (mode == 3)
           gemm2_run(3, InX{A, nullptr, nullptr, nullptr, 0}, gx, Bt, nullptr, C, s.M, s.N, s.K, false, nullptr, 1, st,
-                    part, StatSink{}, wgs);
+                    part, StatSink{}, wgs, GradSink{}, wbf);
         else
           gemm2_run(mode, ax, GradX{}, Bt, s.bias ? bias : nullptr, C, s.M, s.N, s.K, false, mode == 2 ? m1 : nullptr,
-                    mode == 2 ? s.M : 1, st, part, sink, wgs);
+                    mode == 2 ? s.M : 1, st, part, sink, wgs, GradSink{}, wbf);
+      };
+      // C as floats (a bf16 forward stores bf16 elements)
+      const bool cbf = wbf && mode != 3;
+      auto fetch = [&](std::vector<float>& out) {
+        if (!cbf) {
+          hipMemcpy(out.data(), C, out.size() * 4, hipMemcpyDeviceToHost);
+          return;
+        }
+        std::vector<uint16_t> hb(out.size());
+        hipMemcpy(hb.data(), C, hb.size() * 2, hipMemcpyDeviceToHost);
+        for (size_t i = 0; i < hb.size(); ++i) {
+          const uint32_t u = (uint32_t)hb[i] << 16;
+          memcpy(&out[i], &u, 4);
+        }
       };
       auto timeit = [&]() {
         for (int i = 0; i < 3; ++i) go();
@@ -174,15 +210,15 @@ int main(int argc, char** argv) {
       go();
       hipStreamSynchronize(st);
       std::vector<float> base((size_t)s.M * s.N), hc(base.size());
-      hipMemcpy(base.data(), C, base.size() * 4, hipMemcpyDeviceToHost);
+      fetch(base);
       const double tb = timeit();
-      Gemm2Plan q = plan_gemm2(s.M, s.N, s.K, wgs);
+      Gemm2Plan q = plan_gemm2(s.M, s.N, s.K, wgs, wbf);
       printf("wsk M=%8d N=%5d K=%5d split  grid=%dx%dx%d  %8.1f us\n", s.M, s.N, s.K, q.gx, q.gy, q.splits, tb);
       for (auto& t : tiles) {
         gemm2_force_wsk(t[0], t[1]);
         go();
         hipStreamSynchronize(st);
-        hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost);
+        fetch(hc);
         double md = 0, mr = 0;
         for (size_t i = 0; i < hc.size(); ++i) {
           md = std::max(md, (double)std::fabs(hc[i] - base[i]));
@@ -193,7 +229,7 @@ int main(int argc, char** argv) {
                t[1], tw, tb / tw, md, mr);
       }
       gemm2_force_wsk(0, 0);
-      Gemm2Plan d = plan_gemm2(s.M, s.N, s.K, wgs);
+      Gemm2Plan d = plan_gemm2(s.M, s.N, s.K, wgs, wbf);
       printf("wsk M=%8d N=%5d K=%5d default wsk=%d\n", s.M, s.N, s.K, d.wsk);
     }
   }
