@@ -92,7 +92,8 @@ def cpu_baseline(size, batch, threads, budget_s=15.0):
 
 # kernels behind each launch-group kind of the library profiler (for the rocprof cross-check)
 KIND_KERNELS = {
-    "gemm": "k_gemm2<WM,TM,TN,MODE,SK,NS> (+ k_gemm<NT,WM,MODE,SK> for N<=16, k_gemm_splitk_reduce(_stats))",
+    "gemm": "k_gemm2 / k_gemm2r <WM,TM,TN,MODE,SK,NS,BF,ST>, k_gemm2k <TM,TN,MODE,SK,BF,ST> (deep K: K split "
+            "across a workgroup's waves) (+ k_gemm<NT,WM,MODE,SK> for N<=16, k_gemm_splitk_reduce(_stats))",
     "bn_stats": "k_bn_finalize<false,StatsEpi,NS> (statistics partials from the producer's epilogue)",
     "bn_bwd_reduce": "k_bn_finalize<true,BwdEpi2,NS> (BN-backward sums from the consumer's dgrad)",
     "dw_fwd": "k_dw_fwd<K,S,RPT,STATS,NS>",

@@ -258,7 +258,12 @@ void conv3_gemm(const float* x, float* col, const float* Bt, const float* bias, 
     return;
   }
   un_im2col(x, col, B, H, W, C, Ho, Wo, Kp, mode, st, pt, pl, s);
-  gemm(col, Bt, bias, out, (long)B * Ho * Wo, N, Kp, false, part, s);
+  // the implicit im2col's plan (no wave-split K), so both forms multiply in the same order
+  if (gemm_impl_for(N) == 2)
+    gemm2_run(0, InX{col, nullptr, nullptr, nullptr, 0}, GradX{}, Bt, bias, out, (int)((long)B * Ho * Wo), N, Kp, false,
+              nullptr, 1, s, part, StatSink{}, gemm2_target_wgs(), GradSink{}, false, false);
+  else
+    gemm(col, Bt, bias, out, (long)B * Ho * Wo, N, Kp, false, part, s);
 }
 
 }  // namespace

@@ -69,7 +69,8 @@ struct Gemm2Plan {
                    // counts the N tiles of one workgroup's sweep and gy the sweeps
   int wsk = 0;     // > 0: the wave-split-K kernel (k_gemm2k, kernels_gemm_wsk.hip) with tile tm x tn
 };
-Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false, bool allow_res = true);
+Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16 = false, bool allow_res = true,
+                     bool allow_wsk = true);
 void gemm2_force_cfg(int wm, int tm, int tn, int splits);  // tools/gemm_bench sweeps only (0 = off)
 void gemm2_force_wsk(int tm, int tn);                       // tools/gemm_bench sweeps only (0 = off, -1 = never)
 struct Gemm2Args;
@@ -82,7 +83,8 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
               float* partial, StatSink sink, GradSink gsk = GradSink{});
 int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, float* C, int M, int N,
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s,
-              float* partial, StatSink sink, int target_wgs, GradSink gsk = GradSink{}, bool bf16 = false);
+              float* partial, StatSink sink, int target_wgs, GradSink gsk = GradSink{}, bool bf16 = false,
+              bool allow_wsk = true);
 int gemm_splitk_stats_partials(int M, int N);
 // cbf: C holds bf16 activations (the partial slabs are fp32)
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,

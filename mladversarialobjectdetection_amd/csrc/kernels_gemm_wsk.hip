@@ -2,7 +2,7 @@
 // workgroup instead of across workgroups (fp32 matrix cores, v_mfma_f32_32x32x2_f32).
 //
 //   C[M,N] (+)= A'[M,K] * Bt[N,K]^T (+ bias)      A' as in k_gemm2 (raw, BN view, x SE rowscale,
-//                                                 gradient view)
+//                                                 gradient view, implicit im2col of a 3x3 conv)
 //
 // Why: the stage 5-7 convs (M = 4096-16384 rows, K = 320-1152) have fewer than 256 output tiles of
 // the k_gemm2 sizes, so k_gemm2 split K across workgroups: fp32 partial slabs in HBM, a second
@@ -43,6 +43,7 @@ struct G2K {
 template <class P, int MODE>
 struct G2KRegs {
   float4 a[P::NA];
+  bool gok[MODE == 4 ? P::NA : 1];
   float4 y[MODE == 3 ? P::NA : 1];
   float4 rs[MODE == 2 ? P::NA : 1];
   float4 b[P::NB];
@@ -59,16 +60,46 @@ __device__ __forceinline__ void g2k_load(G2KRegs<P, MODE>& r, const Gemm2Args& a
   const int kc = kk < a.K ? kk : a.K - 4;
   if (MODE == 1 || MODE == 2) r.ck = inx_chan4(a.A, kc);
   if (MODE == 3) r.gk = gx_chan4(a.G, kc);
+  if constexpr (MODE == 4) {
+    // implicit im2col (k_gemm2 MODE 4): row -> (image, oy, ox), quad kc -> (tap, channel), zero taps
+    // outside the input (the same gather as g2_load, so a column matrix in HBM gives the same values)
+    const G2Geo g = g2_geo((uint32_t)a.rpi);
+    const int tap = kc >> g.lC, c = kc & ((1 << g.lC) - 1);
+    const int ky = (tap * 11) >> 5, kx = tap - 3 * ky;  // tap / 3 for tap < 9
 #pragma unroll
-  for (int u = 0; u < P::NA; ++u) {
-    const int row = min(m0 + t / P::KQ + P::RPP * u, a.M - 1);
-    const long e = (long)row * a.K + kc;
-    if (MODE == 3) {
-      r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
-      r.y[u] = ald4<ST == 2>(a.G.y, e);
-    } else {
-      r.a[u] = ald4<ST == 1>(a.A.p, e);
-      if (MODE == 2) r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(row / a.rpi) * a.K + kc);
+    for (int u = 0; u < P::NA; ++u) {
+      const int row = min(m0 + t / P::KQ + P::RPP * u, a.M - 1);
+      const int ox = row & ((1 << g.lWo) - 1), oy = (row >> g.lWo) & ((1 << g.lHo) - 1);
+      const int b = row >> (g.lWo + g.lHo);
+      int iy, ix;
+      bool ok = kk < a.K && tap < 9;
+      if (g.mode == 0) {
+        iy = oy * g.s + ky - g.pt;
+        ix = ox * g.s + kx - g.pl;
+      } else {
+        const int dy = oy - ky, dx = ox - kx;
+        ok = ok && dy >= 0 && dx >= 0 && !(dy & 1) && !(dx & 1);
+        iy = dy >> 1;
+        ix = dx >> 1;
+      }
+      ok = ok && iy >= 0 && iy < (1 << g.lH) && ix >= 0 && ix < (1 << g.lW);
+      const long e = ok ? ((((long)b << g.lH) + iy) << g.lW | ix) << g.lC | c : 0;
+      r.a[u] = *reinterpret_cast<const float4*>(a.A.p + e);
+      r.gok[u] = ok;
+    }
+  }
+  if constexpr (MODE != 4) {
+#pragma unroll
+    for (int u = 0; u < P::NA; ++u) {
+      const int row = min(m0 + t / P::KQ + P::RPP * u, a.M - 1);
+      const long e = (long)row * a.K + kc;
+      if (MODE == 3) {
+        r.a[u] = *reinterpret_cast<const float4*>(a.G.da + e);
+        r.y[u] = ald4<ST == 2>(a.G.y, e);
+      } else {
+        r.a[u] = ald4<ST == 1>(a.A.p, e);
+        if (MODE == 2) r.rs[u] = *reinterpret_cast<const float4*>(a.rowscale + (long)(row / a.rpi) * a.K + kc);
+      }
     }
   }
 #pragma unroll
@@ -99,7 +130,9 @@ __device__ __forceinline__ void g2k_store_act(const G2KRegs<P, MODE>& r, const G
   for (int u = 0; u < P::NA; ++u) {
     const int rl = t / P::KQ + P::RPP * u;
     float4 v = r.a[u];
-    if (kok && m0 + rl < a.M) {
+    if (MODE == 4) {
+      if (!(r.gok[u] && m0 + rl < a.M)) v = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (kok && m0 + rl < a.M) {
       if (MODE == 1 || MODE == 2) v = inx_apply4(ax, r.ck, v);
       if (MODE == 2) {
         v.x *= r.rs[u].x; v.y *= r.rs[u].y; v.z *= r.rs[u].z; v.w *= r.rs[u].w;
@@ -367,8 +400,12 @@ static void g2k_go(int mode, int sk, dim3 g, hipStream_t s, const Gemm2Args& a, 
       if (sk == 2) g2k_st<TM, TN, 3, 2>(g, s, a, bf, st);
       else g2k_st<TM, TN, 3, 0>(g, s, a, bf, st);
       break;
+    case 4:  // the implicit im2col: fp32, no sinks (as k_gemm2)
+      if (sk || bf || st) throw std::logic_error("gemm2k: the implicit im2col runs in fp32 without sinks");
+      PHX_TLAUNCH((k_gemm2k<TM, TN, 4, 0, false, 0>), g, dim3(256), 0, s, a);
+      break;
     default:
-      throw std::logic_error("gemm2k: no implicit im2col");
+      throw std::logic_error("gemm2k: unknown mode");
   }
 }
 
