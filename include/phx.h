@@ -299,6 +299,19 @@ int phx_def_eval_workspace_bytes(phx_def* d, int B, size_t* bytes);
  * grad: num_params floats followed by the metric row [loss] (SUM-all-reducible). */
 int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,
                       const float* params, float* grad, int64_t step, int32_t global_image_offset, void* stream);
+/* Cross-step first-pass prefetch.  The first pass of a training step depends only on its images
+ * (the protege is frozen), so the host loop (defender_train.py's fit over the generator, which has
+ * the next batch ready) may name the next batch: the next phx_def_step_grad then also runs the
+ * victim's first pass of next_images — for step + 1 at global_image_offset — on the defender's own
+ * stream beside its U-Net work, into a second box buffer, and the phx_def_step_grad call for exactly
+ * those images, B, step and offset (without caller boxes) uses those boxes instead of running the
+ * first pass (attack_detection.py:174-178: the same boxes either way).  next_images must keep its
+ * contents until that call; NULL withdraws it.  A prefetch ties up the victim ctx until it
+ * finishes: the defender's own calls wait for it, other users of the victim ctx call phx_def_sync
+ * on their stream first. */
+int phx_def_set_next(phx_def* d, const float* next_images, int B, int32_t global_image_offset);
+/* makes `stream` wait for the first pass a phx_def_set_next prefetch has in flight */
+int phx_def_sync(phx_def* d, void* stream);
 /* PatchAttackDefender.call(images, training=False) as test_step runs it (attack_detection.py:168-198,
  * 320-326): first pass (or the caller's boxes), the Masker's evaluation branch with the attacker's
  * trained patch — eval_patch = [patch 640*640*3 | scale] (device; the PatchAttackDefender eval_patch

@@ -107,6 +107,8 @@ _SIGS = [
     ("phx_def_eval_workspace_bytes", c_int, [c_void_p, c_int, POINTER(c_size_t)]),
     ("phx_def_step_grad", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
+    ("phx_def_set_next", c_int, [c_void_p, c_void_p, c_int, c_int]),
+    ("phx_def_sync", c_int, [c_void_p, c_void_p]),
     ("phx_def_eval_step", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
       c_void_p, c_int64, c_int, c_void_p]),

@@ -82,6 +82,36 @@ struct phx_def {
   int out_conv = -1;
   long nparams = 0, nmoving = 0, nbt = 0;
   DBuf moving;  // [mean | var] per BN
+  // cross-step first-pass prefetch (phx_def_set_next): the next batch's first pass runs on `side`
+  // beside this step's U-Net work, into pboxes / pcount[slot]
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_done = nullptr;
+  struct Next {
+    const float* images = nullptr;
+    int B = 0, gimg0 = 0;
+  } next;
+  struct Pre {
+    const float* images = nullptr;
+    int B = 0, gimg0 = 0, slot = 0;
+    int64_t step = -1;
+    bool pending = false;
+  } pre;
+  float* pboxes[2] = {nullptr, nullptr};
+  int* pcount[2] = {nullptr, nullptr};
+  const float* last_boxes = nullptr;  // the boxes the last step placed its patches by (phx_def_debug)
+  const int* last_count = nullptr;
+  // `s` waits for the prefetch in flight (the victim ctx and its executor are in use until then)
+  void join(hipStream_t s) {
+    if (pre.pending) PHX_HIP(hipStreamWaitEvent(s, ev_done, 0));
+  }
+  ~phx_def() {
+    if (side) {
+      (void)hipStreamSynchronize(side);
+      (void)hipStreamDestroy(side);
+      (void)hipEventDestroy(ev_fork);
+      (void)hipEventDestroy(ev_done);
+    }
+  }
   // per batch-size workspace
   int wsB = 0;
   std::vector<DBuf> owned;
@@ -271,6 +301,7 @@ void conv3_gemm(const float* x, float* col, const float* Bt, const float* bias, 
 void phx_def::workspace(int B) {
   if (B == wsB) return;
   PHX_HIP(hipDeviceSynchronize());
+  pre = Pre{};  // (its buffers go with the old workspace)
   owned.clear();
   ws_bytes = 0;
   wsB = B;
@@ -367,6 +398,12 @@ void phx_def::workspace(int B) {
   mask = F(Mf * 3);
   boxes = F((size_t)B * PHX_MAX_OUT * 4);
   count = alloc<int>(B);
+  for (int k = 0; k < 2; ++k) {
+    pboxes[k] = F((size_t)B * PHX_MAX_OUT * 4);
+    pcount[k] = alloc<int>(B);
+  }
+  last_boxes = boxes;
+  last_count = count;
   info = alloc<int>((size_t)B * 3);
   eerr = alloc<int>(1);
   // the evaluation Masker's buffers are reserved by the first evaluation (eval_reserve): a run that
@@ -483,15 +520,27 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   workspace(B);
   const float* W = params;
   float* G = grad;
+  // a first pass prefetched by the previous step for exactly this batch (phx_def_set_next)
+  const bool use_pre = pre.pending && !boxes_in && pre.images == images && pre.B == B && pre.step == stp &&
+                       pre.gimg0 == gimg0;
+  join(s);
+  pre.pending = false;
   prep_weights(W, s);
   // ---- first pass + Masker ----
   const float* bx = boxes_in;
   const int* cn = count_in;
-  if (!bx) {
+  int used_slot = -1;
+  if (use_pre) {
+    used_slot = pre.slot;
+    bx = pboxes[used_slot];
+    cn = pcount[used_slot];
+  } else if (!bx) {
     def_first_pass(victim, images, B, stp, gimg0, boxes, count, s);
     bx = boxes;
     cn = count;
   }
+  last_boxes = bx == boxes_in ? boxes : bx;
+  last_count = cn == count_in ? count : cn;
   DScope gm(victim, "masker", 0.0, 4.0 * B * ((double)S * S * 3 * 3 + 2.0 * ed.P * ed.P * 3), s);
   def_perm_crops(images, info, crops, B, S, S, ed.P, seed, stp, gimg0, s);
   PlaceRule rule;
@@ -505,6 +554,20 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   launch_eot_composite(ed, images, place, rstore, patched, nullptr, s, mask);
   prof_end(gm.r);
   gm.r.p = nullptr;
+  // the next batch's first pass (the step after this one) on the side stream, beside the U-Net work
+  // below: it starts once this step's own first pass and Masker are done with the victim executor
+  // and the boxes, and writes the slot this step did not read
+  if (next.images) {
+    if (next.B == B) {
+      const int slot = used_slot == 0 ? 1 : 0;
+      PHX_HIP(hipEventRecord(ev_fork, s));
+      PHX_HIP(hipStreamWaitEvent(side, ev_fork, 0));
+      def_first_pass(victim, next.images, B, stp + 1, next.gimg0, pboxes[slot], pcount[slot], side);
+      PHX_HIP(hipEventRecord(ev_done, side));
+      pre = Pre{next.images, B, next.gimg0, slot, stp + 1, true};
+    }
+    next = Next{};
+  }
 
   unet_forward(B, W, true, stp, gimg0, G + nparams, s);
   const float* x = dt[3].a2;
@@ -647,6 +710,7 @@ void phx_def::eval(const float* images, int B, const float* boxes_in, const int*
   // placement side <= floor(longer side * scale) <= S for scale in [0, 1] (the attacker's clip)
   e2.rcap = (long)B * PHX_MAX_OUT * S * S * 3;
   eval_reserve(B);
+  join(s);  // (a prefetched first pass stays valid: this call only shares the victim executor)
   prep_weights(W, s);
   const float* bx = boxes_in;
   const int* cn = count_in;
@@ -778,6 +842,30 @@ int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes
   DEF_CATCH(d)
 }
 
+int phx_def_set_next(phx_def* d, const float* next_images, int B, int32_t global_image_offset) {
+  if (!d) return PHX_EINVAL;
+  if (next_images && (B <= 0 || B > d->max_batch)) return B <= 0 ? PHX_EINVAL : PHX_ECAP;
+  DEF_TRY
+  PHX_HIP(hipSetDevice(d->device));
+  if (next_images && !d->side) {
+    PHX_HIP(hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
+    PHX_HIP(hipEventCreateWithFlags(&d->ev_fork, hipEventDisableTiming));
+    PHX_HIP(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
+  }
+  d->next = next_images ? phx_def::Next{next_images, B, global_image_offset} : phx_def::Next{};
+  return PHX_OK;
+  DEF_CATCH(d)
+}
+
+int phx_def_sync(phx_def* d, void* stream) {
+  if (!d) return PHX_EINVAL;
+  DEF_TRY
+  PHX_HIP(hipSetDevice(d->device));
+  d->join((hipStream_t)stream);
+  return PHX_OK;
+  DEF_CATCH(d)
+}
+
 int phx_def_eval_step(phx_def* d, const float* images, int B, const float* boxes, const int32_t* count,
                       const float* params, const float* eval_patch, float* metrics, float* out_boxes,
                       float* out_scores, int32_t* out_count, int64_t step, int32_t global_image_offset, void* stream) {
@@ -802,8 +890,8 @@ int phx_def_debug(phx_def* d, int what, float* dst, size_t n, void* stream) {
     case PHX_DEF_PATCHED: src = d->patched; have = Mf * 3; break;
     case PHX_DEF_TARGETS: src = d->mask; have = Mf * 3; break;
     case PHX_DEF_UPDATES: src = d->upd; have = Mf * 3; break;
-    case PHX_DEF_BOXES: src = d->boxes; have = (size_t)d->wsB * PHX_MAX_OUT * 4; break;
-    case PHX_DEF_COUNTS: src = reinterpret_cast<const float*>(d->count); have = d->wsB; break;
+    case PHX_DEF_BOXES: src = d->last_boxes; have = (size_t)d->wsB * PHX_MAX_OUT * 4; break;
+    case PHX_DEF_COUNTS: src = reinterpret_cast<const float*>(d->last_count); have = d->wsB; break;
     default: throw std::invalid_argument("phx_def_debug: unknown tensor");
   }
   if (n < have) throw std::out_of_range("phx_def_debug: destination too small");

@@ -240,6 +240,11 @@ class PatchAttackDefender:
 
     __call__ = call
 
+    def sync(self):
+        """Makes the current stream wait for a prefetched first pass (train_step(next_inputs=...))
+        before other users of the protege's context run on it."""
+        self.handle.call("phx_def_sync", _stream())
+
     def global_offset(self, B):
         """Global index of this rank's first image (RNG keys: draws do not depend on the GPU count)."""
         return ddp.global_offset(B)
@@ -253,9 +258,16 @@ class PatchAttackDefender:
         if rc != 0:
             raise _lib.PhxError(f"phx_adam failed ({rc})")
 
-    def train_step(self, inputs, boxes=None):
+    def train_step(self, inputs, boxes=None, next_inputs=None):
         """attack_detection.py:327-336: grads = self(inputs); apply_gradients.  Returns the loss as a
-        device scalar (reading it synchronises)."""
+        device scalar (reading it synchronises).  next_inputs: the batch the next train_step will get
+        (defender_train.py's fit draws it from the generator): its first pass (a function of the
+        images alone: the protege is frozen) then runs beside this step's U-Net work
+        (phx_def_set_next), and that train_step uses its boxes.  The result is the same either way."""
+        if next_inputs is not None:
+            nx = self.protege_model._check_images(next_inputs)
+            self._next_keep = nx  # alive until the step that consumes it
+            self.handle.call("phx_def_set_next", nx.data_ptr(), nx.shape[0], self.global_offset(nx.shape[0]))
         self.call(inputs, boxes=boxes)
         ddp.allreduce_sum_(self._red)
         self.apply_gradients()

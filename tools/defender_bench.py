@@ -64,6 +64,9 @@ def main():
     ap.add_argument("--person-bias", type=float, default=4.6)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-prefetch", action="store_true",
+                    help="run each step's first pass in the step (default: the fit loop hands train_step the next "
+                         "batch, whose first pass then runs beside the current step's U-Net work)")
     a = ap.parse_args()
 
     from mladversarialobjectdetection_amd import distributed as ddp
@@ -80,15 +83,25 @@ def main():
                                 device=local, person_bias=a.person_bias)
     d = PatchAttackDefender(victim, protege_config_override={"nms_configs": {"iou_thresh": .5, "score_thresh": .5}},
                             seed=3, device=dev)
-    images = torch.as_tensor(synth_images(list(range(rank * B, (rank + 1) * B)), S), device=dev)
+    # two batches, alternating (the generator's next batch is the other one)
+    batches = [torch.as_tensor(synth_images(list(range((2 * rank + j) * B, (2 * rank + j + 1) * B)), S), device=dev)
+               for j in range(2)]
+    k = 0
+
+    def train_step():
+        nonlocal k
+        out = d.train_step(batches[k % 2], next_inputs=None if a.no_prefetch else batches[(k + 1) % 2])
+        k += 1
+        return out
+
     for _ in range(a.warmup):
-        d.train_step(images)
+        train_step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        out = d.train_step(images)
+        out = train_step()
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -101,7 +114,8 @@ def main():
         # one extra, untimed step with per-launch-group HIP events (the victim context's profiler
         # covers the first pass, the Masker and every U-Net launch group)
         victim.ctx.profile(True)
-        d.train_step(images)
+        train_step()
+        d.sync()
         rep = victim.ctx.profile_report()
         victim.ctx.profile(False)
         kind, r = max(rep.items(), key=lambda kv: kv[1]["ms"])
@@ -124,7 +138,9 @@ def main():
             "value": round(world * B * a.steps / el, 3), "unit": "images/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1e3 * el / a.steps, 3),
             "higher_is_better": True, "scaling": "weak", "dtype": "f32",
-            "data": f"synthetic (U(-1,1) images, synthetic efficientdet-d0 weights, person_bias {a.person_bias})",
+            "data": f"synthetic (two alternating U(-1,1) batches, synthetic efficientdet-d0 weights, person_bias "
+                    f"{a.person_bias}); first pass " + ("in the step" if a.no_prefetch else
+                                                        "of the next batch beside each step (phx_def_set_next)"),
             "config": {"workload": f"C5: defender {S}x{S}, {B} images/GPU", "global_batch": world * B,
                        "u_net_params": d.handle.num_params, "loss": float(out["loss"].item()),
                        "parallelism": f"dp{world}"},
