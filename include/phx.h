@@ -178,6 +178,19 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
                   const int32_t* count, int maxb, const float* params, int64_t step,
                   int global_image_offset, int add_tv, float* grad, float* metrics,
                   void* stream);
+/* Cross-step first-pass prefetch (first-pass placement, bn=local).  The clean first pass of a step
+ * depends on its images, the step (drop connect) and the image offset, not on the patch, so the
+ * training loop (attacker_train.py's fit, whose generator has the next batch ready) may name the
+ * next batch: the next phx_step_grad without caller boxes then also runs the first pass of
+ * next_images — for step + 1 at global_image_offset — on a stream of its own beside its second pass
+ * and backward, deferring that pass's BN moving-statistics updates; the phx_step_grad call for
+ * exactly those images, B, step and offset applies them (after the previous step's, as in the
+ * one-stream order) and places its patches by those detections (attacker.py:180-184), bit for bit
+ * the result of running the first pass itself.  next_images must keep its contents until then; NULL
+ * withdraws it.  phx_load_weights and phx_set_score_thresh drop a pending prefetch; phx_sync makes
+ * `stream` wait for one. */
+int phx_set_next(phx_ctx* ctx, const float* next_images, int B, int32_t global_image_offset);
+int phx_sync(phx_ctx* ctx, void* stream);
 
 /* PatchAttacker.call(images, training=False) as run by test_step (attacker.py:318-326): the
  * victim in inference mode (BN from the moving statistics, no drop connect, moving statistics

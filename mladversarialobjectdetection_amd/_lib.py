@@ -75,6 +75,8 @@ _SIGS = [
     ("phx_step_grad", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
       c_void_p, c_void_p, c_void_p]),
+    ("phx_set_next", c_int, [c_void_p, c_void_p, c_int, c_int]),
+    ("phx_sync", c_int, [c_void_p, c_void_p]),
     ("phx_eval_step", c_int,
      [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_int64, c_int, c_int,
       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -381,6 +381,10 @@ class PatchAttacker:
 
     __call__ = call
 
+    def sync(self):
+        """Makes the current stream wait for a prefetched first pass (train_step(next_inputs=...))."""
+        self.model.ctx.call("phx_sync", _stream())
+
     def apply_gradients(self):
         """optimizer.apply_gradients + variable constraints (attacker.py:315, :51-54)."""
         self.iterations += 1
@@ -434,9 +438,17 @@ class PatchAttacker:
         for old in [k for k in self._snapshots if k < ids[-1] - 1024]:
             del self._snapshots[old]
 
-    def train_step(self, inputs, boxes=None):
+    def train_step(self, inputs, boxes=None, next_inputs=None):
         """attacker.py:307-316: grads = self(inputs); apply_gradients; return metrics.  The metric
-        dict is evaluated lazily (like the tensors Keras returns): reading it synchronises."""
+        dict is evaluated lazily (like the tensors Keras returns): reading it synchronises.
+        next_inputs: the batch the next train_step will get (attacker_train.py's fit draws it from
+        the generator).  With first-pass placement its clean first pass — a function of the images,
+        not of the patch — then runs beside this step's second pass and backward (phx_set_next) and
+        the next train_step places its patches by it; the results are the same either way."""
+        if next_inputs is not None and boxes is None:
+            nx = self.model._check_images(next_inputs)
+            self._next_keep = nx  # alive until the step that consumes it
+            self.model.ctx.call("phx_set_next", nx.data_ptr(), nx.shape[0], self.global_offset(nx.shape[0]))
         self.call(inputs, boxes=boxes)
         sid = self._step_id
         self._step_id += 1

@@ -318,10 +318,37 @@ struct phx_ctx {
   // concurrent first pass (injected placement): its own stream and fork / join events
   hipStream_t s1 = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // cross-step first-pass prefetch (phx_set_next, first-pass placement): the next batch's first pass
+  // on s2 and the side executor (tag 1), beside the current step's second pass and backward
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_pfork = nullptr, ev_pdone = nullptr;
+  struct Next {
+    const float* images = nullptr;
+    int B = 0, gimg0 = 0;
+  } next;
+  struct Pre {
+    const float* images = nullptr;
+    int B = 0, gimg0 = 0;
+    int64_t step = -1;
+    bool pending = false;
+  } pre;
+  // `s` waits for a prefetch in flight (it holds the side executor and its deferred statistics)
+  void pre_join(hipStream_t s) {
+    if (pre.pending) PHX_HIP(hipStreamWaitEvent(s, ev_pdone, 0));
+  }
+  // new weights or thresholds: a prefetched first pass no longer matches what the step would compute
+  void pre_drop() {
+    if (pre.pending) PHX_HIP(hipStreamSynchronize(s2));
+    pre = Pre{};
+  }
   ~phx_ctx() {
+    if (s2) (void)hipStreamSynchronize(s2);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     if (s1) (void)hipStreamDestroy(s1);
+    if (ev_pfork) (void)hipEventDestroy(ev_pfork);
+    if (ev_pdone) (void)hipEventDestroy(ev_pdone);
+    if (s2) (void)hipStreamDestroy(s2);
   }
 };
 
@@ -2008,8 +2035,11 @@ int phx_set_allreduce(phx_ctx* ctx, phx_allreduce_fn fn, void* user) {
 int phx_set_score_thresh(phx_ctx* ctx, float t) {
   if (!ctx) return PHX_EINVAL;
   if (!(t >= 0.f && t <= 1.f)) return fail(ctx, PHX_EINVAL, "score_thresh outside [0, 1]");
+  PHX_TRY(ctx)
+  ctx->pre_drop();
   ctx->set_score_thresh(t);
   return PHX_OK;
+  PHX_CATCH(ctx)
 }
 
 int phx_model_info(const phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
@@ -2062,6 +2092,7 @@ int phx_load_weights(phx_ctx* ctx, const float* blob, size_t nfloats) {
   if (nfloats != ctx->wfloats) return fail(ctx, PHX_EINVAL, "weight blob size mismatch");
   PHX_TRY(ctx)
   PHX_HIP(hipSetDevice(ctx->device));
+  ctx->pre_drop();
   if (!ctx->d_w) ctx->d_w.reset(dalloc<float>(ctx->wfloats));
   PHX_HIP(hipMemcpy(ctx->d_w.get(), blob, nfloats * sizeof(float), hipMemcpyHostToDevice));
   ++ctx->w_ver;
@@ -2334,6 +2365,37 @@ static bool concurrent_first_pass() {
   return !(e && e[0] == '0');
 }
 
+// the cross-step first-pass prefetch runs where a second stream is allowed: bn=local (bn=sync issues
+// collectives that every rank must order alike; bn=frozen has no deferred statistics to carry), not
+// in a profiled step (one stream), not under the checksum / guard diagnostics, not with PHX_CONC=0
+static bool prefetch_ok(phx_ctx* ctx, const Exec& E) {
+  return ctx->s2 && concurrent_first_pass() && ctx->bn_mode == PHX_BN_LOCAL && !ctx->prof.on && !E.ck_on &&
+         !guard_bytes();
+}
+
+int phx_set_next(phx_ctx* ctx, const float* next_images, int B, int32_t global_image_offset) {
+  if (!ctx) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  if (next_images) check_ready(ctx, B);
+  PHX_HIP(hipSetDevice(ctx->device));
+  if (next_images && !ctx->s2) {
+    PHX_HIP(hipStreamCreateWithFlags(&ctx->s2, hipStreamNonBlocking));
+    PHX_HIP(hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming));
+    PHX_HIP(hipEventCreateWithFlags(&ctx->ev_pdone, hipEventDisableTiming));
+  }
+  ctx->next = next_images ? phx_ctx::Next{next_images, B, global_image_offset} : phx_ctx::Next{};
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
+int phx_sync(phx_ctx* ctx, void* stream) {
+  if (!ctx) return PHX_EINVAL;
+  PHX_TRY(ctx)
+  ctx->pre_join((hipStream_t)stream);
+  return PHX_OK;
+  PHX_CATCH(ctx)
+}
+
 int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
                   const int32_t* count, int maxb, const float* params, int64_t step, int gimg0,
                   int add_tv, float* grad, float* metrics, void* stream) {
@@ -2343,9 +2405,14 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   hipStream_t s = (hipStream_t)stream;
   Exec& E = ctx->exec_for(B);
   ctx->last = &E;
+  const bool inject = boxes != nullptr;
+  // a first pass the previous step prefetched for exactly this batch (phx_set_next)
+  const bool use_pre = !inject && ctx->pre.pending && ctx->pre.images == images && ctx->pre.B == B &&
+                       ctx->pre.step == step && ctx->pre.gimg0 == gimg0;
+  ctx->pre_join(s);
+  ctx->pre.pending = false;
   PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
   ck_begin(E, s);
-  const bool inject = boxes != nullptr;
   // Injected placement: the first pass only feeds the ASR denominator (and the moving statistics),
   // so it runs on a second stream beside the second pass and the backward, on its own executor
   // (its own activation arena).  Both passes defer their moving-statistics updates, applied in
@@ -2415,7 +2482,16 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
           }
       }
     }
-  } else {
+  }
+  Exec* Efp = &E;  // the executor whose first-pass detections place the patches
+  if (!fork && use_pre) {
+    // 1'. the prefetched first pass (side executor): its moving-statistics updates, deferred, go in
+    // now — after the previous step's second pass, before this step's — and its ASR denominator
+    Efp = &ctx->exec_for(B, 1);
+    ctx->last = &E;
+    launch_bn_moving_apply(E.mov_tab, E.n_mov, E.mov_cmax, ctx->w(), Efp->side, nullptr, s);
+    launch_count_ge(Efp->nms1_scores, Efp->nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
+  } else if (!fork) {
     // 1. first pass: clean forward, pre_nms, person/valid/threshold filter, soft-NMS
     run_forward(ctx, E, images, s, 0, step, gimg0);
     run_pre_nms(ctx, E, s, 2);
@@ -2427,9 +2503,48 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
     stage_boxes(E, boxes, count, B, maxb, s);  // injected placement boxes
   }
   // 2. EOT paste
-  eot_forward(ctx, E, images, B, inject ? E.inj_boxes : E.nms1_boxes,
-              inject ? E.inj_count : E.nms1_count, params, step, gimg0, s);
+  eot_forward(ctx, E, images, B, inject ? E.inj_boxes : Efp->nms1_boxes,
+              inject ? E.inj_count : Efp->nms1_count, params, step, gimg0, s);
   launch_eot_count(E.ed, E.place, metrics, s);
+  // the next batch's first pass (phx_set_next) on s2 beside this step's second pass and backward:
+  // it starts once this step's own first pass and paste are done with the side executor's
+  // detections, and defers its moving-statistics updates to the step that uses it
+  const phx_ctx::Next nx = ctx->next;
+  if (!inject) ctx->next = phx_ctx::Next{};
+  auto prefetch = [&]() {
+      Exec& E1 = ctx->exec_for(B, 1);
+      ctx->last = &E;
+      PHX_HIP(hipEventRecord(ctx->ev_pfork, s));
+      PHX_HIP(hipStreamWaitEvent(ctx->s2, ctx->ev_pfork, 0));
+      struct Defer {
+        Exec& e;
+        ~Defer() { e.defer_mov = false; }
+      } defer{E1};
+      E1.defer_mov = true;
+      run_forward(ctx, E1, nx.images, ctx->s2, 0, step + 1, nx.gimg0);
+      E1.defer_mov = false;
+      run_pre_nms(ctx, E1, ctx->s2, 2);
+      run_nms(ctx, E1, 2, E1.nms1_boxes, E1.nms1_scores, E1.nms1_count, ctx->s2);
+      PHX_HIP(hipEventRecord(ctx->ev_pdone, ctx->s2));
+      ctx->pre = phx_ctx::Pre{nx.images, B, nx.gimg0, step + 1, true};
+  };
+  if (!inject && nx.images && nx.B == B && prefetch_ok(ctx, E)) {
+    // forked, like the injected flow's concurrent pass, when the second pass reaches the backbone's
+    // stage 6, so its HBM-bound early layers run beside the second pass's deep layers and the
+    // backward rather than beside the second pass's own early layers (PHX_PF_FORK=0: right here)
+    const char* pe = std::getenv("PHX_PF_FORK");
+    if (pe && pe[0] == '0') {
+      prefetch();
+    } else {
+      ctx->fwd_hook = prefetch;
+      ctx->fwd_hook_at = E.prog.ops.size();
+      for (size_t i = 0; i < E.prog.ops.size(); ++i)
+        if (E.prog.tensors[E.prog.ops[i].out].h * 32 <= ctx->mc.image_size) {
+          ctx->fwd_hook_at = i;
+          break;
+        }
+    }
+  }
   ck_note(E, "eot patched", E.patched, (size_t)B * ctx->mc.image_size * ctx->mc.image_size * 12, s);
   // 3. second pass + loss
   run_forward(ctx, E, E.patched, s, 1, step, gimg0);

@@ -335,8 +335,10 @@ __global__ __launch_bounds__(256) void k_bn_moving_apply(const MovEntry* __restr
   const int c = blockIdx.y * 256 + threadIdx.x;
   if (c >= e.C) return;
   const long o = 2L * (e.off + c);
-  W[e.mm + c] = moving_update(moving_update(W[e.mm + c], s0[o]), s1[o]);
-  W[e.mv + c] = moving_update(moving_update(W[e.mv + c], s0[o + 1]), s1[o + 1]);
+  // s1 == nullptr: one deferred pass (a prefetched first pass, phx_set_next)
+  const float mm = moving_update(W[e.mm + c], s0[o]), mv = moving_update(W[e.mv + c], s0[o + 1]);
+  W[e.mm + c] = s1 ? moving_update(mm, s1[o]) : mm;
+  W[e.mv + c] = s1 ? moving_update(mv, s1[o + 1]) : mv;
 }
 
 void launch_bn_moving_apply(const MovEntry* tab, int n, int cmax, float* W, const double* side0,
