@@ -574,6 +574,7 @@ Exec& phx_ctx::exec_for(int B, int tag) {
       if (older(i, lru)) lru = i;
     PHX_HIP(hipDeviceSynchronize());
     if (last == execs[lru].get()) last = nullptr;
+    if (execs[lru]->tag == 1) pre = Pre{};  // a prefetched first pass lives in the side executor
     execs.erase(execs.begin() + (long)lru);
   }
   auto ex = std::make_unique<Exec>();
