@@ -164,8 +164,17 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16, bool allow_
   // (not for the implicit im2col, nor for the U-Net's explicit column matrices that must match it
   // bit for bit: there the inference-mode U-Net amplifies a changed summation order past
   // test_eval_step_matches_oracle's bound, for 0.03 ms of C5)
+  // PHX_GEMM_WSK_SMALL=1: also the few-tile shapes k_gemm2 runs unsplit on under 128 workgroups (the
+  // BiFPN's P5-P7 level convs, K 64: 6.1 -> 3.8 us at M 4096, tools/gemm_bench GEMM_WSK; C2 11.55 ->
+  // 11.47 ms).  Off by default: test_c1_512_batch2_matches_oracle's metric-row bound (sum of the
+  // per-image max scores, rtol 1e-5) fails with it by 6.2e-7 on 0.0463
+  static const bool wsk_small = [] {
+    const char* e = std::getenv("PHX_GEMM_WSK_SMALL");
+    return e && e[0] == '1';
+  }();
+  const bool few = wsk_small && p.splits == 1 && (long)p.mtiles * p.gy < 128;
   if (allow_res && allow_wsk && g_force_wsk[0] >= 0 &&
-      (wsk_forced || (wsk_on && p.splits > 1 && (!bf16 || (wsk_bf16 && !bf16_keep))))) {
+      (wsk_forced || (wsk_on && (p.splits > 1 || few) && (!bf16 || (wsk_bf16 && !bf16_keep))))) {
     p.wsk = wsk_forced ? g_force_wsk[0] * 10 + g_force_wsk[1] : wsk_pick(M, N);
     p.tm = p.wsk / 10;
     p.tn = p.wsk % 10;
@@ -284,7 +293,8 @@ int gemm2_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
 bool gemm_group_ok(const int* M, int n, int N, int K, bool bf16) {
   if (n < 1 || n > kMaxSeg || gemm_impl_for(N, bf16) != 2) return false;
   for (int i = 0; i < n; ++i) {
-    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16);
+    // (the members' own plans without the wave-split kernel: a grouped launch beats separate ones)
+    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16, true, false);
     if (p.splits != 1 || p.wsk) return false;
   }
   return true;
@@ -304,7 +314,7 @@ int gemm_group_run(int mode, const GemmSeg* segs, int n, const float* Bt, int N,
   int gx = 1, P = 1;
   Gemm2Plan p0{};
   for (int i = 0; i < n; ++i) {
-    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16);
+    const Gemm2Plan p = plan_gemm2(M[i], N, K, gemm2_target_wgs(), bf16, true, false);
     if (i == 0) p0 = p;
     gx = std::max(gx, p.gx);
   }

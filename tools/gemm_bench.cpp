@@ -44,7 +44,9 @@ int main(int argc, char** argv) {
       {65536, 512, 512, false, false}, {65536, 512, 512, false, true},  {16384, 1024, 1024, false, false},
       // D4 1024^2 x 4 deep-K shapes (indices 24-27)
       {4096, 272, 1632, false, true},  {16384, 160, 960, false, true},  {4096, 1632, 272, false, true},
-      {16384, 224, 224, false, true}};
+      {16384, 224, 224, false, true},
+      // BiFPN P5-P7 level convs (indices 28-29)
+      {1024, 64, 64, true, true},      {256, 64, 64, true, true}};
   // GEMM_ONLY=i,j,...: run only those shape indices
   if (const char* e = getenv("GEMM_ONLY")) {
     std::vector<S> keep;
