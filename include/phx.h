@@ -187,7 +187,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
  * exactly those images, B, step and offset applies them (after the previous step's, as in the
  * one-stream order) and places its patches by those detections (attacker.py:180-184), bit for bit
  * the result of running the first pass itself.  next_images must keep its contents until then; NULL
- * withdraws it.  phx_load_weights and phx_set_score_thresh drop a pending prefetch; phx_sync makes
+ * withdraws it, and the next phx_step_grad consumes it either way (one with caller boxes drops it).  phx_load_weights and phx_set_score_thresh drop a pending prefetch; phx_sync makes
  * `stream` wait for one. */
 int phx_set_next(phx_ctx* ctx, const float* next_images, int B, int32_t global_image_offset);
 int phx_sync(phx_ctx* ctx, void* stream);

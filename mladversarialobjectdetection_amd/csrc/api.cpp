@@ -2510,8 +2510,9 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
   // the next batch's first pass (phx_set_next) on s2 beside this step's second pass and backward:
   // it starts once this step's own first pass and paste are done with the side executor's
   // detections, and defers its moving-statistics updates to the step that uses it
+  // (consumed by this call either way: a step with caller boxes drops it)
   const phx_ctx::Next nx = ctx->next;
-  if (!inject) ctx->next = phx_ctx::Next{};
+  ctx->next = phx_ctx::Next{};
   auto prefetch = [&]() {
       Exec& E1 = ctx->exec_for(B, 1);
       ctx->last = &E;
