@@ -36,6 +36,9 @@ FLOP_PER_IMAGE = 3 * 2 * D0_MACS
 PEAK_FP32_TFLOPS = 157.3   # MI355X fp32 matrix / vector peak (MI355X_MICROARCH.md)
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA peak (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
+# environment knobs that skip kernels (timing diagnostics only; a build without PHX_DEBUG_KNOBS ignores
+# them): a line measured with one set would not be the reference's step
+WORK_SKIPPING_KNOBS = ("PHX_SKIP_TIMING", "PHX_SKIP_KINDS", "PHX_NO_DROP")
 
 
 def flop_per_image(model, size):
@@ -133,6 +136,17 @@ def kernel_roofline(kind, r, mfma_peak=PEAK_FP32_TFLOPS, pmc="pmc_traffic.json")
     return out
 
 
+def _lib_path():
+    from mladversarialobjectdetection_amd import _lib
+    return _lib.LIB_PATH
+
+
+def _lib_digest():
+    import hashlib
+    with open(_lib_path(), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -161,6 +175,13 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary line (the reference's own placement flow, measured after the headline)")
     args = ap.parse_args()
+
+    # the line certifies itself: every PHX_* knob of the run goes into it, and the diagnostics that
+    # skip work (wrong results; compiled out of the shipped library) refuse to run
+    phx_env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("PHX_")}
+    bad = [k for k in WORK_SKIPPING_KNOBS if k in phx_env]
+    if bad:
+        sys.exit(f"bench.py: {', '.join(bad)} set -- these skip work and give wrong results; no headline")
 
     from mladversarialobjectdetection_amd import distributed as ddp
     ddp.init_from_env()
@@ -286,7 +307,8 @@ def main():
         v2 = EfficientDetVictim(args.model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=0,
                                 device=local, person_bias=4.6, dtype=args.dtype)
         a2 = PatchAttacker(v2, seed=7, device=dev)
-        steps2 = max(1, args.steps // 4)
+        # at least 20 timed steps whatever --steps is (the driver's --steps 20 gave 5 before)
+        steps2 = max(20, args.steps // 4)
         # two batches, alternating; the fit loop hands each step the next one, whose first pass
         # then runs beside the step's second pass and backward (phx_set_next)
         batches = [images, torch.as_tensor(synth_images(list(range(B * (world + rank), B * (world + rank + 1))), S),
@@ -358,6 +380,8 @@ def main():
             "cpu_baseline": cpu,
             "allreduce": allreduce,
             "secondary": secondary,
+            "env": phx_env,
+            "library": {"so": os.path.relpath(_lib_path(), ROOT), "sha256_16": _lib_digest()},
         }
         print(json.dumps(line))
 

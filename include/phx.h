@@ -186,8 +186,11 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
  * and backward, deferring that pass's BN moving-statistics updates; the phx_step_grad call for
  * exactly those images, B, step and offset applies them (after the previous step's, as in the
  * one-stream order) and places its patches by those detections (attacker.py:180-184), bit for bit
- * the result of running the first pass itself.  next_images must keep its contents until then; NULL
- * withdraws it, and the next phx_step_grad consumes it either way (one with caller boxes drops it).  phx_load_weights and phx_set_score_thresh drop a pending prefetch; phx_sync makes
+ * the result of running the first pass itself.  next_images must keep its contents until then.
+ * NULL withdraws a named batch and also a first pass already prefetched for it (a caller that
+ * refilled that device buffer in place: the Python mirror does this when the tensor's version
+ * counter moved); the next phx_step_grad consumes a prefetch either way (one with caller boxes
+ * drops it).  phx_load_weights and phx_set_score_thresh drop a pending prefetch; phx_sync makes
  * `stream` wait for one. */
 int phx_set_next(phx_ctx* ctx, const float* next_images, int B, int32_t global_image_offset);
 int phx_sync(phx_ctx* ctx, void* stream);
@@ -319,7 +322,9 @@ int phx_def_step_grad(phx_def* d, const float* images, int B, const float* boxes
  * stream beside its U-Net work, into a second box buffer, and the phx_def_step_grad call for exactly
  * those images, B, step and offset (without caller boxes) uses those boxes instead of running the
  * first pass (attack_detection.py:174-178: the same boxes either way).  next_images must keep its
- * contents until that call; NULL withdraws it.  A prefetch ties up the victim ctx until it
+ * contents until that call; NULL withdraws it, and a prefetch already made (a refilled buffer).  A
+ * prefetch made at another victim generation (a weight load, a training pass or new score thresholds
+ * on the victim ctx since) is not used.  A prefetch ties up the victim ctx until it
  * finishes: the defender's own calls wait for it, other users of the victim ctx call phx_def_sync
  * on their stream first. */
 int phx_def_set_next(phx_def* d, const float* next_images, int B, int32_t global_image_offset);

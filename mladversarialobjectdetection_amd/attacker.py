@@ -209,6 +209,17 @@ class BrightnessMatcher:
     call = __call__
 
 
+def _withdraw_if_refilled(obj, withdraw):
+    """The first pass prefetched for the next step (phx_set_next / phx_def_set_next) read that batch's
+    buffer as it was then.  If the buffer has been written in place since — the tensor's version
+    counter (shared with every view of it) moved, as a pinned-ring loader refilling one device buffer
+    does — the prefetched detections are stale: withdraw them (set_next(NULL)), so the step runs its
+    own first pass (attacker.py:172-184 computes it from the images the step gets)."""
+    rec = getattr(obj, "_next_rec", None)
+    if rec is not None and rec[0]._version != rec[1]:
+        withdraw()
+
+
 def _pad_boxes(boxes, B, device):
     """list of [n_b,4] (or a padded [B,maxb,4] + count) -> ([B,maxb,4], count[B])"""
     if isinstance(boxes, (tuple, list)) and len(boxes) == 2 and torch.is_tensor(boxes[0]) and boxes[0].dim() == 3:
@@ -445,11 +456,18 @@ class PatchAttacker:
         the generator).  With first-pass placement its clean first pass — a function of the images,
         not of the patch — then runs beside this step's second pass and backward (phx_set_next) and
         the next train_step places its patches by it; the results are the same either way."""
+        # the batch the previous step prefetched, kept alive until this call (which joins its first
+        # pass on the current stream) has been issued
+        prev = getattr(self, "_next_keep", None)
+        _withdraw_if_refilled(self, lambda: self.model.ctx.call("phx_set_next", None, 0, 0))
+        self._next_keep = self._next_rec = None
         if next_inputs is not None and boxes is None:
             nx = self.model._check_images(next_inputs)
             self._next_keep = nx  # alive until the step that consumes it
+            self._next_rec = (nx, nx._version)
             self.model.ctx.call("phx_set_next", nx.data_ptr(), nx.shape[0], self.global_offset(nx.shape[0]))
         self.call(inputs, boxes=boxes)
+        del prev
         sid = self._step_id
         self._step_id += 1
         self.allreduce_gradients()

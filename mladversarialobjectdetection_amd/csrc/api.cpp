@@ -85,9 +85,6 @@ struct Exec {
   std::vector<char> fuse_folded;               // op id of the fuse -> 1
   // expand -> BN -> act -> depthwise fused (kernels_dw.hip): op id of the expand
   // conv -> 1; the expand output is never stored in a training pass (ops i, i+1, i+2)
-  std::vector<char> xdw;
-  double* xdw_part = nullptr;                  // BN0 statistics partials
-  float* xdw_ref = nullptr;                    // BN0 statistics shift (y0 of row 0)
   std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
   std::vector<int> bn_consumer;                // tensor id -> BN op index reading it (-1)
   std::vector<float*> slot_d, slot_e;          // BN backward: mean(dz), mean(dz*xhat)
@@ -112,18 +109,6 @@ struct Exec {
   size_t sp_region = 0, sc_region = 0;
   std::vector<int> stat_region;                // tensor id -> region of its producer's partials
   std::vector<int> gstat_region;               // BN op id -> region of its backward partials
-  // In-launch BN finalize (common.hpp FinDesc): fin_fwd / fin_bwd[i]: BN op i's batch statistics /
-  // backward sums are finalized by the last workgroup of their producer launch, no k_bn_finalize.
-  // Ticket r serves partial region r (a group's member r); descriptors [3 * op]: forward, forward
-  // with deferred moving statistics, backward — built for the weights buffer fin_w.
-  std::vector<char> fin_fwd, fin_bwd;
-  std::vector<int> fin_reg;
-  unsigned* fin_tick = nullptr;
-  FinDesc* fin_desc = nullptr;
-  const float* fin_w = nullptr;
-  const FinDesc* fin_of(int bn, bool bwd) const {
-    return fin_desc + 3 * (size_t)bn + (bwd ? 2 : defer_mov ? 1 : 0);
-  }
   LevelDesc* lev_dev = nullptr;
   std::vector<LevelDesc> lev;
   long* dxoff_dev = nullptr;
@@ -712,102 +697,6 @@ Exec& phx_ctx::exec_for(int B, int tag) {
       E.fuse_folded[i] = 1;
     }
   }
-  // expand -> depthwise fusion: fp32, batch statistics of the rank (bn=local), ungrouped, the expand
-  // output and BN0's output read only by the next op, BN1's statistics from the depthwise conv, and
-  // BN0's backward sums from its data gradient (PHX_XDW=1: on, default off — slower on C2, DESIGN
-  // §5; read per executor)
-  E.xdw.assign(P.ops.size(), 0);
-  {
-    const char* xe = std::getenv("PHX_XDW");
-    const bool on = xe && xe[0] == '1' && !E.abf && bn_mode == PHX_BN_LOCAL;
-    std::vector<int> nuse(P.tensors.size(), 0);
-    for (const Op& op : P.ops)
-      for (int j = 0; j < op.nin; ++j) ++nuse[op.in[j]];
-    size_t part_need = 1, ref_need = 1;
-    for (size_t i = 0; on && i + 3 < P.ops.size(); ++i) {
-      const Op& e = P.ops[i];
-      const Op& bn = P.ops[i + 1];
-      const Op& d = P.ops[i + 2];
-      if (e.t != OP_PW || bn.t != OP_BN || d.t != OP_DW || e.b >= 0 || e.nin != 1) continue;
-      if (bn.in[0] != e.out || d.in[0] != bn.out || nuse[e.out] != 1 || nuse[bn.out] != 1) continue;
-      if (E.grp_of[i] >= 0 || E.grp_of[i + 1] >= 0 || E.grp_of[i + 2] >= 0 || e.in[0] == P.input) continue;
-      const Tensor& tx = P.tensors[e.in[0]];
-      const Tensor& t0 = P.tensors[e.out];
-      if (!xdw_supported(tx.c, t0.c, d.k, d.stride, bn.act) || (d.k == 5 && d.stride == 1)) continue;
-      if (!E.fused_bn[i + 1] || !E.fused_bn[i + 3] || P.ops[i + 3].in[0] != d.out) continue;
-      if (d.bwd && (!bn.bwd || !E.gfused_bn[i + 1])) continue;
-      E.xdw[i] = 1;
-      part_need = std::max(part_need, xdw_stats_scratch_doubles((long)t0.rows(), t0.c));
-      ref_need = std::max(ref_need, (size_t)t0.c);
-      // x's BN takes its backward sums from the fused data gradient (one partial row per 8x8 tile)
-      if (e.bwd && i > 0 && E.gfused_bn[i - 1] && P.ops[i - 1].out == e.in[0]) {
-        E.gstat_P[i - 1] = xdw_dx_partials(tx.n, tx.h, tx.w);
-        sp_need = std::max(sp_need, (size_t)E.gstat_P[i - 1] * tx.c);
-      }
-    }
-    if (part_need > 1) {
-      E.xdw_part = E.alloc<double>(part_need);
-      E.xdw_ref = E.alloc<float>(ref_need);
-    }
-  }
-  // in-launch BN finalize where the producer runs a folding kernel (gemm2 / gemm2r without split-K,
-  // depthwise, elementwise gradient sums) and the partials are few enough for one workgroup to fold
-  // (C * P <= PHX_FIN_MAX; default 0 = every BN finalizes in its own launch: C2 measured the same
-  // either way and C4 0.06 ms slower folded); a group's BNs all
-  // or none (one grouped finalize launch)
-  E.fin_fwd.assign(P.ops.size(), 0);
-  E.fin_bwd.assign(P.ops.size(), 0);
-  E.fin_reg.assign(P.ops.size(), 0);
-  if (bn_mode == PHX_BN_LOCAL) {
-    const long fin_max = [] {  // (read per executor)
-      const char* e = std::getenv("PHX_FIN_MAX");
-      return e ? atol(e) : 0L;
-    }();
-    for (size_t i = 1; fin_max > 0 && i < P.ops.size(); ++i) {
-      const Op& bn = P.ops[i];
-      if (bn.t != OP_BN) continue;
-      const Op& pr = P.ops[i - 1];
-      const Tensor& tz = P.tensors[bn.in[0]];
-      const long C = tz.c;
-      if (E.grp_of[i] >= 0) {
-        const std::vector<int>& g = E.groups[E.grp_of[i]];
-        E.fin_reg[i] = (int)(std::find(g.begin(), g.end(), (int)i) - g.begin());
-      }
-      if (E.fused_bn[i] && pr.out == bn.in[0]) {
-        const Tensor& ti = P.tensors[pr.in[0]];
-        long np = -1;
-        if (pr.t == OP_PW && gemm_fold_ok((int)ti.rows(), tz.c, ti.c, bf16))
-          np = gemm_stat_partials((int)ti.rows(), tz.c, ti.c, bf16);
-        else if (pr.t == OP_DW && !(i >= 3 && E.xdw[i - 3]))
-          np = dw_stat_partials(ti.n, ti.h, ti.w, ti.c, tz.h, tz.w, pr.k, pr.stride, pr.pad_t, pr.pad_l);
-        if (np > 0 && C * np <= fin_max) E.fin_fwd[i] = 1;
-      }
-      if (E.gfused_bn[i] && i + 1 < P.ops.size()) {
-        const Op& L = P.ops[i + 1];
-        const Tensor& li = P.tensors[L.in[0]];
-        const Tensor& lo = P.tensors[L.out];
-        bool ok = L.t == OP_SE || L.t == OP_ADD || (L.t == OP_DW && !(i >= 1 && E.xdw[i - 1]));
-        if (L.t == OP_PW) ok = !E.xdw[i + 1] && gemm_fold_ok((int)li.rows(), li.c, lo.c, bf16);
-        if (ok && C * (long)E.gstat_P[i] <= fin_max) E.fin_bwd[i] = 1;
-      }
-    }
-    // a group's BNs: all or none
-    for (const std::vector<int>& g : E.groups) {
-      if (P.ops[g[0]].t != OP_BN) continue;
-      bool f = true, b = true;
-      for (int m : g) {
-        f = f && E.fin_fwd[m];
-        b = b && E.fin_bwd[m];
-      }
-      for (int m : g) {
-        E.fin_fwd[m] = f;
-        E.fin_bwd[m] = b;
-      }
-    }
-  }
-  E.fin_tick = E.alloc<unsigned>(kMaxSeg);
-  PHX_HIP(hipMemset(E.fin_tick, 0, kMaxSeg * sizeof(unsigned)));
-  E.fin_desc = E.alloc<FinDesc>(3 * P.ops.size());
   const size_t nreg = E.groups.empty() ? 1 : kMaxSeg;
   E.sp_region = sp_need;
   E.sc_region = sc_need;
@@ -960,6 +849,10 @@ GradX gview(phx_ctx* ctx, const Exec& E, int t, const float* input) {
   return GradX{E.gptr(t), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0};
 }
 
+// Work-skipping timing diagnostics (wrong results), compiled in only with -DPHX_DEBUG_KNOBS=1 (make
+// DEBUG_KNOBS=1): the shipped library ignores PHX_SKIP_TIMING / PHX_SKIP_KINDS / PHX_NO_DROP, so no
+// environment can make a measured step skip work (bench.py also refuses to run with them set).
+#if defined(PHX_DEBUG_KNOBS) && PHX_DEBUG_KNOBS
 // PHX_SKIP_TIMING=f,b,s (timing experiments only: wrong results): skip the forward BN finalizes (f),
 // the backward ones (b), the SE MLP launches (s) — what removing them would be worth at most
 bool skip_timing(char k) {
@@ -999,22 +892,10 @@ bool skip_kind(const std::string& kind, const std::string& name) {
     if (name.find(n) != std::string::npos) return true;
   return false;
 }
-
-// the fused expand -> depthwise ops starting at expand op i (E.xdw[i])
-XdwArgs xdw_args(phx_ctx* ctx, const Exec& E, int i, const float* input) {
-  const Program& P = E.prog;
-  const Op& e = P.ops[i];
-  const Op& bn = P.ops[i + 1];
-  XdwArgs a{};
-  a.x = view(ctx, E, e.in[0], input);
-  a.we = ctx->w() + e.w;
-  a.bn0 = InX{nullptr, E.slot_a[bn.slot], E.slot_c[bn.slot], ctx->w() + bn.beta, bn.act, 0};
-  a.rs0 = E.slot_b[bn.slot];
-  a.mdz0 = E.slot_d[bn.slot];
-  a.mdzx0 = E.slot_e[bn.slot];
-  a.ce = P.tensors[e.out].c;
-  return a;
-}
+#else
+bool skip_timing(char) { return false; }
+bool skip_kind(const std::string&, const std::string&) { return false; }
+#endif
 
 // ---- PHX_CKSUM diagnostics -----------------------------------------------------------------
 // Read per call, so one process can compare a one-stream step with concurrent ones op by op: the
@@ -1208,28 +1089,6 @@ bool frozen_reuse_off() {
   return e && e[0] == '0';
 }
 
-// the in-launch finalize descriptors of the executor's folded BNs (rebuilt when the weights buffer moves)
-void fin_prepare(phx_ctx* ctx, Exec& E) {
-  const float* W = ctx->w();
-  if (E.fin_w == W) return;
-  const Program& P = E.prog;
-  std::vector<FinDesc> h(3 * P.ops.size());
-  for (size_t i = 0; i < P.ops.size(); ++i) {
-    const Op& op = P.ops[i];
-    if (op.t != OP_BN || !(E.fin_fwd[i] || E.fin_bwd[i])) continue;
-    const long M = (long)P.tensors[op.in[0]].rows();
-    StatsEpi fe{nullptr, M, E.slot_a[op.slot], E.slot_b[op.slot], W + op.gamma, E.slot_c[op.slot],
-                const_cast<float*>(W) + op.mmean, const_cast<float*>(W) + op.mvar, kBnEps, 0, nullptr};
-    const BwdEpi2 be{M, E.slot_d[op.slot], E.slot_e[op.slot]};
-    unsigned* tk = E.fin_tick + E.fin_reg[i];
-    h[3 * i] = FinDesc{tk, fe, be};
-    h[3 * i + 2] = FinDesc{tk, fe, be};
-    fe.side = E.side + 2 * (size_t)E.side_off[op.slot];
-    h[3 * i + 1] = FinDesc{tk, fe, be};
-  }
-  PHX_HIP(hipMemcpy(E.fin_desc, h.data(), h.size() * sizeof(FinDesc), hipMemcpyHostToDevice));
-  E.fin_w = W;
-}
 
 // bn=sync: the BN sums of `segs` (fold -> the caller's all-reduce -> statistics from the global sums)
 // bn=sync: all-reduce the sums of `n` members already in E.sync_sums, then their statistics
@@ -1256,9 +1115,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
   float* W = ctx->w();
   const bool sink_on = !frozen && g[0] + 1 < (int)P.ops.size() && E.fused_bn[g[0] + 1];
   auto sink_of = [&](int r) {
-    const int bn = g[r] + 1;
-    return sink_on ? StatSink{E.spart + (size_t)r * E.sp_region, E.scnt + (size_t)r * E.sc_region, to0.c, 0,
-                              E.fin_fwd[bn] ? E.fin_of(bn, false) : nullptr}
+    return sink_on ? StatSink{E.spart + (size_t)r * E.sp_region, E.scnt + (size_t)r * E.sc_region, to0.c, 0}
                    : StatSink{};
   };
   double fl = 0, by = 0;
@@ -1329,8 +1186,7 @@ void run_group_fwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            nullptr, nullptr, E.side_for(op.slot)};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, false, s);
-      else if (E.fin_fwd[g[0]]) {  // finalized by the producer group's launch
-      } else if (!skip_timing('f')) launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
+      else if (!skip_timing('f')) launch_bn_finalize_group(segs, n, ti0.c, kBnEps, s);
       break;
     }
     default:
@@ -1351,8 +1207,7 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
     if (!gs_on) return GradSink{};
     const Op& bn = P.ops[g[r] - 1];
     return GradSink{E.spart + (size_t)r * E.sp_region, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input),
-                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0]),
-                    E.fin_bwd[g[r] - 1] ? E.fin_of(g[r] - 1, true) : nullptr};
+                    E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
   };
   double fl = 0, by = 0;
   for (int i : g) {
@@ -1420,8 +1275,7 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
                            nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
       }
       if (ctx->bn_mode == PHX_BN_SYNC) sync_finalize(ctx, E, segs, n, ti0.c, true, s);
-      else if (E.fin_bwd[g[0]]) {  // finalized by the dgrad group's launch
-      } else if (!skip_timing('b')) launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
+      else if (!skip_timing('b')) launch_bn_bwd_finalize_group(segs, n, ti0.c, s);
       break;
     }
     default:
@@ -1448,7 +1302,6 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
   const Program& P = E.prog;
   float* W = ctx->w();
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN || !train || force_frozen;
-  fin_prepare(ctx, E);
   // inference BN: the statistics from the moving averages are a function of the weights, so the
   // slots keep them from the last inference pass at the same weights version (the frozen protege of
   // the defender: 108 launches per step saved); a training pass overwrites the slots and may move
@@ -1475,7 +1328,6 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
       continue;
     }
     if (E.fuse_folded[i]) continue;  // computed by the depthwise conv that follows
-    if (E.xdw[i] && !frozen) continue;  // the expand: recomputed by the fused statistics and depthwise
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
@@ -1493,7 +1345,7 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     }
     // the BN right after this op takes its statistics from this launch (StatSink)
     const bool sink_on = !frozen && i + 1 < P.ops.size() && E.fused_bn[i + 1];
-    const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0, E.fin_fwd[i + 1] ? E.fin_of((int)i + 1, false) : nullptr}
+    const StatSink sink = sink_on ? StatSink{E.spart, E.scnt, to.c, 0}
                                   : StatSink{};
     if (op.t == OP_BN && E.fused_bn[i]) by = 8.0 * (double)E.stat_P[op.in[0]] * ti.c;
     if (skip_kind(std::string("f:") + kind, op.name)) continue;
@@ -1520,12 +1372,6 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         break;
       }
       case OP_DW:
-        if (i >= 2 && E.xdw[i - 2] && !frozen) {
-          const XdwArgs xa = xdw_args(ctx, E, (int)i - 2, input);
-          np = launch_dw_fwd_x(xa, P.tensors[P.ops[i - 2].in[0]].c, W + op.w, y, ti.n, ti.h, ti.w, to.h, to.w,
-                               op.k, op.stride, op.pad_t, op.pad_l, sink, s);
-          break;
-        }
         if (i > 0 && E.fuse_folded[i - 1]) {
           const Op& f = P.ops[i - 1];
           FuseView fv{};
@@ -1551,18 +1397,13 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
         } else if (frozen)
           launch_bn_frozen_stats(W + op.mmean, W + op.mvar, mean, rstd, W + op.gamma,
                                  E.slot_c[op.slot], ti.c, kBnEps, s);
-        else if (i >= 1 && E.xdw[i - 1]) {
-          const XdwArgs xa = xdw_args(ctx, E, (int)i - 1, input);
-          launch_xdw_stats(xa, P.tensors[P.ops[i - 1].in[0]].c, (long)ti.rows(), E.xdw_part, E.xdw_ref, mean, rstd,
-                           W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, kBnEps, s,
-                           E.side_for(op.slot));
-        } else if (E.fused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
+        else if (E.fused_bn[i] && ctx->bn_mode == PHX_BN_SYNC) {
           const BnFinSeg sg{E.spart + E.stat_region[op.in[0]] * E.sp_region,
                             E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]], (long)ti.rows(),
                             mean, rstd, W + op.gamma, E.slot_c[op.slot], W + op.mmean, W + op.mvar, nullptr, nullptr,
                             E.side_for(op.slot)};
           sync_finalize(ctx, E, &sg, 1, ti.c, false, s);
-        } else if (E.fused_bn[i] && (E.fin_fwd[i] || skip_timing('f'))) {  // (finalized by the producer)
+        } else if (E.fused_bn[i] && skip_timing('f')) {  // (timing diagnostics)
         } else if (E.fused_bn[i])
           launch_bn_finalize(E.spart + E.stat_region[op.in[0]] * E.sp_region,
                              E.scnt + E.stat_region[op.in[0]] * E.sc_region, E.stat_P[op.in[0]],
@@ -1589,10 +1430,14 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
                       E.red);
         break;
       case OP_ADD: {
+#if defined(PHX_DEBUG_KNOBS) && PHX_DEBUG_KNOBS
         static const bool no_drop = [] {  // PHX_NO_DROP=1: diagnostics only (not the reference's step)
           const char* e = std::getenv("PHX_NO_DROP");
           return e && e[0] == '1';
         }();
+#else
+        constexpr bool no_drop = false;
+#endif
         const DropView dv = (train && !no_drop) ? drop_view(E, (int)i) : DropView{};
         if (E.ck_on) {  // what the add is about to read (PHX_CKSUM)
           const std::string nm = "p" + std::to_string(pass) + " f " + std::to_string(i) + " add in ";
@@ -1642,7 +1487,6 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
   float* W = ctx->w();
   const bool frozen = ctx->bn_mode == PHX_BN_FROZEN;
   const int na = ctx->mc.num_anchors();
-  fin_prepare(ctx, E);
   // 1. sparse class-head gradient into the inputs of the class-predict pointwise convs
   int K = 0;
   long wpred = -1;
@@ -1707,8 +1551,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     if (i > 0 && E.gfused_bn[i - 1]) {
       const Op& bn = P.ops[i - 1];
       gsk = GradSink{E.spart, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input), E.slot_a[bn.slot],
-                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0]),
-                     E.fin_bwd[i - 1] ? E.fin_of(i - 1, true) : nullptr};
+                     E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
       gsk_in = op.in[0] == bn.out ? 0 : 1;
     }
     if (op.t == OP_BN && E.gfused_bn[i]) by = 8.0 * (double)E.gstat_P[i] * ti.c;
@@ -1732,24 +1575,11 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
         break;
       }
       case OP_PW:
-        if (E.xdw[i]) {  // the expand's data gradient from the depthwise output's, nothing stored between
-          const Op& d = P.ops[i + 2];
-          const Tensor& td = P.tensors[d.out];
-          np = launch_xdw_dx(xdw_args(ctx, E, i, input), ti.c, gview(ctx, E, d.out, input), W + d.w, dx, op.acc[0],
-                             ti.n, ti.h, ti.w, td.h, td.w, d.k, d.stride, d.pad_t, d.pad_l, gsk, s);
-          break;
-        }
         // dX[M,Cin] = dY[M,Cout] * W^T : Bt = W in HWIO layout [Cin][Cout]
         np = launch_gemm_dgrad(gview(ctx, E, op.out, input), W + op.w, dx, (int)ti.rows(), ti.c, to.c,
                                op.acc[0], s, E.gpart, gsk, E.bf16);
         break;
       case OP_DW:
-        if (i >= 2 && E.xdw[i - 2]) {  // BN0's backward sums only, y0 recomputed
-          np = launch_dw_bwd_x(xdw_args(ctx, E, i - 2, input), P.tensors[P.ops[i - 2].in[0]].c,
-                               gview(ctx, E, op.out, input), W + op.w, ti.n, ti.h, ti.w, to.h, to.w, op.k,
-                               op.stride, op.pad_t, op.pad_l, gsk, s);
-          break;
-        }
         np = launch_dw_bwd(gview(ctx, E, op.out, input), W + op.w, dx, ti.n, ti.h, ti.w, ti.c, to.h, to.w, op.k,
                            op.stride, op.pad_t, op.pad_l, op.acc[0], s, gsk);
         break;
@@ -1760,7 +1590,7 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
           const BnFinSeg sg{E.spart + E.gstat_region[i] * E.sp_region, nullptr, E.gstat_P[i], (long)ti.rows(),
                             nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, E.slot_d[op.slot], E.slot_e[op.slot]};
           sync_finalize(ctx, E, &sg, 1, ti.c, true, s);
-        } else if (!frozen && E.gfused_bn[i] && (E.fin_bwd[i] || skip_timing('b'))) {  // (finalized by the dgrad)
+        } else if (!frozen && E.gfused_bn[i] && skip_timing('b')) {  // (timing diagnostics)
         } else if (!frozen && E.gfused_bn[i])
           launch_bn_bwd_finalize(E.spart + E.gstat_region[i] * E.sp_region, E.gstat_P[i], (long)ti.rows(),
                                  ti.c, E.slot_d[op.slot],
@@ -1923,6 +1753,12 @@ int phx::ctx_image_size(const phx_ctx* ctx) { return ctx->mc.image_size; }
 bool phx::ctx_profiling(const phx_ctx* ctx) { return ctx->prof.on; }
 uint64_t phx::ctx_seed(const phx_ctx* ctx) { return ctx->seed; }
 int phx::ctx_device(const phx_ctx* ctx) { return ctx->device; }
+uint64_t phx::ctx_generation(const phx_ctx* ctx) {
+  uint32_t f, n;
+  std::memcpy(&f, &ctx->filter_thresh, 4);
+  std::memcpy(&n, &ctx->nms_thresh, 4);
+  return (ctx->w_ver * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)f << 32 | n);
+}
 
 void phx::def_first_pass(phx_ctx* ctx, const float* images, int B, int64_t step, int gimg0, float* boxes, int* count,
                     hipStream_t s, bool train, int pass, float score_thresh, float* scores) {
@@ -2385,6 +2221,9 @@ int phx_set_next(phx_ctx* ctx, const float* next_images, int B, int32_t global_i
     PHX_HIP(hipEventCreateWithFlags(&ctx->ev_pdone, hipEventDisableTiming));
   }
   ctx->next = next_images ? phx_ctx::Next{next_images, B, global_image_offset} : phx_ctx::Next{};
+  // NULL also withdraws a first pass already prefetched for the next step (the caller refilled that
+  // batch's buffer in place: the prefetch saw the old contents); the step then runs its own
+  if (!next_images) ctx->pre_drop();
   return PHX_OK;
   PHX_CATCH(ctx)
 }
@@ -2522,12 +2361,20 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
         Exec& e;
         ~Defer() { e.defer_mov = false; }
       } defer{E1};
-      E1.defer_mov = true;
-      run_forward(ctx, E1, nx.images, ctx->s2, 0, step + 1, nx.gimg0);
-      E1.defer_mov = false;
-      run_pre_nms(ctx, E1, ctx->s2, 2);
-      run_nms(ctx, E1, 2, E1.nms1_boxes, E1.nms1_scores, E1.nms1_count, ctx->s2);
-      PHX_HIP(hipEventRecord(ctx->ev_pdone, ctx->s2));
+      try {
+        E1.defer_mov = true;
+        run_forward(ctx, E1, nx.images, ctx->s2, 0, step + 1, nx.gimg0);
+        E1.defer_mov = false;
+        run_pre_nms(ctx, E1, ctx->s2, 2);
+        run_nms(ctx, E1, 2, E1.nms1_boxes, E1.nms1_scores, E1.nms1_count, ctx->s2);
+        PHX_HIP(hipEventRecord(ctx->ev_pdone, ctx->s2));
+      } catch (...) {
+        // a part-way enqueued prefetch: drain it (its side executor is shared with the injected flow's
+        // concurrent pass on s1) and leave nothing pending
+        (void)hipStreamSynchronize(ctx->s2);
+        ctx->pre = phx_ctx::Pre{};
+        throw;
+      }
       ctx->pre = phx_ctx::Pre{nx.images, B, nx.gimg0, step + 1, true};
   };
   if (!inject && nx.images && nx.B == B && prefetch_ok(ctx, E)) {
@@ -2737,10 +2584,6 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
                                   " elements)");
     if (which == 0 && op.t == OP_FUSE && E.fuse_folded[i])
       throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
-    for (size_t j = 0; j < E.prog.ops.size(); ++j)
-      if (E.xdw[j] && (E.prog.ops[j].out == t || (which == 1 && E.prog.ops[j + 1].out == op.out)))
-        throw std::invalid_argument("tap: this tensor is recomputed by the fused expand / depthwise kernels, "
-                                    "never stored (PHX_XDW=0 at victim creation keeps it)");
     const float* src = which == 0 ? E.tptr(t, nullptr) : E.gptr(op.out);
     if (!src) throw std::invalid_argument("tap: no gradient for this tensor");
     if (which == 0 && E.tbf(t)) launch_bf16_to_f32(src, out, (long)nfloats, (hipStream_t)stream);

@@ -306,39 +306,18 @@ __device__ __forceinline__ T pick_seg(const T (&arr)[NS], int i) {
   return v;
 }
 
-struct FinDesc;  // in-launch finalize (below)
-
 struct StatSink {
   float2* part;  // [C][P] (sum, M2); nullptr = no statistics wanted
   float* cnt;    // [P]
   int C;
   int P;         // partial rows (set by the producer's launcher)
-  const FinDesc* fd = nullptr;  // set: the producer's last-arriving workgroup finalizes (fin_arrive)
 };
-
-// In-launch finalize: partials are stored write-through (agent-scope relaxed atomic stores: they
-// reach the device-coherent level without a release fence, MI355X_MICROARCH.md inter-workgroup
-// visibility), so the last arriving workgroup can read them after one acquire.
-typedef __attribute__((address_space(1))) unsigned long long fin_gu64;
-typedef __attribute__((address_space(1))) unsigned fin_gu32;
-__device__ __forceinline__ void fin_store2(float2* p, float2 v) {
-  const unsigned long long u = (unsigned long long)__float_as_uint(v.y) << 32 | __float_as_uint(v.x);
-  __hip_atomic_store((fin_gu64*)p, u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void fin_store1(float* p, float v) {
-  __hip_atomic_store((fin_gu32*)p, __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ void sink_put(const StatSink& k, long p, int c, float n, float mean,
                                          float m2) {
-  float2* q = k.part + (long)c * k.P + p;
-  if (k.fd) fin_store2(q, make_float2(n * mean, m2));
-  else *q = make_float2(n * mean, m2);
+  k.part[(long)c * k.P + p] = make_float2(n * mean, m2);
 }
-__device__ __forceinline__ void sink_cnt(const StatSink& k, long p, float n) {
-  if (k.fd) fin_store1(k.cnt + p, n);
-  else k.cnt[p] = n;
-}
+__device__ __forceinline__ void sink_cnt(const StatSink& k, long p, float n) { k.cnt[p] = n; }
 
 // ------------------------------------------------------------------------------------------
 // GradSink: the reduction half of a training-mode BN backward, computed by the kernel that
@@ -357,7 +336,6 @@ struct GradSink {
   const float* be;
   int act;
   int ybf = 0;  // y holds bf16 elements
-  const FinDesc* fd = nullptr;  // set: in-launch finalize (fin_arrive)
 };
 
 struct GSChan4 {
@@ -391,9 +369,7 @@ __device__ __forceinline__ void gs_acc4(const GradSink& g, const GSChan4& k, flo
 }
 
 __device__ __forceinline__ void gsink_put(const GradSink& g, long p, int c, float s1, float s2) {
-  float2* q = g.part + (long)c * g.P + p;
-  if (g.fd) fin_store2(q, make_float2(s1, s2));
-  else *q = make_float2(s1, s2);
+  g.part[(long)c * g.P + p] = make_float2(s1, s2);
 }
 
 // (n, mean, M2) += (nb, mb, m2b)
@@ -409,7 +385,7 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
 }
 
 // ------------------------------------------------------------------------------------------
-// BN finalize epilogues (k_bn_finalize, k_colred_final, and the in-launch finalize below).
+// BN finalize epilogues (k_bn_finalize, k_colred_final).
 // ------------------------------------------------------------------------------------------
 // one moving-average step, m - (m - batch) * (1 - momentum) in fp64 rounded to float
 __device__ __forceinline__ float moving_update(float m, double batch) { return (float)(m - (m - batch) * 0.01); }
@@ -477,112 +453,6 @@ struct BwdEpi2 {
     mdzx[c] = (float)(s1 / (double)M);
   }
 };
-
-// ------------------------------------------------------------------------------------------
-// In-launch BN finalize (the k_bn_finalize launch folded into its producer).  Every producer
-// workgroup stores its partials write-through (sink_put / gsink_put with a FinDesc), drains them,
-// and adds the number of (channel, partial row) entries it stored to the BN's ticket; the workgroup
-// whose addition completes C * P acquires once, folds every channel's P partials in row order in
-// fp64 (fixed order: bit-reproducible run to run), runs the StatsEpi / BwdEpi2 epilogue and resets
-// the ticket for the next launch (stream order).  The descriptor lives in device memory (one per
-// BN and pass kind, built by the executor), so the producer's kernel arguments grow by a pointer.
-// ------------------------------------------------------------------------------------------
-struct FinDesc {
-  unsigned* tick;  // zero between launches
-  StatsEpi fe;     // forward (StatSink)
-  BwdEpi2 be;      // backward (GradSink)
-};
-
-// One channel's P partials folded by L lanes (a power of two <= 64: the group shares a wave): lane j
-// folds rows j, j + L, ... in row order in fp64, 16 loads in flight at a time, then an xor-shuffle
-// tree over the L lanes (commutative pairwise adds: every lane of the group ends with the same
-// sums, in a fixed order — bit-reproducible run to run).  Forward: partial = (sum, M2) of cnt[p]
-// rows, folded as S1 = sum x, S2 = sum x^2 = M2 + sum^2 / n; backward: plain sums.  All L lanes
-// must call it (c >= C: zeros).
-template <bool BWD>
-__device__ __forceinline__ void fin_fold(const float2* part, const float* cnt, int C, int P, int c, int j, int L,
-                                         double& s1, double& s2) {
-  s1 = 0.0;
-  s2 = 0.0;
-  if (c < C) {
-    const float2* pc = part + (long)c * P;
-    for (int p0 = j; p0 < P; p0 += 16 * L) {
-      float2 v[16];
-      float n[16];
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int p = min(p0 + k * L, P - 1);
-        v[k] = pc[p];
-        n[k] = BWD ? 1.f : cnt[p];
-      }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        if (p0 + k * L >= P) break;
-        if (BWD) {
-          s1 += (double)v[k].x;
-          s2 += (double)v[k].y;
-        } else if (n[k] > 0.f) {
-          s1 += (double)v[k].x;
-          s2 += (double)v[k].y + (double)v[k].x * (double)v[k].x / (double)n[k];
-        }
-      }
-    }
-  }
-  for (int o = 1; o < L; o <<= 1) {
-    s1 += __shfl_xor(s1, o);
-    s2 += __shfl_xor(s2, o);
-  }
-}
-
-// the in-launch fold, by the last arriver: L lanes per channel, as many channels at a time as fill
-// the workgroup
-template <bool BWD>
-__device__ void fin_run(const FinDesc* fd, const float2* part, const float* cnt, int C, int P) {
-  int L = 1;
-  while (L < 64 && C * L < 256 && L < P) L <<= 1;
-  for (int u0 = 0; u0 < C * L; u0 += 256) {
-    const int u = u0 + (int)threadIdx.x;
-    const int c = u / L, j = u % L;
-    double s1, s2;
-    fin_fold<BWD>(part, cnt, C, P, c, j, L, s1, s2);
-    if (c < C && j == 0) {
-      if (BWD) fd->be.fin(BwdEpi2::Pre{}, c, s1, s2);
-      else fd->fe.fin(fd->fe.pre(c), c, s1, s2);
-    }
-  }
-}
-
-// every thread of the workgroup, after its partial stores (uniform: contains barriers).  The
-// "last" flag goes through `lds`, a word of LDS this kernel no longer needs (no LDS object of its
-// own: a second __shared__ object can de-pipeline a GEMM's k-loop, cdna_hip_programming.md
-// projection-GEMM trap (a)).
-template <bool BWD>
-__device__ void fin_arrive(const FinDesc* fd, const float2* part, const float* cnt, int C, int P, unsigned entries,
-                           void* lds) {
-  volatile unsigned* fin_last = reinterpret_cast<volatile unsigned*>(lds);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through stores are done
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* tick = fd->tick;
-    const unsigned old = __hip_atomic_fetch_add((fin_gu32*)tick, entries, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = old + entries == (unsigned)C * (unsigned)P ? 1u : 0u;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *fin_last = last;
-  }
-  __syncthreads();
-  if (!*fin_last) return;
-  fin_run<BWD>(fd, part, cnt, C, P);
-  if (threadIdx.x == 0) __hip_atomic_store((fin_gu32*)fd->tick, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void sink_finish(const StatSink& k, unsigned entries, void* lds) {
-  if (k.fd) fin_arrive<false>(k.fd, k.part, k.cnt, k.C, k.P, entries, lds);
-}
-__device__ __forceinline__ void gsink_finish(const GradSink& g, unsigned entries, void* lds) {
-  if (g.fd) fin_arrive<true>(g.fd, g.part, nullptr, g.C, g.P, entries, lds);
-}
 
 // ------------------------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11), counter-based: identical draws for a given

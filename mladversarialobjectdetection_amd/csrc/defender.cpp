@@ -95,6 +95,7 @@ struct phx_def {
     int B = 0, gimg0 = 0, slot = 0;
     int64_t step = -1;
     bool pending = false;
+    uint64_t gen = 0;  // the victim's generation (ctx_generation) it was made at
   } pre;
   float* pboxes[2] = {nullptr, nullptr};
   int* pcount[2] = {nullptr, nullptr};
@@ -521,8 +522,10 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   const float* W = params;
   float* G = grad;
   // a first pass prefetched by the previous step for exactly this batch (phx_def_set_next)
+  // (and the victim unchanged since: a weight load, a training pass or new score thresholds on the
+  // protege's context make its detections stale)
   const bool use_pre = pre.pending && !boxes_in && pre.images == images && pre.B == B && pre.step == stp &&
-                       pre.gimg0 == gimg0;
+                       pre.gimg0 == gimg0 && pre.gen == ctx_generation(victim);
   join(s);
   pre.pending = false;
   prep_weights(W, s);
@@ -557,14 +560,16 @@ void phx_def::step(const float* images, int B, const float* boxes_in, const int*
   // the next batch's first pass (the step after this one) on the side stream, beside the U-Net work
   // below: it starts once this step's own first pass and Masker are done with the victim executor
   // and the boxes, and writes the slot this step did not read
+  // (not while the victim is profiled: a profiled step runs its launch groups one at a time, as the
+  // attacker's prefetch_ok keeps a profiled step on one stream)
   if (next.images) {
-    if (next.B == B) {
+    if (next.B == B && !ctx_profiling(victim)) {
       const int slot = used_slot == 0 ? 1 : 0;
       PHX_HIP(hipEventRecord(ev_fork, s));
       PHX_HIP(hipStreamWaitEvent(side, ev_fork, 0));
       def_first_pass(victim, next.images, B, stp + 1, next.gimg0, pboxes[slot], pcount[slot], side);
       PHX_HIP(hipEventRecord(ev_done, side));
-      pre = Pre{next.images, B, next.gimg0, slot, stp + 1, true};
+      pre = Pre{next.images, B, next.gimg0, slot, stp + 1, true, ctx_generation(victim)};
     }
     next = Next{};
   }
@@ -853,6 +858,11 @@ int phx_def_set_next(phx_def* d, const float* next_images, int B, int32_t global
     PHX_HIP(hipEventCreateWithFlags(&d->ev_done, hipEventDisableTiming));
   }
   d->next = next_images ? phx_def::Next{next_images, B, global_image_offset} : phx_def::Next{};
+  // NULL also withdraws a prefetched first pass (the caller refilled that batch's buffer in place)
+  if (!next_images && d->pre.pending) {
+    PHX_HIP(hipStreamSynchronize(d->side));
+    d->pre = phx_def::Pre{};
+  }
   return PHX_OK;
   DEF_CATCH(d)
 }

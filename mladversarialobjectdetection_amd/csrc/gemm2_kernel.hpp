@@ -575,10 +575,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       if constexpr (STATS)
         if (blockIdx.y == 0 && wn == 0 && lane == 0) sink_cnt(a.sink, blockIdx.x, ntot);
     }
-    // in-launch finalize (FinDesc): this workgroup stored partial row blockIdx.x of its columns
-    const unsigned ent = (unsigned)max(0, min(BN, a.N - n0));
-    if constexpr (STATS) sink_finish(a.sink, ent, sm);
-    else gsink_finish(a.gsk, ent, sm);
   }
 }
 
@@ -931,14 +927,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm2r(Gemm2Group<NS> grp) {
     return true;
   };
   while (step()) {
-  }
-  if constexpr (SK != 0) {
-    // in-launch finalize (FinDesc): WM partial rows per M tile of this workgroup, its N-tile run's columns
-    const int nmt = (a.mtiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-    const unsigned ent = (unsigned)(nmt * WM * (min(a.N, nte * BN) - nt0 * BN));
-    __syncthreads();  // (the last step's LDS reads are done before the scratch is reused)
-    if constexpr (SK == 1) sink_finish(a.sink, ent, g2r_sm);
-    else gsink_finish(a.gsk, ent, g2r_sm);
   }
 }
 

@@ -141,41 +141,6 @@ struct DwSeg {
 };
 void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
                          hipStream_t s, int* nps);
-// ---- expand -> BN -> activation -> depthwise, fused (kernels_dw.hip) ---------------------------
-// The expand conv of an MBConv block with a narrow input (CIN 16 / 24 / 32 channels, CE <= 192
-// expanded) is never stored: F1 launch_xdw_stats gives BN0's statistics, F2 launch_dw_fwd_x the
-// depthwise forward from x, B1 launch_dw_bwd_x BN0's backward sums, B2 launch_xdw_dx the expand's
-// data gradient; y0 = view(x) * We is recomputed by each with one FMA order.
-struct XdwArgs {
-  InX x;             // block input through its BN view; p = raw [B,H,W,CIN] fp32
-  const float* we;   // expand kernel [CIN][CE] (HWIO)
-  InX bn0;           // BN0 as a view (p unused): mean, gamma*rstd, beta, act
-  const float* rs0;  // BN0 rstd, mean(dz), mean(dz*xhat) (B2)
-  const float* mdz0;
-  const float* mdzx0;
-  int ce;
-};
-bool xdw_supported(int cin, int ce, int k, int s, int act0);
-size_t xdw_stats_scratch_doubles(long M, int ce);
-// BN0 statistics (as launch_bn_stats: mean, rstd, sc, moving statistics or side); ref: ce floats
-void launch_xdw_stats(const XdwArgs& a, int cin, long M, double* scratch, float* ref, float* mean, float* rstd,
-                      const float* gamma, float* sc, float* mmean, float* mvar, float eps, hipStream_t s,
-                      double* side = nullptr);
-// returns the StatSink partial rows (dw_stat_partials of the same depthwise conv)
-int launch_dw_fwd_x(const XdwArgs& a, int cin, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                    int k, int stride, int pt, int pl, StatSink sink, hipStream_t s);
-// gv: BN1's gradient view of the depthwise output; gs0: BN0's GradSink (y unused); returns its rows
-// (dw_bwd_partials of the same conv)
-int launch_dw_bwd_x(const XdwArgs& a, int cin, GradX gv, const float* w, int B, int H, int W, int Ho, int Wo,
-                    int k, int stride, int pt, int pl, GradSink gs0, hipStream_t s);
-int xdw_dx_partials(int B, int H, int W);
-// dx [B,H,W,CIN] (+)= the expand's data gradient; gsx: the BN-backward sums of x's BN (or off)
-int launch_xdw_dx(const XdwArgs& a, int cin, GradX gv, const float* w, float* dx, bool acc, int B, int H, int W,
-                  int Ho, int Wo, int k, int stride, int pt, int pl, GradSink gsx, hipStream_t s);
-// k_colred_final with StatsEpi over chunk partials [chunks][C][2] (sum (y - ref), sum (y - ref)^2)
-void launch_bn_stats_final(const double* part, int chunks, long M, int C, const float* ref, float* mean, float* rstd,
-                           const float* gamma, float* sc, float* mmean, float* mvar, float eps, double* side,
-                           hipStream_t s);
 // depthwise 3x3 s1 whose input is a BiFPN fuse computed on load (FuseView); no statistics
 void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, int H, int W, int C, int Ho,
                          int Wo, int k, int stride, int pt, int pl, hipStream_t s);

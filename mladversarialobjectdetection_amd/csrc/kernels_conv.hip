@@ -360,7 +360,6 @@ void launch_stem_bwd_gx(GradX g, const float* w, const int16_t* owner, float* dx
 int launch_stem_fwd(const float* x, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
                     int Co, int pt, int pl, hipStream_t s, StatSink sink, bool ybf) {
   if (pt != 0 || pl != 0 || (H & 1) || (W & 1)) throw std::invalid_argument("stem: odd image side");
-  if (sink.fd) throw std::logic_error("stem: no in-launch finalize");
   stem_dispatch<StemFwd>(Co, x, w, y, B, H, W, Ho, Wo, sink, ybf, s);
   PHX_LAUNCH_CHECK();
   return cdiv((long)B * Ho * Wo, 256);
@@ -921,7 +920,6 @@ int gemm_stat_partials(int M, int N, int K, bool bf16) {
 // statistics of the result come out of the same pass.  Returns the StatSink partial rows.
 int gemm_splitk_finish(const float* partial, int splits, int M, int N, const float* bias, float* C,
                        bool acc, StatSink sink, hipStream_t s, bool cbf) {
-  if (sink.fd) throw std::logic_error("gemm: no in-launch finalize after a split-K reduce");
   if (sink.part) {
     const int rb = splitk_stats_rb(M, N);
     sink.P = cdiv(M, rb);
@@ -949,7 +947,6 @@ int gemm1_run(int mode, InX A, GradX G, const float* Bt, const float* bias, floa
               int K, bool acc, const float* rowscale, int rows_per_img, hipStream_t s, float* partial,
               StatSink sink, GradSink gsk) {
   if (K % 4 != 0) throw std::runtime_error("gemm: K must be a multiple of 4");
-  if (sink.fd || gsk.fd) throw std::logic_error("gemm: the in-launch finalize runs in the gemm2 kernels only");
   GemmPlan p = plan_gemm(M, N, K);
   float* part = p.splits > 1 ? partial : nullptr;
   if (p.splits > 1 && !partial) throw std::runtime_error("gemm: split-K needs a partial buffer");

@@ -405,7 +405,6 @@ __global__ __launch_bounds__(256) void k_dw_fwd(DwFwdGroup<NS, XV> grp) {
   }
   if constexpr (STATS) {
     dw_stats<RPT>(acc, vmask, g.lcg, c, (long)b * g.ntiles + tl, sink);
-    sink_finish(sink, 4u << g.lcg, tile);
   }
 }
 
@@ -547,515 +546,6 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
   }
   if constexpr (GS) {
     dw_gsums(s1, s2, g.lcg, c, (long)b * g.ntiles + tl, gsk);
-    gsink_finish(gsk, 4u << g.lcg, tile);
-  }
-}
-
-// ---- expand -> BN -> activation -> depthwise, fused ------------------------------------------
-// The first MBConv blocks expand a narrow input (CIN = 16..32 channels) six-fold at the largest
-// spatial sizes: D0's block 1 writes and re-reads a [16,256,256,96] fp32 tensor (402 MB) four times
-// a step.  Fused, the expand output y0 = view(x) * We is never stored:
-//   F1 k_xdw_stats   BN0's batch statistics, y0 recomputed row by row (column-reduction partials)
-//   F2 k_dw_fwd_x    the depthwise forward, staging act(BN0(y0)) computed from a staged x window
-//   B1 k_dw_bwd_x    the depthwise data gradient's BN0-backward sums, y0 recomputed, nothing stored
-//   B2 k_xdw_dx      per input pixel: the depthwise transpose over all CE channels, BN0 backward and
-//                    the expand's data gradient dx = dy0 * We^T (+ the BN-backward sums of x's BN)
-// Every y0 is the same FMA chain (xdw_y0, k ascending), so the statistics, the forward and both
-// backward passes see bit-identical values.
-template <int CIN, class WF>
-__device__ __forceinline__ float4 xdw_y0(const float* xr, WF wk) {
-  float4 e = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int k = 0; k < CIN; ++k) {
-    const float4 w = wk(k);
-    e.x = fmaf(xr[k], w.x, e.x);
-    e.y = fmaf(xr[k], w.y, e.y);
-    e.z = fmaf(xr[k], w.z, e.z);
-    e.w = fmaf(xr[k], w.w, e.w);
-  }
-  return e;
-}
-
-// x's view of 4 input channels (the block input is a BN output: its BN and activation on load)
-__device__ __forceinline__ float4 xdw_xview(const InX& x, int k, float4 raw) {
-  return x.mu ? inx_apply4(x, inx_chan4(x, k), raw) : raw;
-}
-
-// F1: per chunk of rows, the shifted sums (sum (y0 - ref), sum (y0 - ref)^2) of every channel,
-// fp32 runs folded into fp64 partials [chunk][CE][2] (the k_colred_part layout, finished by
-// k_colred_final with StatsEpi; ref = y0 of row 0, written by chunk 0 for the epilogue)
-template <int CIN>
-__global__ __launch_bounds__(256) void k_xdw_stats(XdwArgs a, long M, long rpc, double* __restrict__ part,
-                                                   float* __restrict__ ref_out) {
-  constexpr int XQ = CIN / 4;
-  constexpr int RB = 64;  // rows staged per round
-  __shared__ float4 wes[CIN * 48];  // We [CIN][CE/4], CE <= 192
-  __shared__ float xs[RB * CIN];
-  __shared__ float4 refs[48];
-  __shared__ double sh[8][256];
-  const int CE = a.ce, tpr = CE >> 2, rpi = 256 / tpr;
-  const int t = threadIdx.x, rr = t / tpr, cc = t % tpr;
-  const bool active = rr < rpi;
-  for (int e = t; e < CIN * tpr; e += 256) wes[e] = reinterpret_cast<const float4*>(a.we)[e];
-  if (t < tpr) {  // ref = y0 of row 0
-    float xr[CIN];
-#pragma unroll
-    for (int q = 0; q < XQ; ++q) {
-      const float4 v = xdw_xview(a.x, 4 * q, reinterpret_cast<const float4*>(a.x.p)[q]);
-      xr[4 * q] = v.x; xr[4 * q + 1] = v.y; xr[4 * q + 2] = v.z; xr[4 * q + 3] = v.w;
-    }
-    const float4 r = xdw_y0<CIN>(xr, [&](int k) { return reinterpret_cast<const float4*>(a.we)[k * tpr + t]; });
-    refs[t] = r;
-    if (blockIdx.x == 0) reinterpret_cast<float4*>(ref_out)[t] = r;
-  }
-  __syncthreads();
-  const float4 ref = refs[active ? cc : 0];
-  const long m0 = (long)blockIdx.x * rpc, m1 = min(M, m0 + rpc);
-  double d0[4] = {0, 0, 0, 0}, d1[4] = {0, 0, 0, 0};
-  // register prefetch of the next round's x quads (RB * XQ of them over 256 lanes)
-  constexpr int NL = (RB * XQ + 255) / 256;
-  float4 pre[NL];
-  auto load_round = [&](long r0) {
-#pragma unroll
-    for (int u = 0; u < NL; ++u) {
-      const int e = t + 256 * u;
-      const long m = min(r0 + e / XQ, M - 1);
-      pre[u] = reinterpret_cast<const float4*>(a.x.p)[m * XQ + e % XQ];
-    }
-  };
-  load_round(m0);
-  for (long r0 = m0; r0 < m1; r0 += RB) {
-#pragma unroll
-    for (int u = 0; u < NL; ++u) {
-      const int e = t + 256 * u;
-      if (e < RB * XQ) {
-        const float4 v = xdw_xview(a.x, 4 * (e % XQ), pre[u]);
-        *reinterpret_cast<float4*>(xs + e * 4) = v;
-      }
-    }
-    __syncthreads();
-    if (r0 + RB < m1) load_round(r0 + RB);
-    if (active) {
-      float a0[4] = {0.f, 0.f, 0.f, 0.f}, a1[4] = {0.f, 0.f, 0.f, 0.f};
-      const int nr = (int)min((long)RB, m1 - r0);
-      for (int r = rr; r < nr; r += rpi) {
-        const float4 y = xdw_y0<CIN>(xs + r * CIN, [&](int k) { return wes[k * tpr + cc]; });
-        const float dd[4] = {y.x - ref.x, y.y - ref.y, y.z - ref.z, y.w - ref.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a0[j] += dd[j];
-          a1[j] = fmaf(dd[j], dd[j], a1[j]);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        d0[j] += a0[j];
-        d1[j] += a1[j];
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    sh[j][t] = d0[j];
-    sh[4 + j][t] = d1[j];
-  }
-  __syncthreads();
-  if (active && rr == 0) {
-    for (int r = 1; r < rpi; ++r) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        d0[j] += sh[j][r * tpr + cc];
-        d1[j] += sh[4 + j][r * tpr + cc];
-      }
-    }
-    double* out = part + ((long)blockIdx.x * CE + cc * 4) * 2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      out[j * 2 + 0] = d0[j];
-      out[j * 2 + 1] = d1[j];
-    }
-  }
-}
-
-// F2: k_dw_fwd with the staged window computed from x: the x window (CIN channels, view applied)
-// and the group's slice of We go to LDS, then every (pixel, channel quad) of the window is
-// act0(BN0(y0)), zero outside the image (TF SAME pads the depthwise input, not x)
-template <int K, int S, int RPT, int CIN, int ACT0>
-__global__ __launch_bounds__(256) void k_dw_fwd_x(XdwArgs a, const float* __restrict__ w, float* __restrict__ y,
-                                                  DwGeom g, StatSink sink) {
-  extern __shared__ float4 tile[];
-  constexpr int XQ = CIN / 4;
-  const int b = blockIdx.z;
-  int tl, cgi;
-  if (!dw_block_map(blockIdx.x, g.per, g.ncg, g.ntiles * g.ncg, &tl, &cgi)) return;
-  const int CG = 1 << g.lcg;
-  const int ty = tl / g.tiles_x, tx = tl - ty * g.tiles_x;
-  const int oy0 = ty * g.oth, ox0 = tx * g.otw;
-  const int cg = threadIdx.x & (CG - 1), q = threadIdx.x >> g.lcg;
-  const int col = q % g.otw, rg = q / g.otw;
-  const int c = (cgi * CG + cg) * 4;
-  const int npx = g.rin * g.cin;
-  float4* wt = tile + npx * CG;
-  float4* wes = wt + K * K * CG;
-  float* xs = reinterpret_cast<float*>(wes + CIN * CG);
-  Taps<K> wr;
-  wr.stage(wt, w, g.C, cgi, g.lcg);
-  for (int e = threadIdx.x; e < CIN * CG; e += 256)
-    wes[e] = *reinterpret_cast<const float4*>(a.we + (long)(e >> g.lcg) * g.C + ((cgi << g.lcg) + (e & (CG - 1))) * 4);
-  const int r0 = oy0 * S - g.pt, c0 = ox0 * S - g.pl;
-  for (int e0 = threadIdx.x; e0 < npx * XQ; e0 += 1024) {
-    float4 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = min(e0 + 256 * u, npx * XQ - 1);
-      const int p = e / XQ, prow = p / g.cin, pcol = p - prow * g.cin;
-      const int iy = min(max(r0 + prow, 0), g.H - 1), ix = min(max(c0 + pcol, 0), g.W - 1);
-      v[u] = reinterpret_cast<const float4*>(a.x.p)[(((long)b * g.H + iy) * g.W + ix) * XQ + e % XQ];
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + 256 * u;
-      if (e < npx * XQ) *reinterpret_cast<float4*>(xs + e * 4) = xdw_xview(a.x, 4 * (e % XQ), v[u]);
-    }
-  }
-  __syncthreads();
-  {
-    InX bn = a.bn0;
-    bn.act = ACT0;
-    const Chan4 k0 = inx_chan4(bn, c);
-    // the lane's We column stays in registers (one LDS read of x per 16 FMAs in the loop)
-    float4 wreg[CIN];
-#pragma unroll
-    for (int k = 0; k < CIN; ++k) wreg[k] = wes[k * CG + cg];
-#pragma unroll 2
-    for (int pp = threadIdx.x >> g.lcg; pp < npx; pp += 256 >> g.lcg) {
-      const int prow = pp / g.cin, pcol = pp - prow * g.cin;
-      const int iy = r0 + prow, ix = c0 + pcol;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
-        v = inx_apply4(bn, k0, xdw_y0<CIN>(xs + pp * CIN, [&](int k) { return wreg[k]; }));
-      tile[(pp << g.lcg) + cg] = v;
-    }
-  }
-  __syncthreads();
-  const int ox = ox0 + col;
-  const int row0 = rg * RPT;
-  const bool active = rg < g.nrg && ox < g.Wo && oy0 + row0 < g.Ho;
-  float4 acc[RPT];
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (active) {
-    wr.init(wt, w, g.C, c, cg, g.lcg);
-    constexpr int NR = (RPT - 1) * S + K;
-    const float4* base = tile + ((row0 * S) * g.cin + col * S) * CG + cg;
-#pragma unroll
-    for (int ir = 0; ir < NR; ++ir) {
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const float4 v = base[(ir * g.cin + j) * CG];
-#pragma unroll
-        for (int r = 0; r < RPT; ++r) {
-          const int i = ir - r * S;
-          if (i >= 0 && i < K) fma4(acc[r], v, wr(i * K + j));
-        }
-      }
-      if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  unsigned vmask = 0;
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) {
-    const int oy = oy0 + row0 + r;
-    if (active && oy < g.Ho) {
-      vmask |= 1u << r;
-      *reinterpret_cast<float4*>(y + (((long)b * g.Ho + oy) * g.Wo + ox) * g.C + c) = acc[r];
-    }
-  }
-  dw_stats<RPT>(acc, vmask, g.lcg, c, (long)b * g.ntiles + tl, sink);
-}
-
-// B1: k_dw_bwd's GradSink pass for BN0 with y0 recomputed from the x of the tile's own pixels (the
-// gradient w.r.t. act0(BN0(y0)) is only reduced, never stored)
-template <int K, int S, int CIN>
-__global__ __launch_bounds__(256) void k_dw_bwd_x(XdwArgs a, GradX gv, const float* __restrict__ w, DwGeom g,
-                                                  GradSink gsk) {
-  constexpr int RPT = 4, XQ = CIN / 4;
-  extern __shared__ float4 tile[];
-  const int b = blockIdx.z;
-  int tl, cgi;
-  if (!dw_block_map(blockIdx.x, g.per, g.ncg, g.ntiles * g.ncg, &tl, &cgi)) return;
-  const int CG = 1 << g.lcg;
-  const int ty = tl / g.tiles_x, tx = tl - ty * g.tiles_x;
-  const int iy0 = ty * g.oth, ix0 = tx * g.otw;
-  const int cg = threadIdx.x & (CG - 1), q = threadIdx.x >> g.lcg;
-  const int col = q % g.otw, rg = q / g.otw;
-  const int c = (cgi * CG + cg) * 4;
-  const int ay = iy0 + g.pt - (K - 1), ax = ix0 + g.pl - (K - 1);
-  const int oy_lo = S == 1 ? ay : (ay >= 0 ? ay / S : -((-ay + S - 1) / S));
-  const int ox_lo = S == 1 ? ax : (ax >= 0 ? ax / S : -((-ax + S - 1) / S));
-  const int npx = g.rin * g.cin;
-  float4* wt = tile + npx * CG;
-  float4* wes = wt + K * K * CG;
-  float* xs = reinterpret_cast<float*>(wes + CIN * CG);  // [oth * otw][CIN]
-  StageGradX<false> src;
-  src.init(gv, c);
-  Taps<K> wr;
-  wr.stage(wt, w, g.C, cgi, g.lcg);
-  for (int e = threadIdx.x; e < CIN * CG; e += 256)
-    wes[e] = *reinterpret_cast<const float4*>(a.we + (long)(e >> g.lcg) * g.C + ((cgi << g.lcg) + (e & (CG - 1))) * 4);
-  const int tpx = g.oth * g.otw;
-  for (int e = threadIdx.x; e < tpx * XQ; e += 256) {
-    const int p = e / XQ, prow = p / g.otw, pcol = p - prow * g.otw;
-    const int iy = min(iy0 + prow, g.H - 1), ix = min(ix0 + pcol, g.W - 1);
-    const float4 v = reinterpret_cast<const float4*>(a.x.p)[(((long)b * g.H + iy) * g.W + ix) * XQ + e % XQ];
-    *reinterpret_cast<float4*>(xs + e * 4) = xdw_xview(a.x, 4 * (e % XQ), v);
-  }
-  dw_stage<StageGradX<false>, 4>(tile, src, b, g.Ho, g.Wo, g.C, oy_lo, ox_lo, c, g);
-  __syncthreads();
-  const int ix = ix0 + col;
-  const int row0 = rg * RPT;
-  const bool active = rg < g.nrg && ix < g.W && iy0 + row0 < g.H;
-  float4 acc[RPT];
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (active) {
-    wr.init(wt, w, g.C, c, cg, g.lcg);
-    if constexpr (S == 1) {
-      constexpr int NR = RPT + K - 1;
-      const float4* base = tile + (row0 * g.cin + col) * CG + cg;
-#pragma unroll
-      for (int ir = 0; ir < NR; ++ir) {
-#pragma unroll
-        for (int jj = 0; jj < K; ++jj) {
-          const float4 v = base[(ir * g.cin + jj) * CG];
-#pragma unroll
-          for (int r = 0; r < RPT; ++r) {
-            const int ii = ir - r;
-            if (ii >= 0 && ii < K) fma4(acc[r], v, wr((K - 1 - ii) * K + (K - 1 - jj)));
-          }
-        }
-        if constexpr (K > 3) __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-      const int u0 = ix + g.pl;
-#pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const int t0 = iy0 + row0 + r + g.pt;
-#pragma unroll
-        for (int i = 0; i < K; ++i) {
-          const int t = t0 - i;
-          if (t & 1) continue;
-          const int lr = (t >> 1) - oy_lo;
-#pragma unroll
-          for (int j = 0; j < K; ++j) {
-            const int u = u0 - j;
-            if (u & 1) continue;
-            const int lc = (u >> 1) - ox_lo;
-            fma4(acc[r], tile[(lr * g.cin + lc) * CG + cg], wr(i * K + j));
-          }
-        }
-      }
-    }
-  }
-  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
-  if (active) {
-    const GSChan4 kk = gs_chan4(gsk, c);
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      __builtin_amdgcn_sched_barrier(0);  // one row's recompute live at a time (VGPRs)
-      if (iy0 + row0 + r >= g.H) continue;
-      const float4 y0 = xdw_y0<CIN>(xs + ((row0 + r) * g.otw + col) * CIN, [&](int k) { return wes[k * CG + cg]; });
-      gs_acc4(gsk, kk, acc[r], y0, s1, s2);
-    }
-  }
-  dw_gsums(s1, s2, g.lcg, c, (long)b * g.ntiles + tl, gsk);
-}
-
-// B2: one 8x8 tile of input pixels per workgroup, 4 lanes per pixel (lane quarter qq takes the
-// channel quads qq, qq + 4, ...).  The window of the depthwise output gradient (BN1's backward
-// applied on load, every channel), We, the taps and BN0's parameters are staged in LDS; per pixel:
-// da0 = the depthwise transpose, y0 recomputed, dy0 = BN0's backward of act0'(z0) * da0, and
-// dx[k] = sum_c dy0[c] * We[k][c], the quarters' partial sums added by two xor shuffles.  gsx: the
-// BN-backward sums of the BN whose output x is (dx is its output gradient), one partial row per
-// workgroup.
-struct XdwDxGeom {
-  int H, W, Ho, Wo, pt, pl, tiles_x, wr, wc;
-};
-template <int K, int S, int CIN, int ACT0, int ACT1>
-__global__ __launch_bounds__(256) void k_xdw_dx(XdwArgs a, GradX gv, const float* __restrict__ w,
-                                                float* __restrict__ dx, int acc_flag, XdwDxGeom g, GradSink gsx) {
-  constexpr int XQ = CIN / 4;
-  gv.act = ACT1;  // (as StageGradX::finish_t: the same arithmetic as B1's staged window)
-  extern __shared__ float4 tile[];
-  const int CE = a.ce, CQ = CE >> 2;
-  const int b = blockIdx.y;
-  const int ty = blockIdx.x / g.tiles_x, tx = blockIdx.x - ty * g.tiles_x;
-  const int iy0 = ty * 8, ix0 = tx * 8;
-  const int ay = iy0 + g.pt - (K - 1), ax = ix0 + g.pl - (K - 1);
-  const int oy_lo = S == 1 ? ay : (ay >= 0 ? ay / S : -((-ay + S - 1) / S));
-  const int ox_lo = S == 1 ? ax : (ax >= 0 ? ax / S : -((-ax + S - 1) / S));
-  float4* ddw = tile;                           // [wr * wc][CQ]
-  float4* wel = ddw + g.wr * g.wc * CQ;         // We [CIN][CQ]
-  float4* wtl = wel + CIN * CQ;                 // taps [K * K][CQ]
-  float4* bnp = wtl + K * K * CQ;               // BN0: mu, rstd, sc, be, mdz, mdzx [6][CQ]
-  for (int e = threadIdx.x; e < CIN * CQ; e += 256) wel[e] = reinterpret_cast<const float4*>(a.we)[e];
-  for (int e = threadIdx.x; e < K * K * CQ; e += 256) wtl[e] = reinterpret_cast<const float4*>(w)[e];
-  for (int e = threadIdx.x; e < CQ; e += 256) {
-    bnp[e] = reinterpret_cast<const float4*>(a.bn0.mu)[e];
-    bnp[CQ + e] = reinterpret_cast<const float4*>(a.rs0)[e];
-    bnp[2 * CQ + e] = reinterpret_cast<const float4*>(a.bn0.sc)[e];
-    bnp[3 * CQ + e] = reinterpret_cast<const float4*>(a.bn0.be)[e];
-    bnp[4 * CQ + e] = reinterpret_cast<const float4*>(a.mdz0)[e];
-    bnp[5 * CQ + e] = reinterpret_cast<const float4*>(a.mdzx0)[e];
-  }
-  // the gradient window: (pixel, quad) work items, the BN1 backward applied on load
-  const int nwin = g.wr * g.wc * CQ;
-  for (int e0 = threadIdx.x; e0 < nwin; e0 += 1024) {
-    float4 d[4], yv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = min(e0 + 256 * u, nwin - 1);
-      const int p = e / CQ, cq = e - p * CQ;
-      const int prow = p / g.wc, pcol = p - prow * g.wc;
-      const int oy = min(max(oy_lo + prow, 0), g.Ho - 1), ox = min(max(ox_lo + pcol, 0), g.Wo - 1);
-      const long off = (((long)b * g.Ho + oy) * g.Wo + ox) * CE + cq * 4;
-      d[u] = *reinterpret_cast<const float4*>(gv.da + off);
-      if (gv.y) yv[u] = *reinterpret_cast<const float4*>(gv.y + off);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int e = e0 + 256 * u;
-      if (e >= nwin) continue;
-      const int p = e / CQ, cq = e - p * CQ;
-      const int prow = p / g.wc, pcol = p - prow * g.wc;
-      const int oy = oy_lo + prow, ox = ox_lo + pcol;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (oy >= 0 && oy < g.Ho && ox >= 0 && ox < g.Wo) v = gv.y ? gx_apply4(gv, gx_chan4(gv, cq * 4), d[u], yv[u]) : d[u];
-      ddw[e] = v;
-    }
-  }
-  __syncthreads();
-  const int p = threadIdx.x >> 2, qq = threadIdx.x & 3;
-  const int iy = iy0 + (p >> 3), ix = ix0 + (p & 7);
-  const bool active = iy < g.H && ix < g.W;
-  const int iyc = min(iy, g.H - 1), ixc = min(ix, g.W - 1);
-  const long xo = (((long)b * g.H + iyc) * g.W + ixc) * CIN;
-  float xraw[CIN], xr[CIN], dxp[CIN];
-#pragma unroll
-  for (int q4 = 0; q4 < XQ; ++q4) {
-    const float4 v = *reinterpret_cast<const float4*>(a.x.p + xo + 4 * q4);
-    const float4 u = xdw_xview(a.x, 4 * q4, v);
-    xraw[4 * q4] = v.x; xraw[4 * q4 + 1] = v.y; xraw[4 * q4 + 2] = v.z; xraw[4 * q4 + 3] = v.w;
-    xr[4 * q4] = u.x; xr[4 * q4 + 1] = u.y; xr[4 * q4 + 2] = u.z; xr[4 * q4 + 3] = u.w;
-  }
-#pragma unroll
-  for (int k = 0; k < CIN; ++k) dxp[k] = 0.f;
-  const int t0 = iyc + g.pt, u0 = ixc + g.pl;
-  for (int cq = qq; cq < CQ; cq += 4) {
-    // (taps in k_dw_bwd's order, so da0 is bit-identical to the one B1 reduced)
-    float4 da = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (S == 1) {
-#pragma unroll
-      for (int ii = 0; ii < K; ++ii) {
-        const int i = K - 1 - ii, lr = t0 - i - oy_lo;
-#pragma unroll
-        for (int jj = 0; jj < K; ++jj) {
-          const int j = K - 1 - jj, lc = u0 - j - ox_lo;
-          fma4(da, ddw[(lr * g.wc + lc) * CQ + cq], wtl[(i * K + j) * CQ + cq]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const int t = t0 - i;
-        if (t & 1) continue;
-        const int lr = (t >> 1) - oy_lo;
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-          const int u = u0 - j;
-          if (u & 1) continue;
-          const int lc = (u >> 1) - ox_lo;
-          fma4(da, ddw[(lr * g.wc + lc) * CQ + cq], wtl[(i * K + j) * CQ + cq]);
-        }
-      }
-    }
-    const float4 y0 = xdw_y0<CIN>(xr, [&](int k) { return wel[k * CQ + cq]; });
-    const float4 mu = bnp[cq], rs = bnp[CQ + cq], sc = bnp[2 * CQ + cq], be = bnp[3 * CQ + cq];
-    const float4 m1 = bnp[4 * CQ + cq], m2 = bnp[5 * CQ + cq];
-    const float4 dy = make_float4(gx_one(da.x, y0.x, mu.x, rs.x, sc.x, be.x, m1.x, m2.x, ACT0),
-                                  gx_one(da.y, y0.y, mu.y, rs.y, sc.y, be.y, m1.y, m2.y, ACT0),
-                                  gx_one(da.z, y0.z, mu.z, rs.z, sc.z, be.z, m1.z, m2.z, ACT0),
-                                  gx_one(da.w, y0.w, mu.w, rs.w, sc.w, be.w, m1.w, m2.w, ACT0));
-#pragma unroll
-    for (int k = 0; k < CIN; ++k) {
-      const float4 wk = wel[k * CQ + cq];
-      float v = dxp[k];
-      v = fmaf(dy.x, wk.x, v);
-      v = fmaf(dy.y, wk.y, v);
-      v = fmaf(dy.z, wk.z, v);
-      v = fmaf(dy.w, wk.w, v);
-      dxp[k] = v;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < CIN; ++k) {
-    dxp[k] += __shfl_xor(dxp[k], 1);
-    dxp[k] += __shfl_xor(dxp[k], 2);
-  }
-  float4 s1[XQ], s2[XQ];
-#pragma unroll
-  for (int q4 = 0; q4 < XQ; ++q4) s1[q4] = s2[q4] = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (qq == 0 && active) {
-    float4* o = reinterpret_cast<float4*>(dx + xo);
-#pragma unroll
-    for (int q4 = 0; q4 < XQ; ++q4) {
-      float4 v = make_float4(dxp[4 * q4], dxp[4 * q4 + 1], dxp[4 * q4 + 2], dxp[4 * q4 + 3]);
-      if (acc_flag) {
-        const float4 old = o[q4];
-        v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
-      }
-      o[q4] = v;
-      if (gsx.part)
-        gs_acc4(gsx, gs_chan4(gsx, 4 * q4), v,
-                make_float4(xraw[4 * q4], xraw[4 * q4 + 1], xraw[4 * q4 + 2], xraw[4 * q4 + 3]), s1[q4], s2[q4]);
-    }
-  }
-  if (!gsx.part) return;
-  // the 64 pixels' sums: lanes 4 apart in a wave (xor 4..32), then the 4 waves in LDS
-  __shared__ float4 r1[4][XQ], r2[4][XQ];
-#pragma unroll
-  for (int q4 = 0; q4 < XQ; ++q4) {
-#pragma unroll
-    for (int o = 4; o < 64; o <<= 1) {
-      s1[q4].x += __shfl_xor(s1[q4].x, o); s1[q4].y += __shfl_xor(s1[q4].y, o);
-      s1[q4].z += __shfl_xor(s1[q4].z, o); s1[q4].w += __shfl_xor(s1[q4].w, o);
-      s2[q4].x += __shfl_xor(s2[q4].x, o); s2[q4].y += __shfl_xor(s2[q4].y, o);
-      s2[q4].z += __shfl_xor(s2[q4].z, o); s2[q4].w += __shfl_xor(s2[q4].w, o);
-    }
-  }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0)
-#pragma unroll
-    for (int q4 = 0; q4 < XQ; ++q4) {
-      r1[wave][q4] = s1[q4];
-      r2[wave][q4] = s2[q4];
-    }
-  __syncthreads();
-  if (threadIdx.x < XQ) {
-    const int q4 = threadIdx.x;
-    float4 t1 = r1[0][q4], t2 = r2[0][q4];
-#pragma unroll
-    for (int wv = 1; wv < 4; ++wv) {
-      const float4 u = r1[wv][q4], v = r2[wv][q4];
-      t1.x += u.x; t1.y += u.y; t1.z += u.z; t1.w += u.w;
-      t2.x += v.x; t2.y += v.y; t2.z += v.z; t2.w += v.w;
-    }
-    const long prow = (long)b * gridDim.x + blockIdx.x;
-    gsink_put(gsx, prow, 4 * q4 + 0, t1.x, t2.x);
-    gsink_put(gsx, prow, 4 * q4 + 1, t1.y, t2.y);
-    gsink_put(gsx, prow, 4 * q4 + 2, t1.z, t2.z);
-    gsink_put(gsx, prow, 4 * q4 + 3, t1.w, t2.w);
   }
 }
 
@@ -1315,158 +805,6 @@ void launch_dw_bwd_group(const DwSeg* segs, int n, int B, int C, const float* w,
     nps[i] = grp.s[i].gs.P;
   }
   dw_bwd_dispatch(grp, n, B, gsums, k, stride, s);
-}
-
-// ---- expand -> depthwise fusion: host side --------------------------------------------------
-bool xdw_supported(int cin, int ce, int k, int s, int act0) {
-  return (cin == 16 || cin == 24 || cin == 32) && ce % 16 == 0 && ce <= 192 && (k == 3 || k == 5) &&
-         (s == 1 || s == 2) && (act0 == 1 || act0 == 2);
-}
-
-static long xdw_rpc(long M) { return std::max(64L, (M + 1023) / 1024 + 63) / 64 * 64; }
-size_t xdw_stats_scratch_doubles(long M, int ce) { return (size_t)cdiv(M, xdw_rpc(M)) * ce * 2; }
-
-// raise the kernel's dynamic LDS limit to what 160 KB leaves beside its static LDS (once)
-template <auto KFN>
-static void xdw_lds_attr(size_t lds) {
-  static const size_t cap = [] {
-    hipFuncAttributes fa{};
-    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(KFN)) != hipSuccess) return (size_t)0;
-    const size_t c = 160 * 1024 - fa.sharedSizeBytes;
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(KFN), hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)c) == hipSuccess ? c : (size_t)0;
-  }();
-  if (cap == 0) throw std::runtime_error("xdw: cannot raise the dynamic LDS limit");
-  if (lds > cap) throw std::runtime_error("xdw: LDS window too large");
-}
-
-void launch_xdw_stats(const XdwArgs& a, int cin, long M, double* scratch, float* ref, float* mean, float* rstd,
-                      const float* gamma, float* sc, float* mmean, float* mvar, float eps, hipStream_t s,
-                      double* side) {
-  const long rpc = xdw_rpc(M);
-  const int chunks = cdiv(M, rpc);
-  dim3 grid(chunks);
-  if (cin == 16) hipLaunchKernelGGL((k_xdw_stats<16>), grid, dim3(256), 0, s, a, M, rpc, scratch, ref);
-  else if (cin == 24) hipLaunchKernelGGL((k_xdw_stats<24>), grid, dim3(256), 0, s, a, M, rpc, scratch, ref);
-  else if (cin == 32) hipLaunchKernelGGL((k_xdw_stats<32>), grid, dim3(256), 0, s, a, M, rpc, scratch, ref);
-  else throw std::invalid_argument("xdw: unsupported input width");
-  PHX_LAUNCH_CHECK();
-  launch_bn_stats_final(scratch, chunks, M, a.ce, ref, mean, rstd, gamma, sc, mmean, mvar, eps, side, s);
-}
-
-template <int K, int S, int RPT, int CIN>
-static void xdw_fwd_go(const XdwArgs& a, const float* w, float* y, const DwGeom& g, StatSink sink, int B,
-                       hipStream_t s) {
-  const size_t lds = dw_lds(g, K) + (size_t)CIN * (1 << g.lcg) * 16 + (size_t)g.rin * g.cin * CIN * 4;
-  dim3 grid(8 * g.per, 1, B);
-  if (a.bn0.act == 1) {
-    xdw_lds_attr<&k_dw_fwd_x<K, S, RPT, CIN, 1>>(lds);
-    hipLaunchKernelGGL((k_dw_fwd_x<K, S, RPT, CIN, 1>), grid, dim3(256), lds, s, a, w, y, g, sink);
-  } else {
-    xdw_lds_attr<&k_dw_fwd_x<K, S, RPT, CIN, 2>>(lds);
-    hipLaunchKernelGGL((k_dw_fwd_x<K, S, RPT, CIN, 2>), grid, dim3(256), lds, s, a, w, y, g, sink);
-  }
-}
-
-template <int K, int S, int RPT>
-static void xdw_fwd_cin(int cin, const XdwArgs& a, const float* w, float* y, const DwGeom& g, StatSink sink, int B,
-                        hipStream_t s) {
-  if (cin == 16) xdw_fwd_go<K, S, RPT, 16>(a, w, y, g, sink, B, s);
-  else if (cin == 24) xdw_fwd_go<K, S, RPT, 24>(a, w, y, g, sink, B, s);
-  else xdw_fwd_go<K, S, RPT, 32>(a, w, y, g, sink, B, s);
-}
-
-int launch_dw_fwd_x(const XdwArgs& a, int cin, const float* w, float* y, int B, int H, int W, int Ho, int Wo,
-                    int k, int stride, int pt, int pl, StatSink sink, hipStream_t s) {
-  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || !sink.part || sink.fd)
-    throw std::invalid_argument("xdw fwd: unsupported shape");
-  const int rpt = dw_rpt_fwd(stride);
-  if (rpt != 2 && stride == 2) throw std::invalid_argument("xdw fwd: stride 2 runs 2 rows per lane");
-  const DwGeom g = dw_plan(H, W, a.ce, Ho, Wo, pt, pl, k, stride, rpt, false);
-  sink.P = B * g.ntiles;
-  if (k == 3 && stride == 1) xdw_fwd_cin<3, 1, 4>(cin, a, w, y, g, sink, B, s);
-  else if (k == 3) xdw_fwd_cin<3, 2, 2>(cin, a, w, y, g, sink, B, s);
-  else if (stride == 1) xdw_fwd_cin<5, 1, 4>(cin, a, w, y, g, sink, B, s);
-  else xdw_fwd_cin<5, 2, 2>(cin, a, w, y, g, sink, B, s);
-  PHX_LAUNCH_CHECK();
-  return sink.P;
-}
-
-template <int K, int S, int CIN>
-static void xdw_bwd_go(const XdwArgs& a, GradX gv, const float* w, const DwGeom& g, GradSink gs, int B,
-                       hipStream_t s) {
-  const size_t lds = dw_lds(g, K) + (size_t)CIN * (1 << g.lcg) * 16 + (size_t)g.oth * g.otw * CIN * 4;
-  xdw_lds_attr<&k_dw_bwd_x<K, S, CIN>>(lds);
-  hipLaunchKernelGGL((k_dw_bwd_x<K, S, CIN>), dim3(8 * g.per, 1, B), dim3(256), lds, s, a, gv, w, g, gs);
-}
-
-template <int K, int S>
-static void xdw_bwd_cin(int cin, const XdwArgs& a, GradX gv, const float* w, const DwGeom& g, GradSink gs, int B,
-                        hipStream_t s) {
-  if (cin == 16) xdw_bwd_go<K, S, 16>(a, gv, w, g, gs, B, s);
-  else if (cin == 24) xdw_bwd_go<K, S, 24>(a, gv, w, g, gs, B, s);
-  else xdw_bwd_go<K, S, 32>(a, gv, w, g, gs, B, s);
-}
-
-int launch_dw_bwd_x(const XdwArgs& a, int cin, GradX gv, const float* w, int B, int H, int W, int Ho, int Wo,
-                    int k, int stride, int pt, int pl, GradSink gs0, hipStream_t s) {
-  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || !gs0.part || gs0.fd || (gv.y && gv.ybf))
-    throw std::invalid_argument("xdw bwd: unsupported shape");
-  const DwGeom g = dw_plan(H, W, a.ce, Ho, Wo, pt, pl, k, stride, 4, true);
-  gs0.P = B * g.ntiles;
-  if (k == 3 && stride == 1) xdw_bwd_cin<3, 1>(cin, a, gv, w, g, gs0, B, s);
-  else if (k == 3) xdw_bwd_cin<3, 2>(cin, a, gv, w, g, gs0, B, s);
-  else if (stride == 1) xdw_bwd_cin<5, 1>(cin, a, gv, w, g, gs0, B, s);
-  else xdw_bwd_cin<5, 2>(cin, a, gv, w, g, gs0, B, s);
-  PHX_LAUNCH_CHECK();
-  return gs0.P;
-}
-
-int xdw_dx_partials(int B, int H, int W) { return B * cdiv(H, 8) * cdiv(W, 8); }
-
-template <int K, int S, int CIN, int A0, int A1>
-static void xdw_dx_go(const XdwArgs& a, GradX gv, const float* w, float* dx, int acc, const XdwDxGeom& g,
-                      GradSink gsx, int B, size_t lds, hipStream_t s) {
-  xdw_lds_attr<&k_xdw_dx<K, S, CIN, A0, A1>>(lds);
-  hipLaunchKernelGGL((k_xdw_dx<K, S, CIN, A0, A1>), dim3(g.tiles_x * cdiv(g.H, 8), B), dim3(256), lds, s, a, gv, w,
-                     dx, acc, g, gsx);
-}
-
-template <int K, int S, int CIN>
-static void xdw_dx_act(const XdwArgs& a, GradX gv, const float* w, float* dx, int acc, const XdwDxGeom& g,
-                       GradSink gsx, int B, size_t lds, hipStream_t s) {
-  const int a0 = a.bn0.act, a1 = gv.y ? gv.act : 0;
-  if (a0 == 1 && a1 == 1) xdw_dx_go<K, S, CIN, 1, 1>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-  else if (a0 == 2 && a1 == 2) xdw_dx_go<K, S, CIN, 2, 2>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-  else if (a0 == 1 && a1 == 0) xdw_dx_go<K, S, CIN, 1, 0>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-  else if (a0 == 2 && a1 == 0) xdw_dx_go<K, S, CIN, 2, 0>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-  else throw std::invalid_argument("xdw dx: unsupported activations");
-}
-
-template <int K, int S>
-static void xdw_dx_cin(int cin, const XdwArgs& a, GradX gv, const float* w, float* dx, int acc, const XdwDxGeom& g,
-                       GradSink gsx, int B, size_t lds, hipStream_t s) {
-  if (cin == 16) xdw_dx_act<K, S, 16>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-  else if (cin == 24) xdw_dx_act<K, S, 24>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-  else xdw_dx_act<K, S, 32>(a, gv, w, dx, acc, g, gsx, B, lds, s);
-}
-
-int launch_xdw_dx(const XdwArgs& a, int cin, GradX gv, const float* w, float* dx, bool acc, int B, int H, int W,
-                  int Ho, int Wo, int k, int stride, int pt, int pl, GradSink gsx, hipStream_t s) {
-  if (!xdw_supported(cin, a.ce, k, stride, a.bn0.act) || (gv.y && gv.ybf) || (gsx.part && gsx.ybf) || gsx.fd)
-    throw std::invalid_argument("xdw dx: unsupported shape");
-  XdwDxGeom g{H, W, Ho, Wo, pt, pl, cdiv(W, 8), 0, 0};
-  g.wr = stride == 1 ? 8 + k - 1 : (8 - 1 + k - 1) / 2 + 2;
-  g.wc = g.wr;
-  const int CQ = a.ce / 4;
-  const size_t lds = ((size_t)g.wr * g.wc * CQ + (size_t)cin * CQ + (size_t)k * k * CQ + 6 * (size_t)CQ) * 16;
-  gsx.P = xdw_dx_partials(B, H, W);
-  if (k == 3 && stride == 1) xdw_dx_cin<3, 1>(cin, a, gv, w, dx, acc ? 1 : 0, g, gsx, B, lds, s);
-  else if (k == 3) xdw_dx_cin<3, 2>(cin, a, gv, w, dx, acc ? 1 : 0, g, gsx, B, lds, s);
-  else if (stride == 1) xdw_dx_cin<5, 1>(cin, a, gv, w, dx, acc ? 1 : 0, g, gsx, B, lds, s);
-  else xdw_dx_cin<5, 2>(cin, a, gv, w, dx, acc ? 1 : 0, g, gsx, B, lds, s);
-  PHX_LAUNCH_CHECK();
-  return gsx.P;
 }
 
 }  // namespace phx

@@ -347,13 +347,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm2k(Gemm2Args a) {
       if (h == 0 && cok) gsink_put(a.gsk, prow, col, s1, s2);
     }
   }
-  if constexpr (SK != 0) {
-    // in-launch finalize (FinDesc): TM partial rows of this workgroup's columns
-    const unsigned ent = (unsigned)(TM * max(0, min(BN, a.N - n0)));
-    __syncthreads();  // (every wave's LDS reads are done before the scratch word is reused)
-    if constexpr (SK == 1) sink_finish(a.sink, ent, sm);
-    else gsink_finish(a.gsk, ent, sm);
-  }
 }
 
 // storage variants as g2_go: fp32 compute stores fp32 (ST 0); bf16 compute runs its forward modes on

@@ -279,7 +279,6 @@ __global__ __launch_bounds__(256) void k_ew_gstats(F f, long seg_rows, int C, lo
     gsink_put(g, p, c4 * 4 + 2, s1.z, s2.z);
     gsink_put(g, p, c4 * 4 + 3, s1.w, s2.w);
   }
-  gsink_finish(g, 4u * (unsigned)tpr, sh1);
 }
 
 // rows per lane whose loads are in flight together (fp32 / bf16 BN input of the GradSink)
@@ -354,14 +353,6 @@ void launch_bn_stats(const float* y, long M, int C, double* part, float* mean, f
   StatsEpi e{y, M, mean, rstd, gamma, sc, mmean, mvar, eps, ybf ? 1 : 0, side};
   if (ybf) colred(StatsAcc<true>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
   else colred(StatsAcc<false>{y, C, {0, 0, 0, 0}}, e, M, C, 1, part, s);
-}
-
-void launch_bn_stats_final(const double* part, int chunks, long M, int C, const float* ref, float* mean, float* rstd,
-                           const float* gamma, float* sc, float* mmean, float* mvar, float eps, double* side,
-                           hipStream_t s) {
-  StatsEpi e{ref, M, mean, rstd, gamma, sc, mmean, mvar, eps, 0, side};
-  hipLaunchKernelGGL((k_colred_final<StatsEpi>), dim3(cdiv(C, 16), 1), dim3(256), 0, s, e, part, chunks, C);
-  PHX_LAUNCH_CHECK();
 }
 
 // ---- BN statistics from producer partials (StatSink / GradSink) ---------------------------

@@ -94,5 +94,9 @@ void prof_end(const ProfScope& r);
 bool ctx_profiling(const phx_ctx* ctx);  // phx_profile is on (launch groups timed one at a time)
 uint64_t ctx_seed(const phx_ctx* ctx);
 int ctx_device(const phx_ctx* ctx);
+// what a frozen first pass of the victim depends on besides its inputs: the weights / moving-statistics
+// version (bumped by every load and training pass) and the score thresholds — a prefetched first pass
+// made at another generation is stale
+uint64_t ctx_generation(const phx_ctx* ctx);
 
 }  // namespace phx

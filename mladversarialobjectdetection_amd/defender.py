@@ -19,7 +19,7 @@ import torch
 
 from . import _lib
 from . import distributed as ddp
-from .attacker import EfficientDetVictim, _pad_boxes, _stream
+from .attacker import EfficientDetVictim, _pad_boxes, _stream, _withdraw_if_refilled
 from .h5 import read_keras_weights, write_keras_weights
 
 KERAS_MODEL = "patch_neutralizer"  # generator.py:80: PatchNeutralizer's name; its output conv is
@@ -264,11 +264,16 @@ class PatchAttackDefender:
         (defender_train.py's fit draws it from the generator): its first pass (a function of the
         images alone: the protege is frozen) then runs beside this step's U-Net work
         (phx_def_set_next), and that train_step uses its boxes.  The result is the same either way."""
+        prev = getattr(self, "_next_keep", None)  # alive until the call that joins its first pass
+        _withdraw_if_refilled(self, lambda: self.handle.call("phx_def_set_next", None, 0, 0))
+        self._next_keep = self._next_rec = None
         if next_inputs is not None:
             nx = self.protege_model._check_images(next_inputs)
             self._next_keep = nx  # alive until the step that consumes it
+            self._next_rec = (nx, nx._version)
             self.handle.call("phx_def_set_next", nx.data_ptr(), nx.shape[0], self.global_offset(nx.shape[0]))
         self.call(inputs, boxes=boxes)
+        del prev
         ddp.allreduce_sum_(self._red)
         self.apply_gradients()
         self.cur_step += 1

@@ -56,7 +56,8 @@ def _step_vs_oracle(B):
     assert _cos(gp, rp) >= 0.99999, _cos(gp, rp)
     assert np.linalg.norm(gp - rp) / np.linalg.norm(rp) <= 5e-3
     assert abs(g[-1] - ref["grad"][-1]) <= 1e-5 * max(1.0, abs(ref["grad"][-1]))
-    check_metric_row(met, ref, B)
+    # the metric row's sums of m_b are held to the per-image bound below, summed over the batch
+    check_metric_row(met, ref, B, m_rtol=0.0, m_atol=2e-5)
     mt = torch.empty(B, device="cuda")
     v.ctx.call("phx_debug_last_maxscores", mt.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
     # per-image max scores: |d| <= 2e-5 as for the first pass's scores (fp32 through ~100 BN layers

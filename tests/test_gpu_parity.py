@@ -282,16 +282,24 @@ def test_step_grad_matches_oracle(victim, wdict):
     check_metric_row(met, ref, 2)
 
 
-def check_metric_row(met, ref, B, add_tv=True):
-    """R17: the metric row (attacker.py:196-207, calc_asr :238-255) against the oracle's values."""
+def check_metric_row(met, ref, B, add_tv=True, m_rtol=1e-5, m_atol=1e-6):
+    """R17: the metric row (attacker.py:196-207, calc_asr :238-255) against the oracle's values.
+
+    The sums over images of the per-image max score m_b and of m_b^2 are held to the bound the calling
+    test applies to each m_b (|dm_b| <= d_b = m_atol + m_rtol |m_b|, its phx_debug_last_maxscores
+    check), summed: |sum dm_b| <= sum d_b and |sum (m_b^2 - m_ref_b^2)| = |sum dm_b (2 m_ref_b + dm_b)|
+    <= sum d_b (2 |m_ref_b| + d_b).  Nothing else is derived: a row element that is a sum of exactly
+    computed terms (counts, the scale loss, TV) keeps its own bound."""
     from mladversarialobjectdetection_amd import _lib
     assert abs(met[_lib.M_SCALE_LOSS] - ref["scale_loss"]) <= 1e-5 * max(abs(ref["scale_loss"]), 1e-6)
     if add_tv:
         assert abs(met[_lib.M_TV] - ref["tv"]) <= 1e-6 * ref["tv"]
     else:
         assert met[_lib.M_TV] == 0.0
-    np.testing.assert_allclose(met[_lib.M_SUM_M], ref["m"].sum(), rtol=1e-5, atol=1e-7)
-    np.testing.assert_allclose(met[_lib.M_SUM_M2], (ref["m"] ** 2).sum(), rtol=1e-5, atol=1e-7)
+    m = np.abs(np.asarray(ref["m"], np.float64))
+    d = m_atol + m_rtol * m
+    assert abs(met[_lib.M_SUM_M] - ref["m"].sum()) <= d.sum(), (met[_lib.M_SUM_M], ref["m"].sum(), d.sum())
+    assert abs(met[_lib.M_SUM_M2] - (ref["m"] ** 2).sum()) <= (d * (2 * m + d)).sum()
     assert met[_lib.M_ASR_NUM] == ref["asr_num"] and met[_lib.M_ASR_DEN] == ref["asr_den"]
     assert met[_lib.M_NBOX] == ref["nbox"] and met[_lib.M_NIMG] == B
 
