@@ -83,6 +83,9 @@ struct Exec {
   std::vector<int> se_of_tensor;               // tensor id -> SE op index producing it (-1)
   // BiFPN node fuse folded into the depthwise conv after it (computed on load, never written)
   std::vector<char> fuse_folded;               // op id of the fuse -> 1
+  // fused separable convs (kernels_sep.hip): sep[i] = 1 for a 3x3 depthwise op i whose output only the
+  // pointwise op i + 1 reads; one launch computes both and the depthwise output is never stored
+  std::vector<char> sep;
   // expand -> BN -> act -> depthwise fused (kernels_dw.hip): op id of the expand
   // conv -> 1; the expand output is never stored in a training pass (ops i, i+1, i+2)
   std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
@@ -697,6 +700,54 @@ Exec& phx_ctx::exec_for(int B, int tag) {
       E.fuse_folded[i] = 1;
     }
   }
+  // fused separable convs: a 3x3 stride-1 depthwise op whose output feeds only the next op's
+  // pointwise conv (keras SeparableConv2D of the BiFPN nodes and both heads, model.cpp sepconv), fp32,
+  // both ungrouped or grouped member for member (the heads' per-level copies).  PHX_SEP=0 keeps the
+  // two launches (A/B; read per executor).
+  E.sep.assign(P.ops.size(), 0);
+  {
+    const char* se = std::getenv("PHX_SEP");
+    const bool on = !(se && se[0] == '0');
+    const char* sr = std::getenv("PHX_SEP_MINROWS");
+    const long sep_min_rows = sr ? atol(sr) : 32768;
+    std::vector<int> nuse(P.tensors.size(), 0);
+    for (const Op& op : P.ops)
+      for (int j = 0; j < op.nin; ++j) ++nuse[op.in[j]];
+    for (size_t i = 0; on && i + 1 < P.ops.size(); ++i) {
+      const Op& d = P.ops[i];
+      const Op& pw = P.ops[i + 1];
+      if (d.t != OP_DW || pw.t != OP_PW || pw.in[0] != d.out || pw.nin != 1 || nuse[d.out] != 1) continue;
+      if (d.k != 3 || d.stride != 1 || d.in[0] == P.input) continue;
+      const Tensor& ti = P.tensors[d.in[0]];
+      const Tensor& to = P.tensors[pw.out];
+      if (!sep_supported(ti.c, to.c, E.bf16 || E.abf) || E.se_of_tensor[d.out] >= 0) continue;
+      // the fused launch is a latency chain per 8 x 16 tile (window, depthwise, MFMAs, stores): it wins
+      // where there are enough tiles to fill the chip (the P3 level; a head group, whose P3 member
+      // dominates) and loses to the two launches on the small levels (tools/sep_probe: 4 x 4 to
+      // 32 x 32 levels of 16 images 1-5 us slower fused)
+      if ((long)ti.rows() < sep_min_rows) continue;
+      const int gd = E.grp_of[i], gp = E.grp_of[i + 1];
+      if ((gd >= 0) != (gp >= 0)) continue;
+      if (gd >= 0) {
+        const std::vector<int>& a = E.groups[gd];
+        const std::vector<int>& b = E.groups[gp];
+        bool ok = a.size() == b.size() && a[0] == (int)i;
+        for (size_t r = 0; ok && r < a.size(); ++r) ok = b[r] == a[r] + 1 && P.ops[a[r]].out == P.ops[b[r]].in[0];
+        if (!ok) continue;
+      }
+      if (i > 0 && E.fuse_folded[i - 1] && gd >= 0) continue;  // (a fuse view is never grouped)
+      const std::vector<int> mem = gd >= 0 ? E.groups[gd] : std::vector<int>{(int)i};
+      for (int di : mem) {
+        E.sep[di] = 1;
+        const Tensor& tm = P.tensors[P.ops[di].in[0]];
+        if (di + 2 < (int)P.ops.size() && E.fused_bn[di + 2] && P.ops[di + 2].in[0] == P.ops[di + 1].out) {
+          const int np = sep_stat_partials(tm.n, tm.h, tm.w);
+          sp_need = std::max(sp_need, (size_t)np * to.c);
+          sc_need = std::max(sc_need, (size_t)np);
+        }
+      }
+    }
+  }
   const size_t nreg = E.groups.empty() ? 1 : kMaxSeg;
   E.sp_region = sp_need;
   E.sc_region = sc_need;
@@ -928,7 +979,7 @@ void ck_fwd(Exec& E, int i, int pass, hipStream_t s) {
   if (!E.ck_on) return;
   const Program& P = E.prog;
   const Op& op = P.ops[i];
-  if (E.fuse_folded[i]) return;
+  if (E.fuse_folded[i] || E.sep[i]) return;  // (never stored)
   const std::string nm = "p" + std::to_string(pass) + " f " + std::to_string(i) + " " + op.name;
   const Tensor& ti = P.tensors[op.in[0]];
   if (op.t == OP_BN) {
@@ -1283,6 +1334,62 @@ void run_group_bwd(phx_ctx* ctx, Exec& E, int gid, const float* input, hipStream
   }
 }
 
+// the fused separable conv whose depthwise op is i (its group's members when grouped): the depthwise
+// op's input view — the BiFPN node fuse computed on load when that fuse is folded — the pointwise op's
+// weights and output, and the BN after it takes its statistics from this launch
+void run_sep(phx_ctx* ctx, Exec& E, int i, const float* input, hipStream_t s, bool frozen) {
+  const Program& P = E.prog;
+  float* W = ctx->w();
+  const int gd = E.grp_of[i];
+  const std::vector<int> mem = gd >= 0 ? E.groups[gd] : std::vector<int>{i};
+  const int n = (int)mem.size();
+  const Op& d0 = P.ops[mem[0]];
+  const Op& p0 = P.ops[mem[0] + 1];
+  const int C = P.tensors[d0.in[0]].c, N = P.tensors[p0.out].c;
+  const bool sink_on = !frozen && mem[0] + 2 < (int)P.ops.size() && E.fused_bn[mem[0] + 2];
+  SepMember m[kMaxSeg];
+  double fl = 0, by = 4.0 * (9.0 * C + (double)N * C + N);
+  for (int r = 0; r < n; ++r) {
+    const int di = mem[r];
+    const Op& d = P.ops[di];
+    const Op& pw = P.ops[di + 1];
+    const Tensor& ti = P.tensors[d.in[0]];
+    SepMember& mm = m[r];
+    mm = SepMember{};
+    if (di > 0 && E.fuse_folded[di - 1]) {
+      const Op& f = P.ops[di - 1];
+      mm.fuse = true;
+      mm.f.nin = f.nin;
+      for (int k = 0; k < f.nin; ++k) {
+        mm.f.x[k] = view(ctx, E, f.in[k], input);
+        mm.f.w[k] = f.wsm[k] >= 0 ? W + f.wsm[k] : nullptr;
+      }
+      mm.f.method = f.fuse_method;
+      mm.f.act = f.act;
+      by += 4.0 * (double)ti.numel() * (f.nin - 1);
+    } else {
+      mm.x = view(ctx, E, d.in[0], input);
+    }
+    mm.y = E.tptr(pw.out, input);
+    mm.H = ti.h;
+    mm.W = ti.w;
+    if (sink_on)
+      mm.sink = StatSink{E.spart + (size_t)(gd >= 0 ? r : 0) * E.sp_region, E.scnt + (size_t)(gd >= 0 ? r : 0) * E.sc_region,
+                         N, 0};
+    fl += 2.0 * ti.numel() * 9.0 + 2.0 * (double)ti.rows() * C * N;
+    by += 4.0 * ((double)ti.numel() + (double)ti.rows() * N);
+  }
+  Scope scope(ctx, "sep_fwd", fl, by, s,
+              prof_detail() ? std::string(n > 1 ? " group" : "") + op_tag(P, p0, false) : std::string());
+  int nps[kMaxSeg];
+  launch_sep_fwd(m, n, E.B, C, N, W + d0.w, ctx->wt_of(p0.w), p0.b >= 0 ? W + p0.b : nullptr, s, nps);
+  if (sink_on)
+    for (int r = 0; r < n; ++r) {
+      E.stat_P[P.ops[mem[r] + 1].out] = nps[r];
+      E.stat_region[P.ops[mem[r] + 1].out] = gd >= 0 ? r : 0;
+    }
+}
+
 // victim forward over the program (EfficientDetNet.call, efficientdet_keras.py:884-906)
 // pass: 0 first (clean) pass, 1 second (patched) pass, 2 standalone detect — with `step` and the
 // global index of the first image it keys the drop-connect draws
@@ -1322,12 +1429,23 @@ void run_forward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s, int p
     }
     if (E.grp_of[i] >= 0) {
       if (E.groups[E.grp_of[i]].front() == (int)i) {
-        run_group_fwd(ctx, E, E.grp_of[i], input, s, frozen);
-        for (int m : E.groups[E.grp_of[i]]) ck_fwd(E, m, pass, s);
+        if (E.sep[i]) {
+          run_sep(ctx, E, (int)i, input, s, frozen);
+          for (int m : E.groups[E.grp_of[i]]) ck_fwd(E, m + 1, pass, s);
+        } else if (!(i > 0 && E.sep[i - 1])) {  // (a fused sepconv's pointwise group: done above)
+          run_group_fwd(ctx, E, E.grp_of[i], input, s, frozen);
+          for (int m : E.groups[E.grp_of[i]]) ck_fwd(E, m, pass, s);
+        }
       }
       continue;
     }
     if (E.fuse_folded[i]) continue;  // computed by the depthwise conv that follows
+    if (E.sep[i]) {  // depthwise + pointwise in one launch
+      run_sep(ctx, E, (int)i, input, s, frozen);
+      ck_fwd(E, (int)i + 1, pass, s);
+      continue;
+    }
+    if (i > 0 && E.sep[i - 1]) continue;  // (the pointwise half of the fused sepconv above)
     const Op& op = P.ops[i];
     const Tensor& ti = P.tensors[op.in[0]];
     const Tensor& to = P.tensors[op.out];
@@ -2584,6 +2702,9 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
                                   " elements)");
     if (which == 0 && op.t == OP_FUSE && E.fuse_folded[i])
       throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
+    if (which == 0 && op.t == OP_DW && E.sep[i])
+      throw std::invalid_argument("tap: this depthwise output feeds the fused separable conv's registers only, "
+                                  "never stored (PHX_SEP=0 at victim creation keeps it)");
     const float* src = which == 0 ? E.tptr(t, nullptr) : E.gptr(op.out);
     if (!src) throw std::invalid_argument("tap: no gradient for this tensor");
     if (which == 0 && E.tbf(t)) launch_bf16_to_f32(src, out, (long)nfloats, (hipStream_t)stream);

@@ -141,6 +141,25 @@ struct DwSeg {
 };
 void launch_dw_fwd_group(const DwSeg* segs, int n, int B, int C, const float* w, int k, int stride,
                          hipStream_t s, int* nps);
+// ---- fused separable conv (kernels_sep.hip) ---------------------------------------------------
+// keras SeparableConv2D(3x3, SAME, depth_multiplier 1) + bias: y [B,H,W,N] = pw(dw(view(x))) + bias,
+// the depthwise output never stored.  Members share the taps wd [3][3][C], the transposed pointwise
+// kernel bt [N][C], the bias and C, N (the per-level copies of a head conv); each has its input view —
+// a BN view (x) or a BiFPN node fuse computed on load (f, fuse = true; ungrouped only) — output and
+// StatSink (the consumer BN's batch statistics of y; part == nullptr: none).  nps[i]: member i's
+// partial rows (sep_stat_partials)
+struct SepMember {
+  InX x;
+  FuseView f;
+  bool fuse;
+  float* y;
+  int H, W;
+  StatSink sink;
+};
+bool sep_supported(int C, int N, bool bf16);
+int sep_stat_partials(int B, int H, int W);
+void launch_sep_fwd(const SepMember* m, int n, int B, int C, int N, const float* wd, const float* bt,
+                    const float* bias, hipStream_t s, int* nps);
 // depthwise 3x3 s1 whose input is a BiFPN fuse computed on load (FuseView); no statistics
 void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, int H, int W, int C, int Ho,
                          int Wo, int k, int stride, int pt, int pl, hipStream_t s);

@@ -1,0 +1,91 @@
+"""The fused separable conv (kernels_sep.hip: depthwise 3x3 -> pointwise + bias in one launch, the
+depthwise output never stored) against the two-launch path (PHX_SEP=0 at victim creation).
+
+The fused kernel applies the depthwise taps in k_dw_fwd's order and runs the pointwise GEMM in
+k_gemm2's k order on the same fp32 matrix-core instruction, so every sepconv output equals the
+unfused one bit for bit when its input does.  In inference BN (bn=frozen) nothing else differs, so
+the whole detector output is bit-identical.  In a training step the consumer BN's batch statistics are
+reduced per 8 x 16 tile instead of per GEMM workgroup (another fp32 summation order), so from the
+first BN after a fused conv on results agree to rounding only: the step is checked against the
+unfused step with the oracle tests' tolerances, and the fused path is what every oracle test runs.
+
+References: efficientdet_keras.py:195-207 (OpAfterCombine), :447-455 (ClassNet), :535-547 (BoxNet).
+"""
+import numpy as np
+import pytest
+import torch
+
+from bench import synth_boxes, synth_images
+
+pytestmark = pytest.mark.gpu
+
+
+def _victim(monkeypatch, sep, model="efficientdet-d0", S=256, B=2, bn_mode="local"):
+    """PHX_SEP_MINROWS=0: every 3x3 sepconv fused, whatever its level's size (the default fuses the
+    levels with >= 32768 rows only, where the fused launch is faster: the C2 bench's P3 convs and head
+    groups, which the C2 oracle tests run)."""
+    from mladversarialobjectdetection_amd.attacker import EfficientDetVictim
+    monkeypatch.setenv("PHX_SEP", sep)
+    monkeypatch.setenv("PHX_SEP_MINROWS", "0")
+    return EfficientDetVictim(model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=5, bn_mode=bn_mode)
+
+
+@pytest.mark.parametrize("model,S", [("efficientdet-d0", 256), ("efficientdet-lite0", 320)])
+def test_sep_inference_bit_identical(monkeypatch, model, S):
+    """bn=frozen: scores, classes and boxes of every anchor equal the two-launch path's bit for bit
+    (D0: swish; lite0: relu6 and BiFPN 'sum' fuse)."""
+    imgs = torch.as_tensor(synth_images([0, 1], S)).cuda()
+    out = []
+    for sep in ("1", "0"):
+        v = _victim(monkeypatch, sep, model, S, 2, "frozen")
+        b, sc, c = v.detect(imgs)
+        torch.cuda.synchronize()
+        out.append((b.cpu().numpy(), sc.cpu().numpy(), c.cpu().numpy()))
+    (b1, s1, c1), (b0, s0, c0) = out
+    assert np.isfinite(s1).all()
+    assert np.array_equal(s1, s0) and np.array_equal(c1, c0) and np.array_equal(b1, b0)
+
+
+def test_sep_first_output_bit_identical_and_step_close(monkeypatch):
+    """Training step, D0 512^2, 4 images: the first BiFPN sepconv's output (the BN input of
+    fnode0, reached through unchanged ops) is bit-identical to the two-launch path; the step's loss,
+    d scale and d patch agree within the oracle tests' bounds (loss 1e-5, cosine 0.99999)."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd.attacker import PatchAttacker
+    B, S = 4, 512
+    imgs = torch.as_tensor(synth_images(list(range(B)), S)).cuda()
+    boxes = synth_boxes(list(range(B)), S)
+    name = b"fpn_cells/cell_0/fnode0/op_after_combine5/bn"
+    res = []
+    for sep in ("1", "0"):
+        v = _victim(monkeypatch, sep, S=S, B=B)
+        att = PatchAttacker(v, seed=7)
+        att.cur_step = 2
+        att.call(imgs, boxes=boxes)
+        n = B * (S // 64) * (S // 64) * 64
+        t = torch.empty(n, device="cuda")
+        v.ctx.call("phx_debug_tap", name, 0, t.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        res.append((att.grad.cpu().numpy().astype(np.float64), att.metrics_buf.cpu().numpy(), t.cpu().numpy()))
+    (g1, m1, t1), (g0, m0, t0) = res
+    assert np.array_equal(t1, t0)
+    assert abs(m1[_lib.M_LOSS] - m0[_lib.M_LOSS]) <= 1e-5 * abs(m0[_lib.M_LOSS])
+    assert abs(g1[-1] - g0[-1]) <= 1e-5 * max(1.0, abs(g0[-1]))
+    a, b = g1[:-1], g0[:-1]
+    assert a @ b / (np.linalg.norm(a) * np.linalg.norm(b)) >= 0.99999
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) <= 1e-3
+
+
+def test_sep_depthwise_output_not_stored(monkeypatch):
+    """The fused depthwise output is never written: tapping it is refused (PHX_SEP=0 keeps it)."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd.attacker import PatchAttacker
+    v = _victim(monkeypatch, "1")
+    att = PatchAttacker(v, seed=7)
+    imgs = torch.as_tensor(synth_images([0, 1], 256)).cuda()
+    att.call(imgs, boxes=synth_boxes([0, 1], 256))
+    n = 2 * 4 * 4 * 64  # fnode0 is the P6 node: 4 x 4 at 256^2
+    t = torch.empty(n, device="cuda")
+    with pytest.raises(_lib.PhxError, match="never stored"):
+        v.ctx.call("phx_debug_tap", b"fpn_cells/cell_0/fnode0/op_after_combine5/conv/depthwise_kernel", 0,
+                   t.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
