@@ -86,6 +86,9 @@ struct Exec {
   // fused separable convs (kernels_sep.hip): sep[i] = 1 for a 3x3 depthwise op i whose output only the
   // pointwise op i + 1 reads; one launch computes both and the depthwise output is never stored
   std::vector<char> sep;
+  // sepb[i]: the fused sepconv at depthwise op i also runs its backward in one launch (the pointwise
+  // data gradient never stored)
+  std::vector<char> sepb;
   // expand -> BN -> act -> depthwise fused (kernels_dw.hip): op id of the expand
   // conv -> 1; the expand output is never stored in a training pass (ops i, i+1, i+2)
   std::vector<int> bn_of_tensor;               // tensor id -> BN op index producing it (-1)
@@ -727,12 +730,18 @@ Exec& phx_ctx::exec_for(int B, int tag) {
       // 32 x 32 levels of 16 images 1-5 us slower fused)
       if ((long)ti.rows() < sep_min_rows) continue;
       const int gd = E.grp_of[i], gp = E.grp_of[i + 1];
-      if ((gd >= 0) != (gp >= 0)) continue;
+      if (gd < 0 && gp >= 0) continue;
       if (gd >= 0) {
+        // the pointwise members: the depthwise group's, member for member — or ungrouped copies of one
+        // kernel (the class head's predict conv: N = 810 is not grouped as a GEMM)
         const std::vector<int>& a = E.groups[gd];
-        const std::vector<int>& b = E.groups[gp];
-        bool ok = a.size() == b.size() && a[0] == (int)i;
-        for (size_t r = 0; ok && r < a.size(); ++r) ok = b[r] == a[r] + 1 && P.ops[a[r]].out == P.ops[b[r]].in[0];
+        bool ok = a[0] == (int)i;
+        for (size_t r = 0; ok && r < a.size(); ++r) {
+          const Op& pr = P.ops[a[r] + 1];
+          ok = pr.t == OP_PW && pr.in[0] == P.ops[a[r]].out && pr.w == pw.w && pr.b == pw.b &&
+               (gp >= 0 ? E.grp_of[a[r] + 1] == gp && E.groups[gp][r] == a[r] + 1 : E.grp_of[a[r] + 1] < 0);
+        }
+        if (gp >= 0) ok = ok && E.groups[gp].size() == a.size();
         if (!ok) continue;
       }
       if (i > 0 && E.fuse_folded[i - 1] && gd >= 0) continue;  // (a fuse view is never grouped)
@@ -744,6 +753,41 @@ Exec& phx_ctx::exec_for(int B, int tag) {
           const int np = sep_stat_partials(tm.n, tm.h, tm.w);
           sp_need = std::max(sp_need, (size_t)np * to.c);
           sc_need = std::max(sc_need, (size_t)np);
+        }
+      }
+    }
+  }
+  // the fused sepconvs' backward: pointwise dgrad through the consumer BN's gradient view and the
+  // depthwise transpose in one launch (not the class-predict conv: its input gradient is the sparse
+  // scatter's).  PHX_SEPB=0 keeps the two launches.
+  E.sepb.assign(P.ops.size(), 0);
+  {
+    const char* sb = std::getenv("PHX_SEPB");
+    const bool on = !(sb && sb[0] == '0') && batch_bn();
+    for (size_t i = 0; on && i + 1 < P.ops.size(); ++i) {
+      if (!E.sep[i]) continue;
+      const int gd = E.grp_of[i];
+      if (gd >= 0 && E.groups[gd][0] != (int)i) continue;  // (decided per group, at its first member)
+      const std::vector<int> mem = gd >= 0 ? E.groups[gd] : std::vector<int>{(int)i};
+      bool ok = true;
+      for (int di : mem) {
+        const Op& d = P.ops[di];
+        const Op& pw = P.ops[di + 1];
+        const int bi = E.bn_consumer[pw.out];
+        ok = ok && d.bwd && pw.bwd && !is_cls_out(P, pw.out) && bi >= 0 && P.ops[bi].bwd &&
+             sep_bwd_supported(P.tensors[d.in[0]].c, P.tensors[pw.out].c, E.bf16 || E.abf);
+        ok = ok && (di > 0 && E.gfused_bn[di - 1]) == (mem[0] > 0 && E.gfused_bn[mem[0] - 1]);
+      }
+      // a grouped pointwise dgrad must be the depthwise group's twin (the launch replaces both)
+      if (gd >= 0 && E.grp_of[i + 1] < 0) ok = false;
+      if (!ok) continue;
+      for (int di : mem) {
+        E.sepb[di] = 1;
+        if (di > 0 && E.gfused_bn[di - 1]) {
+          const Tensor& tm = P.tensors[P.ops[di].in[0]];
+          const int np = sep_stat_partials(tm.n, tm.h, tm.w);
+          E.gstat_P[di - 1] = np;
+          sp_need = std::max(sp_need, (size_t)np * tm.c);
         }
       }
     }
@@ -1599,6 +1643,52 @@ bool is_cls_out(const Program& P, int t) {
   return std::find(P.cls_out.begin(), P.cls_out.end(), t) != P.cls_out.end();
 }
 
+// the fused backward of the sepconv whose depthwise op is i (its group's members when grouped): dx of
+// the depthwise input from the pointwise output's gradient view, and the BN-backward sums of the BN
+// the depthwise conv reads
+void run_sep_bwd(phx_ctx* ctx, Exec& E, int i, const float* input, hipStream_t s) {
+  const Program& P = E.prog;
+  float* W = ctx->w();
+  const int gd = E.grp_of[i];
+  const std::vector<int> mem = gd >= 0 ? E.groups[gd] : std::vector<int>{i};
+  const int n = (int)mem.size();
+  const Op& d0 = P.ops[mem[0]];
+  const Op& p0 = P.ops[mem[0] + 1];
+  const int C = P.tensors[d0.in[0]].c, N = P.tensors[p0.out].c;
+  const bool gs_on = mem[0] > 0 && E.gfused_bn[mem[0] - 1];
+  SepBwdMember m[kMaxSeg];
+  double fl = 0, by = 4.0 * (9.0 * C + (double)N * C);
+  for (int r = 0; r < n; ++r) {
+    const int di = mem[r];
+    const Op& d = P.ops[di];
+    const Op& pw = P.ops[di + 1];
+    const Tensor& ti = P.tensors[d.in[0]];
+    SepBwdMember& mm = m[r];
+    mm = SepBwdMember{};
+    mm.gv = gview(ctx, E, pw.out, input);
+    mm.dx = E.gptr(d.in[0]);
+    mm.H = ti.h;
+    mm.W = ti.w;
+    mm.acc = d.acc[0];
+    if (gs_on) {
+      const Op& bn = P.ops[di - 1];
+      mm.gs = GradSink{E.spart + (size_t)(gd >= 0 ? r : 0) * E.sp_region, P.tensors[bn.out].c, 0, E.tptr(bn.in[0], input),
+                       E.slot_a[bn.slot], E.slot_b[bn.slot], E.slot_c[bn.slot], W + bn.beta, bn.act, E.tbf(bn.in[0])};
+    }
+    fl += 2.0 * (double)ti.rows() * C * N + 2.0 * ti.numel() * 9.0;
+    by += 4.0 * (3.0 * (double)ti.rows() * N + (d.acc[0] ? 2.0 : 1.0) * ti.numel() + (gs_on ? ti.numel() : 0.0));
+  }
+  Scope scope(ctx, "sep_bwd", fl, by, s,
+              prof_detail() ? std::string(n > 1 ? " group" : "") + op_tag(P, p0, true) : std::string());
+  int nps[kMaxSeg];
+  launch_sep_bwd(m, n, E.B, C, N, W + d0.w, W + p0.w, s, nps);
+  if (gs_on)
+    for (int r = 0; r < n; ++r) {
+      if (nps[r] != E.gstat_P[mem[r] - 1]) throw std::logic_error("sep bwd: planned and launched partial counts differ");
+      E.gstat_region[mem[r] - 1] = gd >= 0 ? r : 0;
+    }
+}
+
 // data-gradient of the victim from the sparse class-logit gradient (attacker.py:217)
 void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
   const Program& P = E.prog;
@@ -1635,11 +1725,18 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     const Op& op = P.ops[i];
     if (!op.bwd) continue;
     if (op.t == OP_PW && is_cls_out(P, op.out)) continue;  // handled by the scatter
+    if (i > 0 && E.sepb[i - 1]) continue;  // (the pointwise half of a fused sepconv: with its depthwise op)
     if (E.grp_of[i] >= 0) {
       if (E.groups[E.grp_of[i]].back() == i) {
-        run_group_bwd(ctx, E, E.grp_of[i], input, s);
+        if (E.sepb[i]) run_sep_bwd(ctx, E, i, input, s);
+        else run_group_bwd(ctx, E, E.grp_of[i], input, s);
         for (int m : E.groups[E.grp_of[i]]) ck_bwd(E, m, s);
       }
+      continue;
+    }
+    if (E.sepb[i]) {
+      run_sep_bwd(ctx, E, i, input, s);
+      ck_bwd(E, i, s);
       continue;
     }
     const Tensor& ti = P.tensors[op.in[0]];
@@ -2702,6 +2799,9 @@ int phx_debug_tap(phx_ctx* ctx, const char* op_name, int which, float* out, size
                                   " elements)");
     if (which == 0 && op.t == OP_FUSE && E.fuse_folded[i])
       throw std::invalid_argument("tap: this fuse is computed on load by its depthwise conv, never stored");
+    if (which == 1 && op.t == OP_DW && E.sepb[i])
+      throw std::invalid_argument("tap: this depthwise output's gradient is formed in LDS by the fused "
+                                  "separable-conv backward, never stored (PHX_SEPB=0 keeps it)");
     if (which == 0 && op.t == OP_DW && E.sep[i])
       throw std::invalid_argument("tap: this depthwise output feeds the fused separable conv's registers only, "
                                   "never stored (PHX_SEP=0 at victim creation keeps it)");

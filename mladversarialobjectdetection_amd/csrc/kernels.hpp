@@ -160,6 +160,20 @@ bool sep_supported(int C, int N, bool bf16);
 int sep_stat_partials(int B, int H, int W);
 void launch_sep_fwd(const SepMember* m, int n, int B, int C, int N, const float* wd, const float* bt,
                     const float* bias, hipStream_t s, int* nps);
+// its backward through the depthwise input: dx [B,H,W,C] (+)= dw^T(gv(dy) W^T), the pointwise data
+// gradient never stored.  gv: the pointwise output's gradient view (the consumer BN's backward applied
+// on load); wp: the pointwise kernel HWIO [C][N]; gs: the BN-backward sums of the BN whose output the
+// depthwise conv reads (part == nullptr: none), nps[i] = member i's partial rows (sep_stat_partials)
+struct SepBwdMember {
+  GradX gv;
+  float* dx;
+  int H, W;
+  bool acc;
+  GradSink gs;
+};
+bool sep_bwd_supported(int C, int N, bool bf16);
+void launch_sep_bwd(const SepBwdMember* m, int n, int B, int C, int N, const float* wd, const float* wp,
+                    hipStream_t s, int* nps);
 // depthwise 3x3 s1 whose input is a BiFPN fuse computed on load (FuseView); no statistics
 void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, int H, int W, int C, int Ho,
                          int Wo, int k, int stride, int pt, int pl, hipStream_t s);

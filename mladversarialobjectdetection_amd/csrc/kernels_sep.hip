@@ -396,6 +396,262 @@ SepGeom sep_geom(int H, int W, int w0) {
   return g;
 }
 
+// ---- backward: the pointwise data gradient and the depthwise transpose in one launch -------------
+// For an 8 x 16 (or 16 x 8 / 16 x 4) tile of the depthwise input's gradient dx, the workgroup
+//   1. stages the gradient of the pointwise output over the tile's window (tile + 1-pixel halo) through
+//      the consumer BN's backward view (GradX: dy = sc (dz - mean dz - xhat mean dz xhat)), zero outside
+//      the image;
+//   2. multiplies it by the pointwise kernel on the fp32 matrix cores — dd = dy W^T for every window
+//      pixel, the halo recomputed instead of stored (k_gemm2's k order: the dd of a pixel equals the
+//      unfused dgrad's) — and writes dd over the staged window in LDS;
+//   3. gathers dx from dd with the flipped taps in k_dw_bwd's order (accumulating into dx when the
+//      depthwise input has several consumers), and with a GradSink the BN-backward sums of the BN whose
+//      output the depthwise conv read, one partial row per tile.
+// dd never reaches HBM.
+template <int NS>
+struct SepBwdGroup {
+  struct Seg {
+    GradX gv;     // the pointwise output's gradient view
+    float* dx;    // [B,H,W,C]
+    SepGeom g;
+    int acc;
+    GradSink gs;  // the depthwise input's BN (part == nullptr: none)
+  } s[NS];
+  const float* wd;  // depthwise taps [3][3][C]
+  const float* wp;  // pointwise kernel HWIO [C][N]
+  int n, total, per, B;
+};
+
+template <int C>
+struct SepBwdLds {
+  static constexpr int WIN = kSepNPX * kSepWP;    // g, then dd
+  static constexpr int WPL = C * (kSepNC + 4);    // pointwise kernel [C][N + 4]
+  static constexpr int TAPS = 9 * kSepCC;
+  static constexpr int GS = 4 * 16 * 8;           // per wave, per quad: (s1, s2) float4 each
+  static constexpr int FLOATS = WIN + WPL + TAPS + GS;
+};
+
+template <int C, int NS, bool GS, bool YBF>
+__global__ __launch_bounds__(256, 2) void k_sep_bwd(SepBwdGroup<NS> grp) {
+  static_assert(C == kSepCC, "k_sep_bwd: C = N = 64");
+  constexpr int N = kSepNC, KS = N / 8, WPP = N + 4;
+  using L = SepBwdLds<C>;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* const win = sm;
+  float* const wpl = sm + L::WIN;
+  float* const taps = wpl + L::WPL;
+  float4* const gsl = reinterpret_cast<float4*>(taps + L::TAPS);
+
+  const int Lb = blockIdx.x;
+  const int wi = (Lb & 7) * grp.per + (Lb >> 3);
+  if ((Lb >> 3) >= grp.per || wi >= grp.total) return;  // workgroup-uniform, before any barrier
+  int m = 0;
+#pragma unroll
+  for (int k = 1; k < NS; ++k)
+    if (k < grp.n && wi >= grp.s[k].g.w0) m = k;
+  const auto sg = pick_seg(grp.s, m);
+  const SepGeom& g = sg.g;
+  const int local = wi - g.w0;
+  const int b = local / g.ntiles, tile = local - b * g.ntiles;
+  const int ty = tile / g.tiles_x, tx = tile - ty * g.tiles_x;
+  const int tw = 1 << g.ltw;
+  const int iy0 = ty * g.th, ix0 = tx * tw;
+  const int rw = tw + 2;
+  const int npx = rw * (min(g.th, g.H - iy0) + 2);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int q = threadIdx.x & 15;
+
+  // ---- 1: pointwise kernel, taps, the gradient window through the GradX view ----
+  {
+    const float4* w4 = reinterpret_cast<const float4*>(grp.wp);
+#pragma unroll
+    for (int u = 0; u < C * (N / 4) / 256; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      const int r = e / (N / 4), qq = e - r * (N / 4);
+      *reinterpret_cast<float4*>(wpl + r * WPP + 4 * qq) = w4[e];
+    }
+    if (threadIdx.x < 9 * (C / 4)) {
+      const int t = threadIdx.x / (C / 4), qq = threadIdx.x - t * (C / 4);
+      *reinterpret_cast<float4*>(taps + t * kSepCC + 4 * qq) = *reinterpret_cast<const float4*>(grp.wd + t * C + 4 * qq);
+    }
+  }
+  {
+    StageGradX<YBF> src;
+    src.init(sg.gv, 4 * q);
+    constexpr int U = 6;
+    for (int p0 = threadIdx.x >> 4; p0 < npx; p0 += 16 * U) {
+      typename StageGradX<YBF>::Raw v[U];
+      bool ok[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + 16 * u;
+        const int wy = p / rw, wx = p - wy * rw;
+        const int iy = iy0 - 1 + wy, ix = ix0 - 1 + wx;
+        ok[u] = p < npx && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+        const int iyc = min(max(iy, 0), g.H - 1), ixc = min(max(ix, 0), g.W - 1);
+        v[u] = src.load((((long)b * g.H + iyc) * g.W + ixc) * N + 4 * q);
+      }
+      const int act = src.act();
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + 16 * u;
+        if (p < npx) {
+          float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok[u]) {
+            if (act == 1) o = src.template finish_t<1>(v[u]);
+            else if (act == 2) o = src.template finish_t<2>(v[u]);
+            else o = src.template finish_t<0>(v[u]);
+          }
+          *reinterpret_cast<float4*>(win + p * kSepWP + 4 * q) = o;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- 2: dd = g W^T over the window on the matrix cores (jobs: 32-pixel M tile x 32-channel half) ----
+  const int mtl = (npx + 31) / 32;
+  sep_f16v acc[3];
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) {
+    const int job = wave + 4 * jj;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[jj][e] = 0.f;
+    if (job >= 2 * mtl) continue;  // wave-uniform
+    const int mt = job >> 1, nt = job & 1;
+    const int pr = min(32 * mt + r32, kSepNPX - 1);  // (rows past the window read a valid pixel; not stored)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float4 fa = *reinterpret_cast<const float4*>(win + pr * kSepWP + 8 * s + 4 * h);
+      const float4 fb = *reinterpret_cast<const float4*>(wpl + (32 * nt + r32) * WPP + 8 * s + 4 * h);
+      acc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb.x, acc[jj], 0, 0, 0);
+      acc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb.y, acc[jj], 0, 0, 0);
+      acc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.z, fb.z, acc[jj], 0, 0, 0);
+      acc[jj] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.w, fb.w, acc[jj], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // every wave has read its g rows: the window now takes dd
+#pragma unroll
+  for (int jj = 0; jj < 3; ++jj) {
+    const int job = wave + 4 * jj;
+    if (job >= 2 * mtl) continue;
+    const int mt = job >> 1, nt = job & 1;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int p = 32 * mt + (e & 3) + 8 * (e >> 2) + 4 * h;
+      if (p < npx) win[p * kSepWP + 32 * nt + r32] = acc[jj][e];
+    }
+  }
+  __syncthreads();
+
+  // ---- 3: dx = the depthwise transpose of dd (k_dw_bwd's order), + GradSink sums ----
+  constexpr int RPT = 8;
+  const int col = (threadIdx.x >> 4) & (tw - 1);
+  const int rg = threadIdx.x >> (4 + g.ltw);
+  const int row0 = rg * RPT;
+  const int ix = ix0 + col;
+  const bool active = row0 < g.th && iy0 + row0 < g.H && ix < g.W;
+  const int c = 4 * q;
+  float4 a[RPT];
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) a[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (active) {
+    const float* base = win + (row0 * rw + col) * kSepWP + c;
+#pragma unroll
+    for (int ir = 0; ir < RPT + 2; ++ir) {
+#pragma unroll
+      for (int jj = 0; jj < 3; ++jj) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (ir * rw + jj) * kSepWP);
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+          const int ii = ir - r;
+          if (ii >= 0 && ii < 3) {
+            const float4 w = *reinterpret_cast<const float4*>(taps + ((2 - ii) * 3 + (2 - jj)) * kSepCC + c);
+            a[r].x = fmaf(v.x, w.x, a[r].x);
+            a[r].y = fmaf(v.y, w.y, a[r].y);
+            a[r].z = fmaf(v.z, w.z, a[r].z);
+            a[r].w = fmaf(v.w, w.w, a[r].w);
+          }
+        }
+      }
+    }
+  }
+  float4 s1 = make_float4(0.f, 0.f, 0.f, 0.f), s2 = s1;
+  GSChan4 kk;
+  if (GS && active) kk = gs_chan4(sg.gs, c);
+  float4 old[RPT], yv[RPT];
+  const int ixc = min(ix, g.W - 1);
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const long e = (((long)b * g.H + min(iy0 + row0 + r, g.H - 1)) * g.W + ixc) * C + c;
+    if (sg.acc) old[r] = *reinterpret_cast<const float4*>(sg.dx + e);
+    if constexpr (GS) yv[r] = ald4<YBF>(sg.gs.y, e);
+  }
+#pragma unroll
+  for (int r = 0; r < RPT; ++r) {
+    const int iy = iy0 + row0 + r;
+    if (!active || row0 + r >= g.th || iy >= g.H) continue;
+    const long e = (((long)b * g.H + iy) * g.W + ix) * C + c;
+    float4 v = a[r];
+    if (sg.acc) {
+      v.x += old[r].x; v.y += old[r].y; v.z += old[r].z; v.w += old[r].w;
+    }
+    *reinterpret_cast<float4*>(sg.dx + e) = v;
+    if constexpr (GS) gs_acc4(sg.gs, kk, v, yv[r], s1, s2);
+  }
+  if constexpr (GS) {
+    // lanes of one channel quad: 4 per wave (offsets 16, 32), then the 4 waves in order
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      s1.x += __shfl_xor(s1.x, o); s1.y += __shfl_xor(s1.y, o); s1.z += __shfl_xor(s1.z, o); s1.w += __shfl_xor(s1.w, o);
+      s2.x += __shfl_xor(s2.x, o); s2.y += __shfl_xor(s2.y, o); s2.z += __shfl_xor(s2.z, o); s2.w += __shfl_xor(s2.w, o);
+    }
+    if (lane < 16) {
+      gsl[(wave * 16 + q) * 2] = s1;
+      gsl[(wave * 16 + q) * 2 + 1] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x < 16) {
+      float4 t1 = gsl[q * 2], t2 = gsl[q * 2 + 1];
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float4 u = gsl[(w * 16 + q) * 2], v = gsl[(w * 16 + q) * 2 + 1];
+        t1.x += u.x; t1.y += u.y; t1.z += u.z; t1.w += u.w;
+        t2.x += v.x; t2.y += v.y; t2.z += v.z; t2.w += v.w;
+      }
+      const long p = (long)b * g.ntiles + tile;
+      gsink_put(sg.gs, p, c + 0, t1.x, t2.x);
+      gsink_put(sg.gs, p, c + 1, t1.y, t2.y);
+      gsink_put(sg.gs, p, c + 2, t1.z, t2.z);
+      gsink_put(sg.gs, p, c + 3, t1.w, t2.w);
+    }
+  }
+}
+
+template <int NS>
+void sep_bwd_go(const SepBwdGroup<NS>& grp, bool gs, bool ybf, hipStream_t s) {
+  const size_t lds = (size_t)SepBwdLds<64>::FLOATS * sizeof(float);
+  static_assert((size_t)SepBwdLds<64>::FLOATS * sizeof(float) <= 160 * 1024, "k_sep_bwd: LDS");
+  static const bool attr = [] {
+    const void* ks[] = {reinterpret_cast<const void*>(&k_sep_bwd<64, NS, true, false>),
+                        reinterpret_cast<const void*>(&k_sep_bwd<64, NS, false, false>),
+                        reinterpret_cast<const void*>(&k_sep_bwd<64, NS, true, true>),
+                        reinterpret_cast<const void*>(&k_sep_bwd<64, NS, false, true>)};
+    bool ok = true;
+    for (const void* k : ks)
+      ok = ok && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok;
+  }();
+  (void)attr;
+  const dim3 grid(8 * grp.per), block(256);
+  if (gs && ybf) hipLaunchKernelGGL((k_sep_bwd<64, NS, true, true>), grid, block, lds, s, grp);
+  else if (gs) hipLaunchKernelGGL((k_sep_bwd<64, NS, true, false>), grid, block, lds, s, grp);
+  else if (ybf) hipLaunchKernelGGL((k_sep_bwd<64, NS, false, true>), grid, block, lds, s, grp);
+  else hipLaunchKernelGGL((k_sep_bwd<64, NS, false, false>), grid, block, lds, s, grp);
+  PHX_LAUNCH_CHECK();
+}
+
 template <int NS, class XV>
 int sep_dispatch(SepGroup<NS, XV>& grp, int C, bool stats, hipStream_t s) {
   grp.per = cdiv(grp.total, 8);
@@ -456,6 +712,50 @@ void launch_sep_fwd(const SepMember* mem, int n, int B, int C, int N, const floa
     for (int i = 0; i < n; ++i) grp.s[i].x = mem[i].x;
     fill(grp);
     sep_dispatch(grp, C, stats, s);
+  }
+}
+
+bool sep_bwd_supported(int C, int N, bool bf16) { return !bf16 && C == 64 && N == 64; }
+
+void launch_sep_bwd(const SepBwdMember* mem, int n, int B, int C, int N, const float* wd, const float* wp,
+                    hipStream_t s, int* nps) {
+  if (n < 1 || n > kMaxSeg) throw std::invalid_argument("sep bwd: bad member count");
+  if (!sep_bwd_supported(C, N, false)) throw std::invalid_argument("sep bwd: unsupported shape");
+  const bool gs = mem[0].gs.part != nullptr;
+  const bool ybf = (mem[0].gv.y && mem[0].gv.ybf) || (gs && mem[0].gs.ybf);
+  for (int i = 0; i < n; ++i) {
+    if ((mem[i].gs.part != nullptr) != gs) throw std::invalid_argument("sep bwd: members differ in sinks");
+    if (mem[i].H <= 0 || mem[i].W <= 0) throw std::invalid_argument("sep bwd: empty member");
+  }
+  auto fill = [&](auto& grp) {
+    grp.wd = wd;
+    grp.wp = wp;
+    grp.n = n;
+    grp.B = B;
+    int w0 = 0;
+    for (int i = 0; i < n; ++i) {
+      auto& sg = grp.s[i];
+      sg.gv = mem[i].gv;
+      sg.dx = mem[i].dx;
+      sg.g = sep_geom(mem[i].H, mem[i].W, w0);
+      sg.acc = mem[i].acc ? 1 : 0;
+      sg.gs = mem[i].gs;
+      sg.gs.C = C;
+      sg.gs.P = B * sg.g.ntiles;
+      if (nps) nps[i] = sg.gs.P;
+      w0 += B * sg.g.ntiles;
+    }
+    grp.total = w0;
+    grp.per = cdiv(w0, 8);
+  };
+  if (n == 1) {
+    SepBwdGroup<1> grp{};
+    fill(grp);
+    sep_bwd_go(grp, gs, ybf, s);
+  } else {
+    SepBwdGroup<kMaxSeg> grp{};
+    fill(grp);
+    sep_bwd_go(grp, gs, ybf, s);
   }
 }
 

@@ -3,15 +3,15 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 tag=${1:-sep}
-timeout -k 10 600 python -u -m pytest tests/test_gpu_sep.py tests/test_gpu_parity.py -x -q -m gpu \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_sep.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -q -m gpu \
   -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/${tag}_tests.log; grep -E "^FAILED|^ERROR|Error|assert" gpurun_out/${tag}_tests.log | head -20
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 timeout -k 10 300 python tools/shape_prof.py --top 90 > gpurun_out/${tag}_shapes.txt 2>&1 || exit 3
-grep sep_fwd gpurun_out/${tag}_shapes.txt
+grep sep_ gpurun_out/${tag}_shapes.txt
 for r in 1 2; do
-  for x in 1 0 p; do
-    if [ $x = p ]; then export PHX_SEP=1 PHX_SEP_MINROWS=0; else export PHX_SEP=$x; unset PHX_SEP_MINROWS; fi; timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary > gpurun_out/${tag}_b$x.json 2> gpurun_out/${tag}_b$x.err || exit 3
+  for x in 1 0 b; do
+    if [ $x = b ]; then export PHX_SEP=1 PHX_SEPB=0; else export PHX_SEP=$x; unset PHX_SEPB; fi; timeout -k 10 200 python bench.py --no-cpu-baseline --no-secondary > gpurun_out/${tag}_b$x.json 2> gpurun_out/${tag}_b$x.err || exit 3
     echo "round $r PHX_SEP=$x: $(python -c "import json;d=json.load(open('gpurun_out/${tag}_b$x.json'));print(d['ms_per_step'], d['value'], d['roofline']['kernel'], d['roofline']['avg_us'], d['roofline']['frac'])")"
   done
 done

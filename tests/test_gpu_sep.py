@@ -20,20 +20,41 @@ from bench import synth_boxes, synth_images
 pytestmark = pytest.mark.gpu
 
 
-def _victim(monkeypatch, sep, model="efficientdet-d0", S=256, B=2, bn_mode="local"):
-    """PHX_SEP_MINROWS=0: every 3x3 sepconv fused, whatever its level's size (the default fuses the
-    levels with >= 32768 rows only, where the fused launch is faster: the C2 bench's P3 convs and head
-    groups, which the C2 oracle tests run)."""
+def _victim(monkeypatch, sep, model="efficientdet-d0", S=256, B=2, bn_mode="local", all_levels=True):
+    """all_levels: PHX_SEP_MINROWS=0, every 3x3 sepconv fused whatever its level's size (the default
+    fuses the levels with >= 32768 rows only, where the fused launch is faster: the C2 bench's P3
+    convs and head groups, which the C2 oracle tests run)."""
     from mladversarialobjectdetection_amd.attacker import EfficientDetVictim
     monkeypatch.setenv("PHX_SEP", sep)
-    monkeypatch.setenv("PHX_SEP_MINROWS", "0")
+    if all_levels:
+        monkeypatch.setenv("PHX_SEP_MINROWS", "0")
+    else:
+        monkeypatch.delenv("PHX_SEP_MINROWS", raising=False)
     return EfficientDetVictim(model, "synthetic", seed=0, image_size=S, max_batch=B, rng_seed=5, bn_mode=bn_mode)
 
 
+def test_sep_inference_bit_identical_c2(monkeypatch):
+    """bn=frozen, C2 shapes (D0 512^2, 16 images) at the default fusion policy: every anchor's score,
+    class and box equals the two-launch path's bit for bit (the fused P3 convs replace k_gemm2 / grouped
+    GEMMs, whose k order the fused kernel keeps)."""
+    imgs = torch.as_tensor(synth_images(list(range(16)), 512)).cuda()
+    out = []
+    for sep in ("1", "0"):
+        v = _victim(monkeypatch, sep, S=512, B=16, bn_mode="frozen", all_levels=False)
+        b, sc, c = v.detect(imgs)
+        torch.cuda.synchronize()
+        out.append((b.cpu().numpy(), sc.cpu().numpy(), c.cpu().numpy()))
+        del v
+    (b1, s1, c1), (b0, s0, c0) = out
+    assert np.isfinite(s1).all()
+    assert np.array_equal(s1, s0) and np.array_equal(c1, c0) and np.array_equal(b1, b0)
+
+
 @pytest.mark.parametrize("model,S", [("efficientdet-d0", 256), ("efficientdet-lite0", 320)])
-def test_sep_inference_bit_identical(monkeypatch, model, S):
-    """bn=frozen: scores, classes and boxes of every anchor equal the two-launch path's bit for bit
-    (D0: swish; lite0: relu6 and BiFPN 'sum' fuse)."""
+def test_sep_all_levels_inference_close(monkeypatch, model, S):
+    """bn=frozen, every level fused (D0: swish; lite0: relu6 and the BiFPN 'sum' fuse): the small
+    levels' unfused GEMMs split K across waves (another fp32 summation order), so scores agree to
+    rounding: |d| <= 1e-5 (the oracle tests hold scores to 2e-5), classes >= 99.9 %, boxes rel 1e-5."""
     imgs = torch.as_tensor(synth_images([0, 1], S)).cuda()
     out = []
     for sep in ("1", "0"):
@@ -43,30 +64,34 @@ def test_sep_inference_bit_identical(monkeypatch, model, S):
         out.append((b.cpu().numpy(), sc.cpu().numpy(), c.cpu().numpy()))
     (b1, s1, c1), (b0, s0, c0) = out
     assert np.isfinite(s1).all()
-    assert np.array_equal(s1, s0) and np.array_equal(c1, c0) and np.array_equal(b1, b0)
+    assert np.abs(s1 - s0).max() <= 1e-5
+    assert (c1 == c0).mean() >= 0.999
+    assert np.linalg.norm(b1 - b0) / np.linalg.norm(b0) <= 1e-5
 
 
-def test_sep_first_output_bit_identical_and_step_close(monkeypatch):
-    """Training step, D0 512^2, 4 images: the first BiFPN sepconv's output (the BN input of
-    fnode0, reached through unchanged ops) is bit-identical to the two-launch path; the step's loss,
-    d scale and d patch agree within the oracle tests' bounds (loss 1e-5, cosine 0.99999)."""
+def test_sep_first_p3_output_bit_identical_and_step_close(monkeypatch):
+    """Training step, C2 shapes (D0 512^2, 16 images) at the default policy: the first fused BiFPN
+    sepconv (the P3 node fnode3, whose inputs come through unfused ops) gives its BN bit-identical
+    inputs; the step's loss, d scale and d patch agree with the two-launch step within the oracle
+    tests' bounds (loss 1e-5, cosine 0.99999, rel 1e-3)."""
     from mladversarialobjectdetection_amd import _lib
     from mladversarialobjectdetection_amd.attacker import PatchAttacker
-    B, S = 4, 512
+    B, S = 16, 512
     imgs = torch.as_tensor(synth_images(list(range(B)), S)).cuda()
     boxes = synth_boxes(list(range(B)), S)
-    name = b"fpn_cells/cell_0/fnode0/op_after_combine5/bn"
+    name = b"fpn_cells/cell_0/fnode3/op_after_combine8/bn"
     res = []
     for sep in ("1", "0"):
-        v = _victim(monkeypatch, sep, S=S, B=B)
+        v = _victim(monkeypatch, sep, S=S, B=B, all_levels=False)
         att = PatchAttacker(v, seed=7)
         att.cur_step = 2
         att.call(imgs, boxes=boxes)
-        n = B * (S // 64) * (S // 64) * 64
+        n = B * (S // 8) * (S // 8) * 64
         t = torch.empty(n, device="cuda")
         v.ctx.call("phx_debug_tap", name, 0, t.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         res.append((att.grad.cpu().numpy().astype(np.float64), att.metrics_buf.cpu().numpy(), t.cpu().numpy()))
+        del att, v
     (g1, m1, t1), (g0, m0, t0) = res
     assert np.array_equal(t1, t0)
     assert abs(m1[_lib.M_LOSS] - m0[_lib.M_LOSS]) <= 1e-5 * abs(m0[_lib.M_LOSS])
@@ -89,3 +114,41 @@ def test_sep_depthwise_output_not_stored(monkeypatch):
     with pytest.raises(_lib.PhxError, match="never stored"):
         v.ctx.call("phx_debug_tap", b"fpn_cells/cell_0/fnode0/op_after_combine5/conv/depthwise_kernel", 0,
                    t.data_ptr(), n, torch.cuda.current_stream().cuda_stream)
+
+
+def test_sep_backward_first_dx_bit_identical_and_step_close(monkeypatch):
+    """The fused backward (pointwise dgrad + depthwise transpose in one launch, PHX_SEPB) against the
+    two launches: the first fused sepconv of the reverse sweep (the class head's last repeat, all five
+    levels) sees the same inputs, so its depthwise-input gradient (of class-1-bn-3 .. -7's outputs) is
+    bit-identical; the BN-backward sums it feeds are reduced per tile (another order), so the step's
+    d patch agrees within the oracle tests' bounds."""
+    from mladversarialobjectdetection_amd import _lib
+    from mladversarialobjectdetection_amd.attacker import PatchAttacker
+    B, S = 2, 256
+    imgs = torch.as_tensor(synth_images(list(range(B)), S)).cuda()
+    boxes = synth_boxes(list(range(B)), S)
+    res = []
+    for sepb in ("1", "0"):
+        monkeypatch.setenv("PHX_SEPB", sepb)
+        v = _victim(monkeypatch, "1", S=S, B=B)
+        att = PatchAttacker(v, seed=7)
+        att.cur_step = 2
+        att.call(imgs, boxes=boxes)
+        taps = []
+        for lev in range(3, 8):  # the sparse loss gradient reaches the levels holding the max anchors
+            n = B * (S >> lev) * (S >> lev) * 64
+            t = torch.empty(n, device="cuda")
+            v.ctx.call("phx_debug_tap", f"class_net/class-1-bn-{lev}".encode(), 1, t.data_ptr(), n,
+                       torch.cuda.current_stream().cuda_stream)
+            taps.append(t)
+        torch.cuda.synchronize()
+        res.append((att.grad.cpu().numpy().astype(np.float64), att.metrics_buf.cpu().numpy(),
+                    np.concatenate([t.cpu().numpy() for t in taps])))
+    (g1, m1, t1), (g0, m0, t0) = res
+    assert np.abs(t0).sum() > 0
+    assert np.array_equal(t1, t0)
+    assert m1[_lib.M_LOSS] == m0[_lib.M_LOSS]  # (the forward is the same launches)
+    a, b = g1[:-1], g0[:-1]
+    assert a @ b / (np.linalg.norm(a) * np.linalg.norm(b)) >= 0.99999
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) <= 1e-3
+    assert abs(g1[-1] - g0[-1]) <= 1e-5 * max(1.0, abs(g0[-1]))
