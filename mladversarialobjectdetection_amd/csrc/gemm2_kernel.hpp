@@ -261,6 +261,25 @@ __device__ __forceinline__ void g2_store(const G2Regs<WM, TM, TN, MODE, BF>& r, 
   else g2_store_act<WM, TM, TN, MODE, BF, 0>(r, a, sm, buf, m0, n0, k0, kend);
 }
 
+// every staging register of r used here (an empty asm reading it), so the loads that fill them are
+// waited for at this point on every control path
+template <int WM, int TM, int TN, int MODE, bool BF>
+__device__ __forceinline__ void g2_consume(const G2Regs<WM, TM, TN, MODE, BF>& r) {
+  using P = G2<WM, TM, TN, MODE, BF>;
+#pragma unroll
+  for (int u = 0; u < P::NA; ++u) asm volatile("" ::"v"(r.a[u].x), "v"(r.a[u].y), "v"(r.a[u].z), "v"(r.a[u].w));
+#pragma unroll
+  for (int u = 0; u < P::NB; ++u) asm volatile("" ::"v"(r.b[u].x), "v"(r.b[u].y), "v"(r.b[u].z), "v"(r.b[u].w));
+  if constexpr (MODE == 3) {
+#pragma unroll
+    for (int u = 0; u < P::NA; ++u) asm volatile("" ::"v"(r.y[u].x), "v"(r.y[u].y), "v"(r.y[u].z), "v"(r.y[u].w));
+  }
+  if constexpr (MODE == 2) {
+#pragma unroll
+    for (int u = 0; u < P::NA; ++u) asm volatile("" ::"v"(r.rs[u].x), "v"(r.rs[u].y), "v"(r.rs[u].z), "v"(r.rs[u].w));
+  }
+}
+
 // SK: 0 plain, 1 StatSink (BN statistics of C), 2 GradSink (BN-backward sums of a dgrad's C)
 #ifndef PHX_GEMM_PF2
 #define PHX_GEMM_PF2 0
@@ -393,6 +412,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             }
         }
       }
+      // The next chunk goes into the other LDS buffer before this tile's epilogue: its loads are then
+      // the youngest memory operations when their wait is issued (the epilogue's stores come after it,
+      // so the wait does not wait for them — in-order vmcnt), and every staging register is consumed
+      // on every path, so the loop head needs no wait either (before, the compiler's conservative
+      // counts made each tile wait for its own epilogue stores at the next chunk).
+      if (h1) {
+        g2_store<WM, TM, TN, MODE, BF>(PF2 ? S : L, a, sm, buf ^ 1, t1 * BM, n0, kbeg + k1 * BK, kend);
+        g2_consume(PF2 ? S : L);
+      }
       if (kc == ksteps - 1) {
         // ---- epilogue of `tile` ----
         // In the 32x32 C/D layout lane (r32, h) holds column r32, rows (e&3) + 8*(e>>2) + 4*h.
@@ -519,7 +547,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
       }
       if (!h1) return false;
-      g2_store<WM, TM, TN, MODE, BF>(PF2 ? S : L, a, sm, buf ^ 1, t1 * BM, n0, kbeg + k1 * BK, kend);
       __syncthreads();
       buf ^= 1;
       tile = t1;
