@@ -1709,14 +1709,23 @@ void run_backward(phx_ctx* ctx, Exec& E, const float* input, hipStream_t s) {
     }
   }
   std::sort(zero.begin(), zero.end());
+  std::vector<char*> zp;
+  std::vector<size_t> zb;
   for (size_t i = 0; i < zero.size();) {
     char* p0 = zero[i].first;
     char* p1 = p0 + zero[i].second;
     size_t j = i + 1;
     for (; j < zero.size() && zero[j].first <= p1; ++j) p1 = std::max(p1, zero[j].first + zero[j].second);
-    PHX_HIP(hipMemsetAsync(p0, 0, (size_t)(p1 - p0), s));
+    zp.push_back(p0);
+    zb.push_back((size_t)(p1 - p0));
     i = j;
   }
+  // one launch for all of them (was one memset packet per level)
+  bool aligned = zp.size() <= (size_t)kZeroSegs;
+  for (size_t k = 0; k < zp.size(); ++k) aligned = aligned && ((reinterpret_cast<uintptr_t>(zp[k]) | zb[k]) & 15) == 0;
+  if (aligned) launch_zero_segs(zp.data(), zb.data(), (int)zp.size(), s);
+  else
+    for (size_t k = 0; k < zp.size(); ++k) PHX_HIP(hipMemsetAsync(zp[k], 0, zb[k], s));
   launch_cls_scatter(E.scores, E.keep, E.mraw, E.nties, E.dm, E.tptr(P.cls_out[0], input),
                      E.lev_dev, (int)E.lev.size(), ctx->A, E.B, ctx->mc.num_classes, na,
                      W + wpred, K, E.grad, E.dxoff_dev, s, E.tbf(P.cls_out[0]));
@@ -2466,7 +2475,12 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
                        ctx->pre.step == step && ctx->pre.gimg0 == gimg0;
   ctx->pre_join(s);
   ctx->pre.pending = false;
-  PHX_HIP(hipMemsetAsync(metrics, 0, PHX_NMETRIC * sizeof(float), s));
+  if (inject && !count) throw std::invalid_argument("boxes without count");
+  if (inject && maxb > PHX_MAX_OUT) throw std::out_of_range("maxb > 100");
+  // the metric row zeroed and the caller's boxes staged in one launch (16-B aligned boxes)
+  const bool inject_k = inject && (reinterpret_cast<uintptr_t>(boxes) & 15) == 0;
+  launch_step_prologue(metrics, PHX_NMETRIC, inject_k ? boxes : nullptr, count, B, maxb, E.inj_boxes,
+                       E.inj_count, s);
   ck_begin(E, s);
   // Injected placement: the first pass only feeds the ASR denominator (and the moving statistics),
   // so it runs on a second stream beside the second pass and the backward, on its own executor
@@ -2553,10 +2567,7 @@ int phx_step_grad(phx_ctx* ctx, const float* images, int B, const float* boxes,
     run_nms(ctx, E, 2, E.nms1_boxes, E.nms1_scores, E.nms1_count, s);
     launch_count_ge(E.nms1_scores, E.nms1_count, B, PHX_MAX_OUT, 0.5f, metrics + PHX_M_ASR_DEN, s);
   }
-  if (inject) {
-    if (!count) throw std::invalid_argument("boxes without count");
-    stage_boxes(E, boxes, count, B, maxb, s);  // injected placement boxes
-  }
+  if (inject && !inject_k) stage_boxes(E, boxes, count, B, maxb, s);  // (unaligned caller boxes)
   // 2. EOT paste
   eot_forward(ctx, E, images, B, inject ? E.inj_boxes : Efp->nms1_boxes,
               inject ? E.inj_count : Efp->nms1_count, params, step, gimg0, s);

@@ -1269,4 +1269,73 @@ void launch_count_ge(const float* sc, const int* cnt, int B, int maxo, float th,
   PHX_LAUNCH_CHECK();
 }
 
+// ---- launch merges: buffer zeroing and the step prologue (each replaced several memset / copy
+// packets of ~5 us apiece on the step's stream) ----
+struct ZeroSegs {
+  float4* p[kZeroSegs];
+  long n4[kZeroSegs];  // float4 count
+  long off[kZeroSegs + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void k_zero_segs(ZeroSegs z) {
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < z.off[z.n]; i += stride) {
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < kZeroSegs; ++j)
+      if (j < z.n && i >= z.off[j]) k = j;
+    float4* p = z.p[0];
+    long o = z.off[0];
+#pragma unroll
+    for (int j = 1; j < kZeroSegs; ++j)
+      if (j == k) {
+        p = z.p[j];
+        o = z.off[j];
+      }
+    p[i - o] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+void launch_zero_segs(char* const* ptr, const size_t* bytes, int n, hipStream_t s) {
+  if (n <= 0) return;
+  if (n > kZeroSegs) throw std::invalid_argument("zero_segs: too many buffers");
+  ZeroSegs z{};
+  z.n = n;
+  z.off[0] = 0;
+  for (int k = 0; k < n; ++k) {
+    if ((reinterpret_cast<uintptr_t>(ptr[k]) | bytes[k]) & 15) throw std::invalid_argument("zero_segs: alignment");
+    z.p[k] = reinterpret_cast<float4*>(ptr[k]);
+    z.n4[k] = (long)(bytes[k] / 16);
+    z.off[k + 1] = z.off[k] + z.n4[k];
+  }
+  const long blocks = std::min<long>(cdiv(z.off[n], 256L), 4096L);
+  hipLaunchKernelGGL(k_zero_segs, dim3((unsigned)std::max<long>(blocks, 1)), dim3(256), 0, s, z);
+  PHX_LAUNCH_CHECK();
+}
+
+__global__ __launch_bounds__(256) void k_step_prologue(float* metrics, int nmetric, const float4* boxes,
+                                                       const int32_t* count, int B, int maxb, float4* inj_boxes,
+                                                       int* inj_count) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < nmetric) metrics[i] = 0.f;
+  if (!boxes) return;
+  if (i < B * PHX_MAX_OUT_DEV) {
+    const int b = i / PHX_MAX_OUT_DEV, j = i - b * PHX_MAX_OUT_DEV;
+    inj_boxes[i] = j < maxb ? boxes[(long)b * maxb + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  if (i < B) inj_count[i] = count[i];
+}
+
+void launch_step_prologue(float* metrics, int nmetric, const float* boxes, const int32_t* count, int B, int maxb,
+                          float* inj_boxes, int* inj_count, hipStream_t s) {
+  if (boxes && (maxb < 0 || maxb > PHX_MAX_OUT_DEV)) throw std::out_of_range("maxb > 100");
+  if (boxes && (reinterpret_cast<uintptr_t>(boxes) & 15)) throw std::invalid_argument("boxes: 16-B alignment");
+  const int n = std::max(nmetric, boxes ? B * PHX_MAX_OUT_DEV : 0);
+  hipLaunchKernelGGL(k_step_prologue, dim3(cdiv(n, 256)), dim3(256), 0, s, metrics, nmetric,
+                     reinterpret_cast<const float4*>(boxes), count, B, maxb, reinterpret_cast<float4*>(inj_boxes),
+                     inj_count);
+  PHX_LAUNCH_CHECK();
+}
+
 }  // namespace phx

@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256, 2) void k_sep_fwd(SepGroup<NS, XV> grp) {
     }
     SEP_STAMP(6);
   }
-  if constexpr (STATS) {  // (N <= 64: one part)
+  if constexpr (STATS) {  // (each part its own columns of the partial row)
     if (lane == 0) wcn[wave] = nw;
     __syncthreads();
     SEP_STAMP(7);
@@ -338,8 +338,8 @@ __global__ __launch_bounds__(256, 2) void k_sep_fwd(SepGroup<NS, XV> grp) {
         const float2 v = wst[w * kSepNC + threadIdx.x];
         chan_merge(tn, tm, t2, wcn[w], v.x, v.y);
       }
-      sink_put(sg.sink, bgidx, threadIdx.x, tn, tm, t2);
-      if (threadIdx.x == 0) sink_cnt(sg.sink, bgidx, tn);
+      sink_put(sg.sink, bgidx, n0 + threadIdx.x, tn, tm, t2);
+      if (threadIdx.x == 0 && part == 0) sink_cnt(sg.sink, bgidx, tn);
     }
   }
   SEP_STAMP(8);
@@ -631,11 +631,13 @@ void sep_bwd_go(const SepBwdGroup<NS>& grp, bool gs, bool ybf, hipStream_t s) {
   PHX_LAUNCH_CHECK();
 }
 
-// N <= 64: one part of two tiles (the consumer BN's statistics need every column of a row in one
-// workgroup; wider outputs are not planned, see sep_supported)
+// N <= 64: one part of two 32-column tiles (each part writes its own columns of the statistics
+// partial row; wider outputs are not planned, see sep_supported)
 template <int NS, class XV>
 int sep_dispatch(SepGroup<NS, XV>& grp, int C, bool stats, hipStream_t s) {
   if (C != 64 || grp.N > 64) throw std::invalid_argument("sep: unsupported shape");
+  // (one 32-column part per workgroup — twice the workgroups, the depthwise pass repeated — measured
+  // slower: P3 19.3 -> 25.7 us, C2 +0.15 ms; scripts/gpu_r06_seppt.sh)
   constexpr int pt = 2;
   grp.np = cdiv(grp.N, 32 * pt);
   const int total = grp.total;

@@ -24,6 +24,13 @@ void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* m
                         hipStream_t s, bool bf = false);  // bf: cls_base holds bf16 logits
 void launch_count_ge(const float* sc, const int* cnt, int B, int maxo, float th, float* out,
                      hipStream_t s);
+// zero up to kZeroSegs buffers (16-B aligned, sizes multiples of 16 B) in one launch
+constexpr int kZeroSegs = 8;
+void launch_zero_segs(char* const* ptr, const size_t* bytes, int n, hipStream_t s);
+// the step's prologue in one launch: the metric row zeroed and, with caller boxes ([B,maxb,4],
+// count [B]), the injected-placement slots [B,100,4] (slots past maxb zero) and counts staged
+void launch_step_prologue(float* metrics, int nmetric, const float* boxes, const int32_t* count, int B, int maxb,
+                          float* inj_boxes, int* inj_count, hipStream_t s);
 
 // ---- EOT (kernels_eot.hip) ------------------------------------------------------------------
 struct BoxPlace {

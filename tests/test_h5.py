@@ -144,3 +144,78 @@ def test_antipatch_reader_matches_scoped_names_and_checks():
     bad = [(ln, [(w, a.reshape(-1) if i == 0 else a) for i, (w, a) in enumerate(ws)]) for ln, ws in layers]
     with pytest.raises(ValueError, match="shape"):
         from_keras_weight_layers(man, bad)
+
+
+def _keras_weights_order(nf=8):
+    """Layer.weights of PatchNeutralizer's top-level layers as Keras orders them, restated from
+    generator.py independently of the product's manifest: a layer's weights are its trainable
+    variables, own first and then its tracked sublayers' in attribute-assignment order (depth first),
+    followed by the non-trainable ones in the same order (BatchNormalization: gamma, beta trainable;
+    moving_mean, moving_variance not).  Sublayers in __init__ order:
+      Conv2DBlock            l1 cnv1, l2 bn1, l4 cnv2, l5 bn2            (generator.py:167-176)
+      AttentionBlock         l1 cnv1, l2 bn1, l3 cnv2, l4 bn2, l7 conv3, l8 bn3   (:110-121)
+      Conv2DTransposeBlock   l1 cnv, att attention, l3 convblock          (:228-236)
+      PatchNeutralizer       conv_blocks conv0..3, conv_no_skip conv4, deconv_blocks deconv0..3
+                             (:30-41), op output (:81)."""
+    def conv(n):
+        return ("conv", n)
+
+    def bn(n):
+        return ("bn", n)
+
+    def block(p):
+        return [conv(f"{p}/cnv1"), bn(f"{p}/bn1"), conv(f"{p}/cnv2"), bn(f"{p}/bn2")]
+
+    def att(p):
+        return [conv(f"{p}/cnv1"), bn(f"{p}/bn1"), conv(f"{p}/cnv2"), bn(f"{p}/bn2"), conv(f"{p}/conv3"),
+                bn(f"{p}/bn3")]
+
+    tops = [(f"conv{i}", block(f"conv{i}")) for i in range(5)]
+    tops += [(f"deconv{i}", [conv(f"deconv{i}/cnv")] + att(f"deconv{i}/attention") + block(f"deconv{i}/convblock"))
+             for i in range(4)]
+    tops.append((f"{KERAS_MODEL}/output", [conv(f"{KERAS_MODEL}/output")]))
+    out = []
+    for name, subs in tops:
+        tr = [f"{n}/{w}:0" for k, n in subs for w in (("kernel", "bias") if k == "conv" else ("gamma", "beta"))]
+        nt = [f"{n}/{w}:0" for k, n in subs if k == "bn" for w in ("moving_mean", "moving_variance")]
+        out.append((name, tr + nt))
+    return out
+
+
+def test_antipatch_positional_order_matches_keras(tmp_path):
+    """Keras's load_weights assigns an HDF5 layer's datasets to layer.weights by POSITION (its
+    weight_names attribute order), not by name.  The file the defender writes must list every layer's
+    weights in the order Keras builds them (restated above from generator.py), and the i-th dataset
+    must hold the product variable that Keras weight i names — read positionally, not through this
+    module's name-matching reader."""
+    man = _manifest()
+    rng = np.random.default_rng(2)
+    params = rng.standard_normal(man["n_params"]).astype(np.float32)
+    moving = rng.standard_normal(man["n_moving"]).astype(np.float32)
+    layers = keras_weight_layers(man, params, moving)
+    want = _keras_weights_order()
+    assert [n for n, _ in layers] == [n for n, _ in want]
+    for (ln, ws), (_, names) in zip(layers, want):
+        assert [w for w, _ in ws] == names, ln
+    p = tmp_path / "antipatch.h5"
+    h5.write_keras_weights(p, layers)
+    f = h5.H5File(p)
+    assert [n.decode() for n in f.attrs("/")["layer_names"]] == [n for n, _ in want]
+    by_param = {e["name"]: e for e in man["params"]}
+    by_bn = {e["name"]: e for e in man["bn"]}
+    for ln, names in want:
+        pos = [w.decode() for w in f.attrs(ln)["weight_names"]]
+        assert pos == names, ln
+        for w in pos:
+            v = w[:-2]
+            if v.startswith(KERAS_MODEL + "/"):
+                v = v[len(KERAS_MODEL) + 1:]
+            arr = np.asarray(f.dataset(f"{ln}/{w}"))
+            if v.endswith(("/moving_mean", "/moving_variance")):
+                b, kind = v.rsplit("/", 1)
+                e = by_bn[b]
+                ref = moving[e[kind]:e[kind] + e["channels"]]
+            else:
+                e = by_param[v]
+                ref = params[e["offset"]:e["offset"] + int(np.prod(e["shape"]))].reshape(e["shape"])
+            np.testing.assert_array_equal(arr, ref, err_msg=w)
