@@ -149,12 +149,14 @@ Gemm2Plan plan_gemm2(int M, int N, int K, int target_wgs, bool bf16, bool allow_
     const char* e = std::getenv("PHX_GEMM_WSK");
     return !(e && e[0] == '0');
   }();
-  // PHX_GEMM_WSK_BF16=1: the bf16 compute type takes k_gemm2k too (default off: C4 28.25 -> 28.07 ms,
-  // gradient unchanged against the oracle, but the D4 256^2 step's loss lands 4.9e-3 from fp64
-  // against 5e-5 with the split kernels, outside test_gpu_bf16's emulation bound)
+  // the bf16 compute type takes k_gemm2k too (C4 27.80 -> 27.52-27.59 ms; PHX_GEMM_WSK_BF16=0 keeps the
+  // split).  Its first affected layer differs from the split kernels' in 8e-5 of the stored bf16
+  // values, each by one quantum (fp32 summation order); deeper, both builds are draws of the same
+  // bf16 storage noise, equally far from the emulation oracle ("bf16 wave-split-K,
+  // diagnosed"; scripts/diag_bf16_wsk_layers.py)
   static const bool wsk_bf16 = [] {
     const char* e = std::getenv("PHX_GEMM_WSK_BF16");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   // bf16: the A view (fp32 VALU, once per N tile) outweighs the cheap bf16 MFMAs, so a split tile that
   // spans all of N exactly (one view pass: N = 160 on 128x160) stays faster than the narrower

@@ -5,9 +5,9 @@ cross-workgroup split (k_gemm2 + reduce) to the wave-split-K kernel (k_gemm2k, P
     python scripts/diag_bf16_wsk_layers.py          (parent: CPU only; each plan runs in a child)
 
 Runs, each in its own process (the plan switches are read once per process):
-  A  default plan (bf16 deep-K GEMMs split across workgroups)
-  B  PHX_GEMM_WSK_BF16=1 (split across the waves of one workgroup instead)
-  C  the default plan again (run-to-run determinism)
+  A  PHX_GEMM_WSK_BF16=0 (bf16 deep-K GEMMs split across workgroups: the round-5 default)
+  B  PHX_GEMM_WSK_BF16=1 (split across the waves of one workgroup instead: the default since round 6)
+  C  A again (run-to-run determinism)
 and, in the parent, the fp64 oracle with the product's bf16 rounding points (Bf16Conv1x1 /
 Bf16Store) and the plain fp64 oracle.  Per batch norm (its input = the stored conv output, forward
 order) it prints the fraction of elements where runs A and B differ, the largest difference in bf16
@@ -106,7 +106,7 @@ def _rel(a, b):
 def main():
     os.makedirs("/tmp", exist_ok=True)
     env0 = {k: v for k, v in os.environ.items() if not k.startswith("PHX_")}
-    runs = {"A": {}, "B": {"PHX_GEMM_WSK_BF16": "1"}, "C": {}}
+    runs = {"A": {"PHX_GEMM_WSK_BF16": "0"}, "B": {"PHX_GEMM_WSK_BF16": "1"}, "C": {"PHX_GEMM_WSK_BF16": "0"}}
 
     def run(tag, extra):
         r = subprocess.run([sys.executable, __file__, "child", tag], env={**env0, **extra}, timeout=600)
