@@ -101,6 +101,8 @@ KIND_KERNELS = {
     "bn_bwd_reduce": "k_bn_finalize<true,BwdEpi2,NS> (BN-backward sums from the consumer's dgrad)",
     "dw_fwd": "k_dw_fwd<K,S,RPT,STATS,NS>",
     "dw_bwd": "k_dw_bwd<K,S,RPT,GS,NS>",
+    "sep_fwd": "k_sep_fwd<C,NS,XV,STATS,PT> (depthwise 3x3 -> pointwise MFMA + bias + BN statistics, one launch)",
+    "sep_bwd": "k_sep_bwd<C,NS,GS,YBF> (pointwise dgrad on MFMA over the window + depthwise transpose)",
 }
 
 

@@ -19,6 +19,7 @@ KINDS = [  # (kind, substring, primary?) — first match wins
     ("gemm", "k_gemm_splitk_reduce", False), ("gemm", "k_gemm2<", True), ("gemm", "k_gemm2r<", True),
     ("gemm", "k_gemm2k<", True), ("gemm", "k_gemm<", True),
     ("dw_fwd", "k_dw_fwd<", True), ("dw_bwd", "k_dw_bwd<", True),
+    ("sep_fwd", "k_sep_fwd<", True), ("sep_bwd", "k_sep_bwd<", True),
     ("bn_stats", "k_bn_finalize<false", True),
     ("bn_stats", "k_colred_part<phx::StatsAcc", True), ("bn_stats", "k_colred_final<phx::StatsEpi>", False),
     ("bn_bwd_reduce", "k_bn_finalize<true", True),
