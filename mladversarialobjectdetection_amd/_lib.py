@@ -207,8 +207,11 @@ class Context:
     def profile_report(self) -> dict:
         need = c_size_t()
         check(self.h, self.lib.phx_profile_report(self.h, None, 0, ctypes.byref(need)), "phx_profile_report")
-        buf = ctypes.create_string_buffer(need.value)
-        check(self.h, self.lib.phx_profile_report(self.h, buf, need.value, ctypes.byref(need)), "phx_profile_report")
+        cap = need.value
+        buf = ctypes.create_string_buffer(cap)
+        check(self.h, self.lib.phx_profile_report(self.h, buf, cap, ctypes.byref(need)), "phx_profile_report")
+        if need.value > cap:  # (a library without the size-query cache: the report grew)
+            raise PhxError(f"phx_profile_report: {need.value} bytes needed, {cap} given")
         return json.loads(buf.value.decode())
 
     def workspace_bytes(self, batch: int) -> int:

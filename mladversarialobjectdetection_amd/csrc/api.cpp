@@ -227,6 +227,7 @@ struct Prof {
   };
   bool on = false;
   std::vector<Rec> recs;
+  std::string report;  // the report a size query (buf == NULL) built: the copy call returns it verbatim
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   hipEvent_t ev() {
@@ -2722,6 +2723,17 @@ int phx_profile(phx_ctx* ctx, int enable) {
 int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   if (!ctx) return PHX_EINVAL;
   PHX_TRY(ctx)
+  // the copy call after a size query returns the string that query measured (rebuilding it could
+  // print a timing differently and no longer fit the caller's buffer)
+  if (buf && cap && !ctx->prof.report.empty()) {
+    const std::string out = std::move(ctx->prof.report);
+    ctx->prof.report.clear();
+    if (needed) *needed = out.size() + 1;
+    const size_t c = std::min(cap - 1, out.size());
+    memcpy(buf, out.data(), c);
+    buf[c] = 0;
+    return PHX_OK;
+  }
   // per launch group: measured time and the roofline time of its algorithmic work at the MI355X
   // peaks (HBM 8 TB/s; fp32 MFMA 157.3 TFLOP/s, bf16 2.5 PFLOP/s for bf16 GEMMs); roof = sum over
   // launches of max(hbm, mfma)
@@ -2754,6 +2766,7 @@ int phx_profile_report(phx_ctx* ctx, char* buf, size_t cap, size_t* needed) {
   js << "}";
   std::string out = js.str();
   if (needed) *needed = out.size() + 1;
+  if (!buf) ctx->prof.report = out;
   if (buf && cap) {
     size_t c = std::min(cap - 1, out.size());
     memcpy(buf, out.data(), c);

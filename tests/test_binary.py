@@ -14,6 +14,7 @@ import re
 import shutil
 import struct
 import subprocess
+import sys
 import tempfile
 
 import pytest
@@ -92,3 +93,16 @@ def test_work_skipping_knobs_compiled_out():
     blob = open(LIB, "rb").read()
     for name in (b"PHX_SKIP_TIMING", b"PHX_SKIP_KINDS", b"PHX_NO_DROP"):
         assert name not in blob, f"{name.decode()} is read by the shipped library (built with DEBUG_KNOBS=1?)"
+
+
+@pytest.mark.parametrize("knob", ["PHX_SKIP_TIMING", "PHX_SKIP_KINDS", "PHX_NO_DROP"])
+def test_bench_refuses_work_skipping_knobs(knob):
+    """bench.py prints no headline when a knob that skips work is set (it exits before any device
+    work, so this runs on CPU); the knobs exist only in a DEBUG_KNOBS=1 build anyway."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, **{knob: "1"})
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "1", "--warmup", "0"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode != 0
+    assert knob in r.stderr and "no headline" in r.stderr
+    assert not r.stdout.strip()
