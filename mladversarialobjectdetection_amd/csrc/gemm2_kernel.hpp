@@ -284,6 +284,9 @@ __device__ __forceinline__ void g2_consume(const G2Regs<WM, TM, TN, MODE, BF>& r
 #ifndef PHX_GEMM_PF2
 #define PHX_GEMM_PF2 0
 #endif
+#ifndef PHX_G2_XCD_TILES
+#define PHX_G2_XCD_TILES 1
+#endif
 template <int WM, int TM, int TN, int MODE, int SK, int NS, bool BF, int ST>
 __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
   constexpr bool CBF = ST == 1;  // C holds bf16 activations (split-K partial slabs stay fp32)
@@ -323,8 +326,17 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
   for (int j = 0; j < TN; ++j)
     bias[j] = (!split && a.bias) ? a.bias[min(n0 + wn * TN * 32 + j * 32 + r32, a.N - 1)] : 0.f;
 
-  int tile = blockIdx.x;
-  if (tile < a.mtiles && ksteps > 0) {
+  // MODE 4 (the implicit im2col of a 3x3 conv): XCD-aware M-tile ranges — workgroup j runs on XCD
+  // j % 8 (gridDim.x a multiple of 8), and each XCD sweeps a contiguous range of M tiles, so the input
+  // rows a 3x3 gather shares between neighbouring tiles are read through one L2.  Every other mode
+  // strides the tiles over the whole grid.  Each tile's arithmetic is the same either way.
+  const bool xr = MODE == 4 && PHX_G2_XCD_TILES && gridDim.x >= 8 && (gridDim.x & 7) == 0;
+  const int tstep = xr ? (int)(gridDim.x >> 3) : (int)gridDim.x;
+  const int tper = xr ? (a.mtiles + 7) / 8 : a.mtiles;
+  const int tbeg = xr ? (int)(blockIdx.x & 7) * tper : 0;
+  const int tend = xr ? min(a.mtiles, tbeg + tper) : a.mtiles;
+  int tile = tbeg + (xr ? (int)(blockIdx.x >> 3) : (int)blockIdx.x);
+  if (tile < tend && ksteps > 0) {
     // PF2: two register sets, the loads of chunk s+2 are issued while chunk s is multiplied and
     // written to LDS at the end of step s+1 (two steps of latency cover; the HBM bytes a
     // workgroup keeps in flight double).  PF1: one set, loads one step ahead.
@@ -337,13 +349,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       tn = t;
       kn = k + 1;
       if (kn == ksteps) {
-        tn = t + gridDim.x;
+        tn = t + tstep;
         kn = 0;
       }
     };
     int t1, k1;
     advance(tile, 0, t1, k1);
-    bool h1 = t1 < a.mtiles;
+    bool h1 = t1 < tend;
     if constexpr (PF2) g2_load<WM, TM, TN, MODE, BF, ST>(rgB, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : 0) * BK, kend);
     __syncthreads();
     floatx16 acc[TM][TN];
@@ -361,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
       // the loads and the MFMAs below do not wait for them)
       if constexpr (PF2) {
         advance(t1, k1, t2, k2);
-        h2 = h1 && t2 < a.mtiles;
+        h2 = h1 && t2 < tend;
         g2_load<WM, TM, TN, MODE, BF, ST>(L, a, (h2 ? t2 : tile) * BM, n0, kbeg + (h2 ? k2 : kc) * BK, kend);
       } else {
         g2_load<WM, TM, TN, MODE, BF, ST>(L, a, (h1 ? t1 : tile) * BM, n0, kbeg + (h1 ? k1 : kc) * BK, kend);
@@ -557,7 +569,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm2(Gemm2Group<NS> grp) {
         h1 = h2;
       } else {
         advance(tile, kc, t1, k1);
-        h1 = t1 < a.mtiles;
+        h1 = t1 < tend;
       }
       return true;
     };

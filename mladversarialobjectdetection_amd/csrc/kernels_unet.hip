@@ -251,6 +251,9 @@ __global__ __launch_bounds__(256) void k_wgrad_mfma(const float* __restrict__ dy
 // columns and walks 16-row tiles (persistent).  The lane's (tap, channel) advances by 4 per step.
 // ------------------------------------------------------------------------------------------
 constexpr int kConvMaxKp = 288, kConvMaxN = 32;
+#ifndef PHX_UN_XCD_TILES
+#define PHX_UN_XCD_TILES 1
+#endif
 
 template <int NT, int MODE, bool VEC>
 __global__ __launch_bounds__(256) void k_conv3_small(const float* __restrict__ x, const float* __restrict__ Bt,
@@ -273,7 +276,17 @@ __global__ __launch_bounds__(256) void k_conv3_small(const float* __restrict__ x
   float bv[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) bv[t] = (bias && 16 * t + i16 < N) ? bias[16 * t + i16] : 0.f;
-  for (long tile = (long)blockIdx.x * 4 + wave; tile < tiles; tile += (long)gridDim.x * 4) {
+  // XCD-aware tile ranges: workgroup j runs on XCD j % 8, and each XCD owns a contiguous range of the
+  // 16-pixel tiles which its workgroups sweep together, so the input rows a 3x3 gather shares between
+  // vertically neighbouring tiles are read through one L2 (round-robin tiles put the three rows of a
+  // window on three XCDs).  Each tile's arithmetic is unchanged.  (Fewer than 8 workgroups: one range.)
+  const int G = (int)gridDim.x;
+  const bool xr = G >= 8 && PHX_UN_XCD_TILES;
+  const int xcd = xr ? (int)(blockIdx.x & 7) : 0, wi = xr ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  const int gper = xr ? (G - xcd + 7) / 8 : G;
+  const long tper = xr ? (tiles + 7) / 8 : tiles;
+  const long tbeg = (long)xcd * tper, tend = min(tiles, tbeg + tper);
+  for (long tile = tbeg + (long)wi * 4 + wave; tile < tend; tile += (long)gper * 4) {
     const long m = tile * 16 + i16;
     const bool rok = m < M;
     const long mm = rok ? m : M - 1;

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-RX='k_gemm|k_dw_|k_sep_|k_colred|k_bn_finalize|k_se_mlp|k_ew_gstats'
+RX=${PMC_RX:-'k_gemm|k_dw_|k_sep_|k_colred|k_bn_finalize|k_se_mlp|k_ew_gstats'}
 CMD=${PMC_CMD:-"python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-secondary"}
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" -d gpurun_out/pmc_fetch -o run \
   --output-format csv -- $CMD > gpurun_out/pmc_fetch.log 2>&1
