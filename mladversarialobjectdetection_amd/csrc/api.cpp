@@ -875,7 +875,7 @@ Exec& phx_ctx::exec_for(int B, int tag) {
   const long nslot = (long)B * PHX_MAX_OUT;
   E.img = E.alloc<ImgParams>(B);
   {
-    size_t bytes = nslot * sizeof(BoxPlace) + (4 + 2 * B + 3 * nslot + 2) * sizeof(int);
+    size_t bytes = nslot * sizeof(BoxPlace) + (4 + 2 * B + 3 * nslot + 2 + 8 * B + 8 * nslot) * sizeof(int);
     E.place = reinterpret_cast<BoxPlace*>(E.alloc<char>(bytes));
   }
   E.spans = E.alloc<SpanEntry>(nslot * S);

@@ -388,7 +388,7 @@ void phx_def::workspace(int B) {
   ed.rcap = (long)B * PHX_MAX_OUT * psmax * psmax * 3;
   const long nslot = (long)B * PHX_MAX_OUT;
   img = alloc<ImgParams>(B);
-  place = reinterpret_cast<BoxPlace*>(alloc<char>(nslot * sizeof(BoxPlace) + (4 + 2 * B + 3 * nslot + 2) * sizeof(int)));
+  place = reinterpret_cast<BoxPlace*>(alloc<char>(nslot * sizeof(BoxPlace) + (4 + 2 * B + 3 * nslot + 2 + 8 * B + 8 * nslot) * sizeof(int)));
   spans = alloc<SpanEntry>(nslot * S_);
   ysum = alloc<double>((size_t)B * 2 * 64);
   ymean = F((size_t)B * 2);

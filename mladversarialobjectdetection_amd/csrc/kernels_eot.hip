@@ -245,6 +245,44 @@ __global__ __launch_bounds__(256) void k_eot_spans(EotDims d, const BoxPlace* __
     tf_span(i, P.ps, d.P, &spans[(long)sl * d.span_stride + i]);
 }
 
+// XCD bands of the forward resize (k_eot_resize): band x holds row tiles x*nt/8 .. (x+1)*nt/8 - 1 of
+// every valid box (nt its row tiles).  One workgroup per image: bvpre[x][v] = band-x tiles of the
+// image's boxes before valid box v (eight exclusive scans in LDS), bcnt[x][b] = the image's total.
+constexpr int kBandMaxBoxes = 128;
+__global__ __launch_bounds__(kBandMaxBoxes) void k_eot_bands(EotDims d, const BoxPlace* __restrict__ place) {
+  const int nslot = d.B * d.maxb;
+  const int* lists = reinterpret_cast<const int*>(place + nslot);
+  const int* img_n = lists + 2;
+  const int* img_first = img_n + d.B;
+  const int* vlist = img_first + d.B;
+  int* bcnt = const_cast<int*>(vlist + 3 * nslot + 2);  // after tprefix: [8][B]
+  int* bvpre = bcnt + 8 * d.B;                          // [8][B*maxb]
+  __shared__ int sc[8][kBandMaxBoxes];
+  const int b = blockIdx.x, j = threadIdx.x, n = img_n[b], v = img_first[b] + j;
+  const int nt = j < n ? (place[vlist[v]].ps + kResizeRT - 1) / kResizeRT : 0;
+  int c[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    c[x] = (x + 1) * nt / 8 - x * nt / 8;
+    sc[x][j] = c[x];
+  }
+  __syncthreads();
+  for (int off = 1; off < kBandMaxBoxes; off <<= 1) {
+    int a[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) a[x] = j >= off ? sc[x][j - off] : 0;
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 8; ++x) sc[x][j] += a[x];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int x = 0; x < 8; ++x) {
+    if (j < n) bvpre[x * nslot + v] = sc[x][j] - c[x];
+    if (j == 0) bcnt[x * d.B + b] = n ? sc[x][n - 1] : 0;
+  }
+}
+
 void launch_eot_place(const EotDims& d, const float* boxes, const int* count, const float* params,
                       uint64_t seed, int64_t step, int gimg0, ImgParams* img, BoxPlace* place,
                       SpanEntry* spans, int* err, hipStream_t s, PlaceRule rule) {
@@ -253,6 +291,9 @@ void launch_eot_place(const EotDims& d, const float* boxes, const int* count, co
                      gimg0, img, place, lists, err, rule);
   PHX_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_eot_spans, dim3(2, d.B * d.maxb), dim3(256), 0, s, d, place, spans);
+  PHX_LAUNCH_CHECK();
+  if (d.maxb > kBandMaxBoxes) throw std::invalid_argument("eot: more than 128 box slots per image");
+  hipLaunchKernelGGL(k_eot_bands, dim3(d.B), dim3(kBandMaxBoxes), 0, s, d, place);
   PHX_LAUNCH_CHECK();
 }
 
@@ -396,6 +437,8 @@ struct ListView {
   const int* vlist;
   const int* cprefix;
   const int* tprefix;  // resize row tiles (kResizeRT rows) per valid box, prefix over vlist
+  const int* bcnt;     // [8][B] XCD-band row tiles of image b (k_eot_bands)
+  const int* bvpre;    // [8][B*maxb] XCD-band row tiles before valid box v within its image
 };
 
 __device__ __forceinline__ ListView lists_of(const EotDims& d, const BoxPlace* place) {
@@ -408,6 +451,8 @@ __device__ __forceinline__ ListView lists_of(const EotDims& d, const BoxPlace* p
   v.vlist = v.img_first + d.B;
   v.cprefix = v.vlist + d.B * d.maxb;
   v.tprefix = v.cprefix + d.B * d.maxb + 1;
+  v.bcnt = v.tprefix + d.B * d.maxb + 1;
+  v.bvpre = v.bcnt + 8 * d.B;
   return v;
 }
 
@@ -427,22 +472,55 @@ constexpr int kBoxGrid = 2048;
 // Separable, vertical pass first: a work item is (valid box, kResizeRT output rows).  Its lanes
 // run along x, so the vertical taps read whole NHWC rows of `matched` (coalesced); the
 // kResizeRT x nx x 3 intermediate stays in LDS for the horizontal pass.
-constexpr int kResizeGrid = 1280;  // 5 workgroups per CU (30 KB of LDS each)
+constexpr int kResizeGrid = 1280;  // 5 workgroups per CU (31 KB of LDS each)
 
 __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __restrict__ matched,
                                                     const BoxPlace* __restrict__ place,
                                                     const SpanEntry* __restrict__ spans,
                                                     uint64_t seed, int64_t step, int gimg0,
                                                     float* __restrict__ rstore, float amp) {
-  extern __shared__ float V[];  // [kResizeRT][nx][3]
+  extern __shared__ float V[];  // [kResizeRT][nx][3], then the band prefix [B+1]
   const ListView L = lists_of(d, place);
-  const int nv = *L.nvalid, total = L.tprefix[nv];
-  for (int item = blockIdx.x; item < total; item += gridDim.x) {
-    const int v = find_box(L.tprefix, nv, item);
+  // XCD bands: workgroup j runs on XCD x = j % 8 and takes only band x's row tiles of every box —
+  // the x-th eighth of each box's output rows, whose vertical spans read about the x-th eighth of the
+  // source rows — so an XCD's L2 holds one band of an image's matched patch for all its boxes
+  // instead of every XCD streaming whole images.  Each row tile's arithmetic is unchanged.
+  const int xb = blockIdx.x & 7;
+  int* const bx = reinterpret_cast<int*>(V + kResizeRT * d.P * 3);  // [B+1] band-x tiles before image b
+  if (threadIdx.x == 0) bx[0] = 0;
+  for (int b0 = 0; b0 < d.B; b0 += 256) {  // (chunks of 256 images, running total in bx[b0])
+    __shared__ int sx[256];
+    const int bb = b0 + (int)threadIdx.x;
+    sx[threadIdx.x] = bb < d.B ? L.bcnt[xb * d.B + bb] : 0;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {
+      const int a = threadIdx.x >= (unsigned)off ? sx[threadIdx.x - off] : 0;
+      __syncthreads();
+      sx[threadIdx.x] += a;
+      __syncthreads();
+    }
+    if (bb < d.B) bx[bb + 1] = bx[b0] + sx[threadIdx.x];
+    __syncthreads();
+  }
+  const int* bv = L.bvpre + xb * d.B * d.maxb;
+  const int total = bx[d.B];
+  for (int item = blockIdx.x >> 3; item < total; item += gridDim.x >> 3) {
+    int b = 0;
+    {
+      int lo = 0, hi = d.B - 1;  // largest image with bx[b] <= item
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (bx[mid] <= item) lo = mid; else hi = mid - 1;
+      }
+      b = lo;
+    }
+    const int local = item - bx[b];
+    const int v = L.img_first[b] + find_box(bv + L.img_first[b], L.img_n[b], local);
     const int sl = L.vlist[v];
     const BoxPlace P = place[sl];
-    const int b = sl / d.maxb, k = sl % d.maxb;
-    const int i0 = (item - L.tprefix[v]) * kResizeRT;
+    const int k = sl % d.maxb;
+    const int nt = (P.ps + kResizeRT - 1) / kResizeRT;
+    const int i0 = (xb * nt / 8 + (local - bv[v])) * kResizeRT;
     const int ni = min(kResizeRT, P.ps - i0);
     const SpanEntry* sp = spans + (long)sl * d.span_stride;
     const float scale = (float)P.ps / (float)d.P;
@@ -528,10 +606,11 @@ __global__ __launch_bounds__(256) void k_eot_resize(EotDims d, const float* __re
 // (A v2 that walked the union of a tile's row spans once per column — one load of each source row
 // for all kResizeRT output rows, weights tabulated in LDS — measured 2.42 ms against v1's 1.73 ms on
 // the first-pass flow, and was dropped.)
+static_assert(kResizeGrid % 8 == 0, "k_eot_resize: XCD bands need a multiple of 8 workgroups");
 void launch_eot_resize(const EotDims& d, const float* matched, const BoxPlace* place,
                        const SpanEntry* spans, uint64_t seed, int64_t step, int gimg0,
                        float* rstore, hipStream_t s, float noise_amp) {
-  const size_t shm = (size_t)kResizeRT * d.P * 3 * sizeof(float);
+  const size_t shm = (size_t)kResizeRT * d.P * 3 * sizeof(float) + (size_t)(d.B + 1) * sizeof(int);
   hipLaunchKernelGGL(k_eot_resize, dim3(kResizeGrid), dim3(256), shm, s, d, matched, place, spans,
                      seed, step, gimg0, rstore, noise_amp);
   PHX_LAUNCH_CHECK();
