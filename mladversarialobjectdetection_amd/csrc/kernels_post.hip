@@ -1215,22 +1215,85 @@ __global__ __launch_bounds__(256) void k_cls_scatter(
   const long prow = (long)b * L.h * L.w + pix;
   float* dx = dx_base + dx_off[l] + prow * K;
   const int N = na * nclass;
+  // the pixel's anchors that carry the image max: every keep / score load in flight at once
+  const long abase = (long)b * A + L.anchor0 + (long)pix * na;
+  constexpr int kNA = 16;
+  uint32_t win = 0;
+  if (na <= kNA) {
+    uint8_t kp[kNA];
+    float sv[kNA];
+#pragma unroll
+    for (int k = 0; k < kNA; ++k) {
+      kp[k] = keep[abase + min(k, na - 1)];
+      sv[k] = scores[abase + min(k, na - 1)];
+    }
+#pragma unroll
+    for (int k = 0; k < kNA; ++k)
+      if (k < na && (kp[k] & 1) && sv[k] == mx) win |= 1u << k;
+  } else {
+    for (int k = 0; k < na && k < 32; ++k)
+      if ((keep[abase + k] & 1) && scores[abase + k] == mx) win |= 1u << k;
+  }
+  if (!win) return;
   for (int k = 0; k < na; ++k) {
-    const long aidx = (long)b * A + L.anchor0 + (long)pix * na + k;
-    if (!(keep[aidx] & 1)) continue;
-    const float s = scores[aidx];
-    if (s != mx) continue;
+    if (!(win >> k & 1)) continue;
+    const float s = scores[abase + k];
     const float dl = ds * s * (1.0f - s);  // SigmoidGrad: y * (1 - y) * dy
     const long lg = L.cls_off + prow * (na * nclass) + (long)k * nclass;  // element offset (BF: bf16)
-    float m = ald1<BF>(cls_base, lg);
-    for (int c = 1; c < nclass; ++c) m = fmaxf(m, ald1<BF>(cls_base, lg + c));
+    // the anchor's logits: all loads issued at once (a scan that loaded them one by one, three times,
+    // was a chain of ~270 round trips), the max and its ties (a class bit mask, ascending) from registers
+    constexpr int kNC = 96;
+    uint32_t tie[kNC / 32] = {0u, 0u, 0u};
     int nt = 0;
-    for (int c = 0; c < nclass; ++c) nt += (ald1<BF>(cls_base, lg + c) == m);
+    float m;
+    if (nclass <= kNC) {
+      float v[kNC];
+#pragma unroll
+      for (int q = 0; q < kNC; ++q) v[q] = ald1<BF>(cls_base, lg + min(q, nclass - 1));
+      m = v[0];
+#pragma unroll
+      for (int q = 1; q < kNC; ++q)
+        if (q < nclass) m = fmaxf(m, v[q]);
+#pragma unroll
+      for (int q = 0; q < kNC; ++q)
+        if (q < nclass && v[q] == m) {
+          tie[q >> 5] |= 1u << (q & 31);
+          ++nt;
+        }
+    } else {
+      m = ald1<BF>(cls_base, lg);
+      for (int c = 1; c < nclass; ++c) m = fmaxf(m, ald1<BF>(cls_base, lg + c));
+      for (int c = 0; c < nclass; ++c) nt += (ald1<BF>(cls_base, lg + c) == m);
+    }
     const float dlc = dl / (float)nt;
     for (int c = 0; c < nclass; ++c) {
-      if (ald1<BF>(cls_base, lg + c) != m) continue;
+      if (nclass <= kNC) {
+        const int wd = c >> 5;
+        const uint32_t rest = (wd == 0 ? tie[0] : wd == 1 ? tie[1] : tie[2]) >> (c & 31);  // next tie at or after c
+        if (!rest) {
+          c = ((c >> 5) + 1) * 32 - 1;  // (none left in this word)
+          continue;
+        }
+        c += __builtin_ctz(rest);
+        if (c >= nclass) break;
+      } else if (ald1<BF>(cls_base, lg + c) != m) {
+        continue;
+      }
       const int col = k * nclass + c;
-      for (int j = 0; j < K; ++j) dx[j] += wpred[(long)j * N + col] * dlc;
+      // 64 kernel-column loads and 64 dx values in flight per round (one lane does this for its
+      // image's winning anchor: a dependent chain of K round trips was ~40 us of the step)
+      for (int j0 = 0; j0 < K; j0 += 64) {
+        float w[64], o[64];
+#pragma unroll
+        for (int u = 0; u < 64; ++u) {
+          const int j = min(j0 + u, K - 1);
+          w[u] = wpred[(long)j * N + col];
+          o[u] = dx[j];
+        }
+#pragma unroll
+        for (int u = 0; u < 64; ++u)
+          if (j0 + u < K) dx[j0 + u] = o[u] + w[u] * dlc;
+      }
     }
   }
 }
@@ -1241,6 +1304,7 @@ void launch_cls_scatter(const float* scores, const uint8_t* keep, const float* m
                         const float* wpred, int K, float* dx_base, const long* dx_off,
                         hipStream_t s, bool bf) {
   if (A % na) throw std::runtime_error("cls_scatter: anchors not a multiple of anchors per pixel");
+  if (na > 32) throw std::runtime_error("cls_scatter: more than 32 anchors per pixel");
   const long n = (long)B * (A / na);
   if (bf)
     hipLaunchKernelGGL(k_cls_scatter<true>, dim3(cdiv(n, 256)), dim3(256), 0, s, scores, keep, mraw, nties,
