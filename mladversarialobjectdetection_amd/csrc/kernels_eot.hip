@@ -360,7 +360,14 @@ __global__ void k_eot_ymean(EotDims d, const double* __restrict__ ysum, int chun
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.B * 2) return;
   double s = 0.0;
-  for (int k = 0; k < chunks; ++k) s += ysum[(long)i * chunks + k];
+  for (int k0 = 0; k0 < chunks; k0 += 16) {  // 16 loads in flight per round, added in order
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = ysum[(long)i * chunks + min(k0 + u, chunks - 1)];
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (k0 + u < chunks) s += v[u];
+  }
   const long npx = (i % 2) == 0 ? (long)d.P * d.P : (long)d.H * d.W;
   ymean[i] = (float)(s / (double)npx);
 }

@@ -1117,16 +1117,29 @@ __global__ void k_image_max_merge(const float* __restrict__ pm, const int* __res
   if (b >= B) return;
   float mx = -FLT_MAX;
   int mi = 0x7fffffff, cnt = 0;
-  for (int k = 0; k < S; ++k) {
-    const int o = b * S + k;
-    const int j = pi[o];
-    if (j == 0x7fffffff) continue;
-    const float v = pm[o];
-    if (mi == 0x7fffffff || v > mx) {
-      mx = v; mi = j; cnt = pc[o];
-    } else if (v == mx) {
-      mi = min(mi, j);
-      cnt += pc[o];
+  // 16 chunks' loads in flight per round, merged in chunk order (a load-use chain per chunk before)
+  for (int k0 = 0; k0 < S; k0 += 16) {
+    float pv[16];
+    int pj[16], pn[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int o = b * S + min(k0 + u, S - 1);
+      pj[u] = pi[o];
+      pv[u] = pm[o];
+      pn[u] = pc[o];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      if (k0 + u >= S) break;
+      const int j = pj[u];
+      if (j == 0x7fffffff) continue;
+      const float v = pv[u];
+      if (mi == 0x7fffffff || v > mx) {
+        mx = v; mi = j; cnt = pn[u];
+      } else if (v == mx) {
+        mi = min(mi, j);
+        cnt += pn[u];
+      }
     }
   }
   m[b] = mi == 0x7fffffff ? -FLT_MAX : mx;
