@@ -60,9 +60,15 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
       }
     }
   }
+  // fp32, training statistics: the block's 256 x CO outputs go through the LDS transpose the
+  // statistics use anyway and leave as whole 16-B runs of the block's contiguous output (a lane's own
+  // CO values were 8 stores of 16 B each at a 128-B lane stride)
+  constexpr bool kStage = STATS && !BF && CO % 4 == 0;
+  if constexpr (!kStage) {
 #pragma unroll
-  for (int c = 0; c < CO / 4; ++c)
-    ast4<BF>(y, p * CO + 4 * c, make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]));
+    for (int c = 0; c < CO / 4; ++c)
+      ast4<BF>(y, p * CO + 4 * c, make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]));
+  }
   if constexpr (STATS) {
     // statistics of the values as stored
 #pragma unroll
@@ -75,6 +81,13 @@ __global__ __launch_bounds__(256) void k_stem_fwd(const float* __restrict__ x,
     for (int c = 0; c < CO; ++c) tl[threadIdx.x][c] = acc[c];
     __syncthreads();
     const int nval = (int)min<long>(256, total - (long)blockIdx.x * 256);
+    if constexpr (kStage) {
+      float4* yb = reinterpret_cast<float4*>(y + (long)blockIdx.x * 256 * CO);
+      for (int e = threadIdx.x; e < nval * (CO / 4); e += 256) {
+        const int px = e / (CO / 4), c4 = e - px * (CO / 4);
+        yb[e] = make_float4(tl[px][4 * c4], tl[px][4 * c4 + 1], tl[px][4 * c4 + 2], tl[px][4 * c4 + 3]);
+      }
+    }
     const int t = threadIdx.x, c = t % CO, gi = t / CO;
     if (gi < G) {
       const int r0 = gi * RG, r1 = min(nval, r0 + RG);
