@@ -111,8 +111,8 @@ struct Taps {
 };
 
 // stage rows [r0, r0+rin) x cols [c0, c0+cin) of the NHWC source (sh x sw) into LDS.
-// Loads are unconditional from clamped (valid) addresses, the padding zeros are selected when the
-// values are written, and the source view's activation is a compile-time constant of the pass (a
+// Loads inside the window are unconditional from clamped (valid) addresses, the padding zeros are
+// selected when the values are written (slots of a batch past the window load nothing), and the source view's activation is a compile-time constant of the pass (a
 // per-element switch on it was a third of the instructions of the staging loop).
 template <int ACT, class Src, int U>
 __device__ __forceinline__ void dw_stage_t(float4* tile, const Src& src, int b, int sh, int sw, int C,
@@ -132,7 +132,8 @@ __device__ __forceinline__ void dw_stage_t(float4* tile, const Src& src, int b, 
       const int iy = r0 + prow, ix = c0 + pcol;
       ok[u] = pp < npx && iy >= 0 && iy < sh && ix >= 0 && ix < sw;
       const int iyc = min(max(iy, 0), sh - 1), ixc = min(max(ix, 0), sw - 1);
-      v[u] = src.load((((long)b * sh + iyc) * sw + ixc) * C + chan);
+      if (pp < npx) v[u] = src.load((((long)b * sh + iyc) * sw + ixc) * C + chan);
+      else v[u] = src.zero();  // past the window (the batch's tail): no load
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
