@@ -473,10 +473,10 @@ static int dw_lcg(int C, int k, int s, bool bwd) {
 
 // tile over an output space of (oh x ow) written by this launch
 static DwGeom dw_plan(int H, int W, int C, int Ho, int Wo, int pt, int pl, int k, int s, int rpt,
-                      bool bwd) {
+                      bool bwd, int lcg = -1) {
   DwGeom g{};
   g.H = H; g.W = W; g.C = C; g.Ho = Ho; g.Wo = Wo; g.pt = pt; g.pl = pl;
-  g.lcg = dw_lcg(C, k, s, bwd);
+  g.lcg = lcg >= 0 ? lcg : dw_lcg(C, k, s, bwd);
   const int px = 256 >> g.lcg;
   const int oh = bwd ? H : Ho, ow = bwd ? W : Wo;
   g.otw = ow < px ? ow : px;
@@ -582,6 +582,22 @@ void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, in
   DwFwdGroup<1, FuseView> grp{};
   grp.w = w;
   grp.s[0] = DwFwdSegT<FuseView>{fv, y, dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 4, false), StatSink{}};
+  // The small BiFPN levels (8x8 .. 32x32) give a few hundred workgroups or less, each walking its
+  // staging batches and four output rows in turn: there one channel quad and one output row per lane
+  // spread the same work over up to 16x the workgroups.  Each output keeps its tap order (rows, then
+  // columns), and this launch has no statistics, so the outputs are bit-identical.
+  static const bool small_on = [] {
+    const char* e = std::getenv("PHX_DW_FUSE_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  const long wgs = (long)B * grp.s[0].g.ntiles * grp.s[0].g.ncg;
+  if (small_on && wgs < 512) {
+    grp.s[0].g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 1, false, 0);
+    if (dw_lds(grp.s[0].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
+    dw_fwd_go<3, 1, 1, 1, FuseView>(grp, 1, B, false, s);
+    PHX_LAUNCH_CHECK();
+    return;
+  }
   if (dw_lds(grp.s[0].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
   dw_fwd_go<3, 1, 4, 1, FuseView>(grp, 1, B, false, s);
   PHX_LAUNCH_CHECK();
