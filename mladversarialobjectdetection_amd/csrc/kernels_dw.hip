@@ -586,12 +586,12 @@ void launch_dw_fwd_fused(const FuseView& fv, const float* w, float* y, int B, in
   // staging batches and four output rows in turn: there one channel quad and one output row per lane
   // spread the same work over up to 16x the workgroups.  Each output keeps its tap order (rows, then
   // columns), and this launch has no statistics, so the outputs are bit-identical.
-  static const bool small_on = [] {
-    const char* e = std::getenv("PHX_DW_FUSE_SMALL");
-    return !(e && e[0] == '0');
+  static const long small_below = [] {
+    const char* e = std::getenv("PHX_DW_FUSE_SMALL");  // workgroup count below which (0: off)
+    return e ? std::atol(e) : 512L;
   }();
   const long wgs = (long)B * grp.s[0].g.ntiles * grp.s[0].g.ncg;
-  if (small_on && wgs < 512) {
+  if (wgs < small_below) {
     grp.s[0].g = dw_plan(H, W, C, Ho, Wo, pt, pl, k, stride, 1, false, 0);
     if (dw_lds(grp.s[0].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
     dw_fwd_go<3, 1, 1, 1, FuseView>(grp, 1, B, false, s);
