@@ -430,31 +430,13 @@ __global__ __launch_bounds__(256) void k_dw_bwd(DwBwdGroup<NS> grp) {
 }
 
 // ---- host planning -------------------------------------------------------------------------
-// output rows per lane of a forward launch: 4 at stride 1; stride 2 defaults to 2 (PHX_DW_S2RPT=4
-// trades LDS / occupancy for less halo re-staging)
-static int dw_rpt_fwd(int stride) {
-  static int s2 = [] {
-    const char* e = std::getenv("PHX_DW_S2RPT");
-    return (e && atoi(e) == 4) ? 4 : 2;
-  }();
-  return stride == 1 ? 4 : s2;
-}
-// staging loads in flight per lane for stride-1 InX forwards (default 8: -0.035 ms/step; PHX_DW_S1SU=4)
-static int dw_s1_su() {
-  static int v = [] {
-    const char* e = std::getenv("PHX_DW_S1SU");
-    return (e && atoi(e) == 4) ? 4 : 8;
-  }();
-  return v;
-}
-// staging loads in flight per lane for stride-2 forwards (default 8: -4 % on those launches; PHX_DW_S2SU=4)
-static int dw_s2_su() {
-  static int v = [] {
-    const char* e = std::getenv("PHX_DW_S2SU");
-    return (e && atoi(e) == 4) ? 4 : 8;
-  }();
-  return v;
-}
+// output rows per lane of a forward launch: 4 at stride 1, 2 at stride 2 (4 rows at stride 2 — a
+// larger window, half the occupancy — and 1 row measured slower: DESIGN.md section 5).  Staging keeps
+// 8 loads in flight per lane for the stride-2 and stride-1 InX forwards (-0.035 ms/step and -4 % on
+// the stride-2 launches against 4; 4 and 16 measured neutral after the tail-load fix), 4 for the
+// fuse views (up to three loads each) and the data gradients (a GradX load is two float4; 8 deep
+// measured 0.1 ms/step slower).
+static int dw_rpt_fwd(int stride) { return stride == 1 ? 4 : 2; }
 
 // log2 of the float4 channel groups a workgroup owns: up to 8 (32 channels), capped at 4 (16
 // channels, twice as wide spatial tiles) for the stride-1 forwards and the 5x5 data gradients,
@@ -526,18 +508,13 @@ static void dw_fwd_go(const DwFwdGroup<NS, XV>& grp, int n, int B, bool stats, h
     lds = std::max(lds, dw_lds(grp.s[i].g, K));
   }
   dim3 grid(gx, n, B);
-  bool su8 = false;
-  if constexpr (S == 2) su8 = dw_s2_su() == 8;
-  if constexpr (S == 1 && std::is_same<XV, InX>::value) su8 = dw_s1_su() == 8;
   if constexpr (S == 2 || std::is_same<XV, InX>::value) {
-    if (su8) {
-      if (bf) dw_fwd_launch<K, S, RPT, NS, XV, 8, true>(grid, lds, grp, stats, s);
-      else dw_fwd_launch<K, S, RPT, NS, XV, 8, false>(grid, lds, grp, stats, s);
-      return;
-    }
+    if (bf) dw_fwd_launch<K, S, RPT, NS, XV, 8, true>(grid, lds, grp, stats, s);
+    else dw_fwd_launch<K, S, RPT, NS, XV, 8, false>(grid, lds, grp, stats, s);
+  } else {
+    if (bf) dw_fwd_launch<K, S, RPT, NS, XV, 4, true>(grid, lds, grp, stats, s);
+    else dw_fwd_launch<K, S, RPT, NS, XV, 4, false>(grid, lds, grp, stats, s);
   }
-  if (bf) dw_fwd_launch<K, S, RPT, NS, XV, 4, true>(grid, lds, grp, stats, s);
-  else dw_fwd_launch<K, S, RPT, NS, XV, 4, false>(grid, lds, grp, stats, s);
 }
 
 template <int NS, class XV>
@@ -545,12 +522,9 @@ static void dw_fwd_dispatch(const DwFwdGroup<NS, XV>& grp, int n, int B, bool st
                             hipStream_t s) {
   for (int i = 0; i < n; ++i)
     if (dw_lds(grp.s[i].g, k) > 160 * 1024) throw std::runtime_error("dw: LDS window too large");
-  const bool r4 = dw_rpt_fwd(2) == 4;
   if (k == 3 && stride == 1) dw_fwd_go<3, 1, 4, NS, XV>(grp, n, B, stats, s);
-  else if (k == 3 && stride == 2 && r4) dw_fwd_go<3, 2, 4, NS, XV>(grp, n, B, stats, s);
   else if (k == 3 && stride == 2) dw_fwd_go<3, 2, 2, NS, XV>(grp, n, B, stats, s);
   else if (k == 5 && stride == 1) dw_fwd_go<5, 1, 4, NS, XV>(grp, n, B, stats, s);
-  else if (k == 5 && stride == 2 && r4) dw_fwd_go<5, 2, 4, NS, XV>(grp, n, B, stats, s);
   else if (k == 5 && stride == 2) dw_fwd_go<5, 2, 2, NS, XV>(grp, n, B, stats, s);
   else throw std::invalid_argument("dw: unsupported kernel/stride");
   PHX_LAUNCH_CHECK();
@@ -630,19 +604,8 @@ static void dw_bwd_go(const DwBwdGroup<NS>& grp, int n, int B, bool gsums, hipSt
     lds = std::max(lds, dw_lds(grp.s[i].g, K));
   }
   dim3 grid(gx, n, B);
-  static const bool su8 = [] {
-    const char* e = std::getenv("PHX_DW_BSU");
-    return e && atoi(e) == 8;
-  }();
   // the BN input y of every member shares the context's storage type
   const bool ybf = (grp.s[0].gv.y && grp.s[0].gv.ybf) || (gsums && grp.s[0].gs.ybf);
-  if (su8 && !ybf) {  // (A/B knob; the bf16-storage variant stages 4 deep)
-    if (gsums)
-      hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS, 8>), grid, dim3(256), lds, s, grp);
-    else
-      hipLaunchKernelGGL((k_dw_bwd<K, S, 4, false, NS, 8>), grid, dim3(256), lds, s, grp);
-    return;
-  }
   if (ybf) {
     if (gsums)
       hipLaunchKernelGGL((k_dw_bwd<K, S, 4, true, NS, 4, true>), grid, dim3(256), lds, s, grp);
