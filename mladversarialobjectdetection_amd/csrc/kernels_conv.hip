@@ -448,6 +448,93 @@ __device__ __forceinline__ void gemm_load(GemmFrag<NT>& f, const InX& Ax, const 
                                : make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
+// The 16-wide (NT = 1) path's loads run PHX_GEMM_PD chunks ahead: the raw loads (A or da / y, B)
+// land in a ring of registers and the view is applied just before the chunk's MFMAs, so a wave
+// keeps PD chunks of HBM reads in flight instead of one.  The view's per-channel parameters of the
+// workgroup's K slice sit in an LDS table (filled once per workgroup) rather than in the ring.
+// Same arithmetic in the same order as gemm_load: bit-identical.
+#ifndef PHX_GEMM_PD
+#define PHX_GEMM_PD 2
+#endif
+constexpr int kGemmTab = 256;  // K-slice length the channel table holds (longer slices: PD = 1)
+
+template <int MODE>
+struct GemmRaw1 {
+  float4 a[2];
+  float4 y[2];   // MODE 3: the BN input y
+  float4 rs[2];  // MODE 2: the SE row scale
+  float4 b;
+};
+
+template <int MODE, int ST>
+__device__ __forceinline__ void gemm_raw1(GemmRaw1<MODE>& f, const InX& Ax, const GradX& Gx,
+                                          const float* __restrict__ Bt, int K, int klim, int kk,
+                                          const int* rows, const bool* rok, int col, bool cok,
+                                          const float* __restrict__ rowscale, int rows_per_img) {
+  const bool kok = kk < klim;
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    if (rok[mt] && kok) {
+      const long e = (long)rows[mt] * K + kk;
+      if (MODE == 3) {
+        f.a[mt] = *reinterpret_cast<const float4*>(Gx.da + e);
+        f.y[mt] = ald4<ST == 2>(Gx.y, e);
+      } else {
+        f.a[mt] = ald4<ST == 1>(Ax.p, e);
+        if (MODE == 2)
+          f.rs[mt] = *reinterpret_cast<const float4*>(rowscale + (long)(rows[mt] / rows_per_img) * K + kk);
+      }
+    }
+  }
+  f.b = (cok && kok) ? *reinterpret_cast<const float4*>(Bt + (long)col * K + kk) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+// tab: parameter p of slice channel kl at tab[p * kGemmTab + kl] (MODE 1/2: mu, sc, be; MODE 3:
+// mu, rstd, sc, be, mdz, mdzx)
+template <int MODE>
+__device__ __forceinline__ void gemm_apply1(GemmFrag<1>& f, const GemmRaw1<MODE>& r, const InX& Ax,
+                                            const GradX& Gx, const float* tab, int kl, bool kok,
+                                            const bool* rok) {
+  Chan4 ck;
+  GChan4 gk;
+  if (kok) {
+    if (MODE == 1 || MODE == 2) {
+      const float4 m = *reinterpret_cast<const float4*>(tab + kl);
+      const float4 s = *reinterpret_cast<const float4*>(tab + kGemmTab + kl);
+      const float4 b = *reinterpret_cast<const float4*>(tab + 2 * kGemmTab + kl);
+      ck.mu[0] = m.x; ck.mu[1] = m.y; ck.mu[2] = m.z; ck.mu[3] = m.w;
+      ck.sc[0] = s.x; ck.sc[1] = s.y; ck.sc[2] = s.z; ck.sc[3] = s.w;
+      ck.be[0] = b.x; ck.be[1] = b.y; ck.be[2] = b.z; ck.be[3] = b.w;
+    }
+    if (MODE == 3) {
+      gk.mu = *reinterpret_cast<const float4*>(tab + kl);
+      gk.rs = *reinterpret_cast<const float4*>(tab + kGemmTab + kl);
+      gk.sc = *reinterpret_cast<const float4*>(tab + 2 * kGemmTab + kl);
+      gk.be = *reinterpret_cast<const float4*>(tab + 3 * kGemmTab + kl);
+      gk.m1 = *reinterpret_cast<const float4*>(tab + 4 * kGemmTab + kl);
+      gk.m2 = *reinterpret_cast<const float4*>(tab + 5 * kGemmTab + kl);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt) {
+    if (rok[mt] && kok) {
+      float4 v = r.a[mt];
+      if (MODE == 3) {
+        v = gx_apply4(Gx, gk, v, r.y[mt]);
+      } else {
+        if (MODE == 1 || MODE == 2) v = inx_apply4(Ax, ck, v);
+        if (MODE == 2) {
+          v.x *= r.rs[mt].x; v.y *= r.rs[mt].y; v.z *= r.rs[mt].z; v.w *= r.rs[mt].w;
+        }
+      }
+      f.a[mt] = v;
+    } else {
+      f.a[mt] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  f.b[0] = r.b;
+}
+
 // Column statistics of a block's C tile for the BN that consumes it (StatSink).  Lane (q, r) of a
 // wave holds rows 4q+j (j < 4) of column r in each of its 2 x NT accumulator tiles: a column's 32
 // wave rows sit in 8 registers of 4 lanes (r, r+16, r+32, r+48).  Two passes over the registers
@@ -607,6 +694,59 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
     cok[nt] = cols[nt] < N;
   }
 
+  constexpr int PD = NT == 1 ? PHX_GEMM_PD : 1;
+  bool done = false;
+  if constexpr (PD > 1) {
+    constexpr int NP = MODE == 3 ? 6 : (MODE == 1 || MODE == 2) ? 3 : 0;
+    __shared__ __attribute__((aligned(16))) float ctab[NP > 0 ? NP * kGemmTab : 1];
+    const int klen = kend - kbeg;  // uniform over the workgroup
+    if (NP == 0 || klen <= kGemmTab) {
+      done = true;
+      if constexpr (NP > 0) {
+        for (int i = threadIdx.x; i < NP * klen; i += 256) {
+          const int pp = i / klen, kl = i - pp * klen;
+          const float* src;
+          if constexpr (MODE == 3) {
+            src = pp == 0 ? Gx.mu : pp == 1 ? Gx.rstd : pp == 2 ? Gx.sc : pp == 3 ? Gx.be : pp == 4 ? Gx.mdz : Gx.mdzx;
+          } else {
+            src = pp == 0 ? Ax.mu : pp == 1 ? Ax.sc : Ax.be;
+          }
+          ctab[pp * kGemmTab + kl] = src[kbeg + kl];
+        }
+      }
+      GemmRaw1<MODE> rr[PD];
+#pragma unroll
+      for (int i = 0; i < PD; ++i) {
+        const int kc = kbeg + 16 * i;
+        if (kc < kend)
+          gemm_raw1<MODE, ST>(rr[i], Ax, Gx, Bt, K, kend, kc + 4 * q, rows, rok, cols[0], cok[0], rowscale,
+                              rows_per_img);
+      }
+      if constexpr (NP > 0) __syncthreads();
+      for (int k0 = kbeg; k0 < kend; k0 += 16 * PD) {
+#pragma unroll
+        for (int i = 0; i < PD; ++i) {
+          const int kc = k0 + 16 * i;
+          if (kc < kend) {
+            GemmFrag<1> f;
+            gemm_apply1<MODE>(f, rr[i], Ax, Gx, ctab, kc - kbeg + 4 * q, kc + 4 * q < kend, rok);
+            const int kn = kc + 16 * PD;
+            if (kn < kend)
+              gemm_raw1<MODE, ST>(rr[i], Ax, Gx, Bt, K, kend, kn + 4 * q, rows, rok, cols[0], cok[0], rowscale,
+                                  rows_per_img);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+              acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[mt].x, f.b[0].x, acc[mt][0], 0, 0, 0);
+              acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[mt].y, f.b[0].y, acc[mt][0], 0, 0, 0);
+              acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[mt].z, f.b[0].z, acc[mt][0], 0, 0, 0);
+              acc[mt][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(f.a[mt].w, f.b[0].w, acc[mt][0], 0, 0, 0);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (!done) {
   GemmFrag<NT> cur, nxt;
   if (kbeg < kend)
     gemm_load<NT, MODE, ST>(cur, Ax, Gx, Bt, K, kend, kbeg + 4 * q, rows, rok, cols, cok, rowscale,
@@ -627,6 +767,7 @@ __global__ __launch_bounds__(256) void k_gemm(InX Ax, GradX Gx, const float* __r
       }
     }
     if (more) cur = nxt;
+  }
   }
 
   constexpr bool CBF = ST == 1;
